@@ -1,0 +1,128 @@
+/*
+ * mpo.h -- C ABI of libmpo.so, the MI355X (gfx950) engine for mpi_opt's
+ * trial-evaluation hot path.
+ *
+ * Conventions:
+ *   - every function returns int status (MPO_OK = 0); the message of the last
+ *     failure on the calling thread is mpo_last_error();
+ *   - no exceptions cross the ABI;
+ *   - the CALLER owns every device buffer (e.g. torch tensors' data_ptr());
+ *     the library never allocates device memory: scratch comes from a caller
+ *     workspace whose size is returned by the matching *_ws_bytes query;
+ *   - every launching call takes an explicit hipStream_t (passed as void*) and
+ *     only enqueues work: no host synchronisation, no allocation, so callers
+ *     may capture any sequence of calls into a hipGraph;
+ *   - not re-entrant per stream; thread-safe across streams/devices.
+ *
+ * Row-major layouts throughout: matrix A(i,j) lives at A[i*ld + j].
+ *
+ * Each entry point cites the reference interface it replaces
+ * (/root/reference/<file>:<line>).
+ */
+#ifndef MPO_H_
+#define MPO_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPO_OK 0
+#define MPO_EINVAL 1      /* bad argument (shape, null pointer, workspace too small) */
+#define MPO_EHIP 2        /* HIP runtime error (launch failure, ...) */
+#define MPO_ENOTSUP 3     /* shape outside what the kernels support */
+
+/* Acquisition selection flags for mpo_gp_acq_score (skopt acquisition.py). */
+#define MPO_ACQ_EI 1u     /* value = -EI  (skopt minimises -EI)  */
+#define MPO_ACQ_PI 2u     /* value = -PI                         */
+#define MPO_ACQ_LCB 4u    /* value = mu - kappa * sd             */
+
+#define MPO_TOPK_MAX 8
+
+const char* mpo_last_error(void);
+/* Library version string, e.g. "mpo 0.1 gfx950". */
+const char* mpo_version(void);
+
+/* ------------------------------------------------------------------------
+ * GP surrogate ("ask" hot path).
+ * Replaces skopt.Optimizer.tell/ask's GaussianProcessRegressor fit tail and
+ * _gaussian_acquisition, reached from Coordinator.fit (coordinator.py:63-79)
+ * and Coordinator.ask (coordinator.py:46-50).
+ * ---------------------------------------------------------------------- */
+
+/* A prepared GP posterior (device pointers into the prepare workspace). */
+typedef struct MpoGpModel {
+    int32_t n;             /* observations                          */
+    int32_t d;             /* dimensions                            */
+    int32_t dp;            /* padded dimensions (4, 8, 16 or 32)    */
+    int32_t np16;          /* n rounded up to 16                    */
+    double amp;            /* ConstantKernel value                  */
+    double y_mean;         /* normalize_y mean                      */
+    double y_std;          /* normalize_y std                       */
+    const double* xs;      /* [n][dp]  observations / length_scale  */
+    const double* ls;      /* [dp]     length scales (pad = 1)      */
+    const double* alpha;   /* [n]      K^-1 y_norm                  */
+    const double* wfrag;   /* packed L^-1 MFMA B-fragments          */
+    const double* L;       /* [n][n]   lower Cholesky factor        */
+    const double* W;       /* [n][n]   L^-1 (lower)                 */
+    int32_t* info;         /* device int: 0 ok, j+1 = chol failed at column j */
+} MpoGpModel;
+
+/* K(i,j) = amp * Matern52(|X_i/ls - X_j/ls|) + (i==j ? diag_add : 0).
+ * X: [n][d] device, ls: [d] device, K: [n][ldk] device. */
+int mpo_gp_kernel_matrix(const double* X, int n, int d, const double* ls, double amp,
+                         double diag_add, double* K, int ldk, void* stream);
+
+/* In-place lower Cholesky A = L L^T (upper triangle left untouched).
+ * info (device int) = 0 on success, j+1 if the pivot of column j is <= 0. */
+int mpo_chol_f64(double* A, int n, int lda, int32_t* info, void* stream);
+
+/* Triangular solve with the lower factor L: trans=0 solves L X = B,
+ * trans=1 solves L^T X = B; B [n][ldb] (nrhs columns) is overwritten with X. */
+int mpo_trsm_f64(const double* L, int n, int lda, double* B, int nrhs, int ldb,
+                 int trans, void* stream);
+
+/* Workspace bytes for mpo_gp_prepare. */
+size_t mpo_gp_prepare_ws_bytes(int n, int d);
+
+/* Build a GP posterior from observations and fitted hyper-parameters:
+ *   xs = X/ls;  K = amp*Matern52 + (noise + 1e-10 jitter) I;  L = chol(K);
+ *   W = L^-1;  alpha = L^-T L^-1 y_norm;  pack W for the scoring kernel.
+ * X [n][d], y_norm [n], ls [d]: device.  `model` (host struct) receives
+ * device pointers into `ws`, which must stay alive while the model is used.
+ * Replaces GaussianProcessRegressor.fit's tail (sklearn _gpr.py:345-365) and
+ * skopt's post-fit K_inv_ (skopt learning/gaussian_process/gpr.py). */
+int mpo_gp_prepare(const double* X, const double* y_norm, int n, int d, const double* ls,
+                   double amp, double noise, double y_mean, double y_std,
+                   MpoGpModel* model, void* ws, size_t ws_bytes, void* stream);
+
+/* Workspace bytes for mpo_gp_acq_score over m candidates. */
+size_t mpo_gp_score_ws_bytes(const MpoGpModel* model, int64_t m, int k);
+
+/* Score m candidates (transformed space, [m][d] device) under the posterior:
+ *   mu, sd           : posterior mean / std (skopt predict(return_std=True));
+ *   vals[a*m + i]    : minimised acquisition value for each flag a in
+ *                      {EI, PI, LCB} order (rows for unset flags untouched);
+ *   topk_idx/val[a*k + r] : the k smallest values of acquisition a, ties to the
+ *                      lowest index (np.argsort(values)[:k] / np.argmin).
+ * Any of mu, sd, vals may be NULL (not written).  topk arrays are device.
+ * Replaces skopt _gaussian_acquisition + gaussian_ei/pi/lcb over the
+ * n_points candidate sample, and the argsort/argmin that picks L-BFGS starts. */
+int mpo_gp_acq_score(const MpoGpModel* model, const double* cand, int64_t m,
+                     double y_opt, double xi, double kappa, unsigned flags,
+                     double* mu, double* sd, double* vals, int k,
+                     int64_t* topk_idx, double* topk_val,
+                     void* ws, size_t ws_bytes, void* stream);
+
+/* EI-only convenience (SURVEY §8b signature family): writes mu, sd, ei (= +EI)
+ * and argmax (device int64, lowest index among maximal EI). */
+int mpo_gp_ei_score(const MpoGpModel* model, const double* cand, int64_t m,
+                    double y_opt, double xi, double* mu, double* sd, double* ei,
+                    int64_t* argmax, void* ws, size_t ws_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPO_H_ */

@@ -1,0 +1,95 @@
+"""ctypes binding of ``libmpo.so`` (the C ABI declared in ``include/mpo.h``).
+
+The product path has no CPU fallback: if the library is missing or a HIP call
+fails, :func:`lib` / :func:`check` raise.  Device buffers are torch tensors;
+only their ``data_ptr()`` and the raw HIP stream handle cross the ABI.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmpo.so")
+
+MPO_OK = 0
+MPO_ACQ_EI = 1
+MPO_ACQ_PI = 2
+MPO_ACQ_LCB = 4
+MPO_TOPK_MAX = 8
+ACQ_FLAGS = {"EI": MPO_ACQ_EI, "PI": MPO_ACQ_PI, "LCB": MPO_ACQ_LCB}
+ACQ_ROW = {"EI": 0, "PI": 1, "LCB": 2}
+
+
+class MpoError(RuntimeError):
+    pass
+
+
+class MpoGpModel(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_int32), ("d", ctypes.c_int32), ("dp", ctypes.c_int32), ("np16", ctypes.c_int32),
+        ("amp", ctypes.c_double), ("y_mean", ctypes.c_double), ("y_std", ctypes.c_double),
+        ("xs", ctypes.c_void_p), ("ls", ctypes.c_void_p), ("alpha", ctypes.c_void_p),
+        ("wfrag", ctypes.c_void_p), ("L", ctypes.c_void_p), ("W", ctypes.c_void_p),
+        ("info", ctypes.c_void_p),
+    ]
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_I64 = ctypes.c_int64
+_D = ctypes.c_double
+_SZ = ctypes.c_size_t
+_U = ctypes.c_uint
+
+# name -> (restype, argtypes); keep in the order of include/mpo.h
+SIGNATURES = {
+    "mpo_last_error": (ctypes.c_char_p, []),
+    "mpo_version": (ctypes.c_char_p, []),
+    "mpo_gp_kernel_matrix": (_I, [_P, _I, _I, _P, _D, _D, _P, _I, _P]),
+    "mpo_chol_f64": (_I, [_P, _I, _I, _P, _P]),
+    "mpo_trsm_f64": (_I, [_P, _I, _I, _P, _I, _I, _I, _P]),
+    "mpo_gp_prepare_ws_bytes": (_SZ, [_I, _I]),
+    "mpo_gp_prepare": (_I, [_P, _P, _I, _I, _P, _D, _D, _D, _D, ctypes.POINTER(MpoGpModel), _P, _SZ, _P]),
+    "mpo_gp_score_ws_bytes": (_SZ, [ctypes.POINTER(MpoGpModel), _I64, _I]),
+    "mpo_gp_acq_score": (_I, [ctypes.POINTER(MpoGpModel), _P, _I64, _D, _D, _D, _U, _P, _P, _P, _I, _P, _P,
+                              _P, _SZ, _P]),
+    "mpo_gp_ei_score": (_I, [ctypes.POINTER(MpoGpModel), _P, _I64, _D, _D, _P, _P, _P, _P, _P, _SZ, _P]),
+}
+
+_LIB = None
+
+
+def lib():
+    """Load libmpo.so (once).  Raises if it has not been built."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise MpoError(f"{LIB_PATH} is missing: build it with `make -C mpi_opt_amd/csrc` "
+                           "or `python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback)")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = handle
+    return _LIB
+
+
+def check(rc: int, what: str = "mpo call"):
+    if rc != MPO_OK:
+        msg = lib().mpo_last_error()
+        raise MpoError(f"{what} failed (status {rc}): {msg.decode() if msg else ''}")
+
+
+def ptr(t) -> int:
+    """Device pointer of a torch tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    import torch
+
+    return torch.cuda.current_stream(device).cuda_stream

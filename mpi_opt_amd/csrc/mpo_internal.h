@@ -1,0 +1,63 @@
+// Internal helpers shared by the libmpo.so translation units (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/mpo.h"
+
+namespace mpo {
+
+// Thread-local message of the last failure (returned by mpo_last_error()).
+void set_error(const char* fmt, ...);
+void clear_error();
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Carve consecutive 256-B aligned regions out of a caller workspace.
+struct WsCarver {
+    char* base;
+    size_t used = 0;
+    explicit WsCarver(void* p) : base(static_cast<char*>(p)) {}
+    template <class T>
+    T* take(size_t count) {
+        used = align_up(used, 256);
+        T* p = base ? reinterpret_cast<T*>(base + used) : nullptr;
+        used += count * sizeof(T);
+        return p;
+    }
+};
+
+}  // namespace mpo
+
+#define MPO_CHECK_ARG(cond, ...)              \
+    do {                                      \
+        if (!(cond)) {                        \
+            ::mpo::set_error(__VA_ARGS__);    \
+            return MPO_EINVAL;                \
+        }                                     \
+    } while (0)
+
+#define MPO_HIP(call)                                                             \
+    do {                                                                          \
+        hipError_t e_ = (call);                                                   \
+        if (e_ != hipSuccess) {                                                   \
+            ::mpo::set_error("%s:%d %s: %s", __FILE__, __LINE__, #call,           \
+                             hipGetErrorString(e_));                              \
+            return MPO_EHIP;                                                      \
+        }                                                                         \
+    } while (0)
+
+#define MPO_LAUNCH_CHECK() MPO_HIP(hipGetLastError())
+
+#define MPO_GUARD_BEGIN try {
+#define MPO_GUARD_END                                         \
+    }                                                         \
+    catch (...) {                                             \
+        ::mpo::set_error("unexpected C++ exception");         \
+        return MPO_EHIP;                                      \
+    }
