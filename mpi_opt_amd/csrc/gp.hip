@@ -404,31 +404,35 @@ __global__ __launch_bounds__(256) void gp_score_kernel(ScoreArgs a) {
     }
 }
 
-// Merge per-block top-k lists of one acquisition (blockIdx.x = acquisition).
+// Merge per-block top-k lists.  grid = (G, 3): block g of acquisition y merges
+// the partial lists [g*chunk, min((g+1)*chunk, nparts)) and writes one list.
+// Stage 1 writes the partial layout [(g*3 + acq)*k + r]; the final stage (G = 1)
+// writes out[acq*out_stride + r] with index -1 for missing entries.
 __global__ __launch_bounds__(256) void topk_merge_kernel(const long long* __restrict__ part_idx,
                                                          const double* __restrict__ part_val,
-                                                         int nblocks, int k, unsigned flags,
+                                                         int nparts, int chunk, int k, unsigned flags,
                                                          long long* __restrict__ out_idx,
                                                          double* __restrict__ out_val,
-                                                         int out_stride) {
+                                                         int out_stride, int final_stage) {
     __shared__ double lv[256 * MPO_TOPK_MAX];
     __shared__ long long li[256 * MPO_TOPK_MAX];
-    const int acq = blockIdx.x;
+    const int acq = blockIdx.y;
     if (!(flags & (1u << acq))) return;
     const int tid = threadIdx.x;
     const double inf = __builtin_huge_val();
     const long long big = 0x7fffffffffffffffLL;
+    const int p0 = blockIdx.x * chunk;
+    const int p1 = min(nparts, p0 + chunk);
     double bv[MPO_TOPK_MAX];
     long long bi[MPO_TOPK_MAX];
 #pragma unroll
     for (int r = 0; r < MPO_TOPK_MAX; ++r) { bv[r] = inf; bi[r] = big; }
-    const long long total = (long long)nblocks * k;
+    const long long total = (long long)(p1 - p0) * k;
     for (long long e = tid; e < total; e += 256) {
-        const long long blk = e / k, r = e % k;
+        const long long blk = p0 + e / k, r = e % k;
         const size_t off = ((size_t)blk * 3 + acq) * k + r;
         double v = part_val[off];
         long long i = part_idx[off];
-        // insertion into the sorted local list (static indices only)
 #pragma unroll
         for (int s = 0; s < MPO_TOPK_MAX; ++s) {
             if (s < k && lex_less(v, i, bv[s], bi[s])) {
@@ -465,8 +469,13 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(const long long* __rest
             for (int q = 0; q < 4; ++q) if (q == src) ptr[q]++;
         }
         if (tid == 0) {
-            out_val[acq * out_stride + r] = gv;
-            out_idx[acq * out_stride + r] = gi == big ? -1 : gi;
+            if (final_stage) {
+                out_val[acq * out_stride + r] = gv;
+                out_idx[acq * out_stride + r] = gi == big ? -1 : gi;
+            } else {
+                out_val[((size_t)blockIdx.x * 3 + acq) * k + r] = gv;
+                out_idx[((size_t)blockIdx.x * 3 + acq) * k + r] = gi;
+            }
         }
     }
 }
@@ -485,6 +494,7 @@ inline int pad_dims(int d) {
 }
 
 constexpr size_t kMaxLds = 160 * 1024;
+constexpr int kMergeGroups = 256;  // stage-1 top-k merge groups
 
 size_t score_lds_bytes(int bm, int dp, int np16) {
     const int S = 4 * (64 / bm);
@@ -671,6 +681,8 @@ size_t mpo_gp_score_ws_bytes(const MpoGpModel* model, int64_t m, int k) {
     mpo::WsCarver c(nullptr);
     c.take<long long>((size_t)nblocks * 3 * kk);
     c.take<double>((size_t)nblocks * 3 * kk);
+    c.take<long long>((size_t)kMergeGroups * 3 * kk);
+    c.take<double>((size_t)kMergeGroups * 3 * kk);
     c.take<long long>(3 * kk);
     c.take<double>(3 * kk);
     return c.used + 256;
@@ -696,6 +708,8 @@ static int gp_score_impl(const MpoGpModel* model, const double* cand, int64_t m,
     const int kk = std::max(k, 1);
     long long* part_idx = c.take<long long>((size_t)nblocks * 3 * kk);
     double* part_val = c.take<double>((size_t)nblocks * 3 * kk);
+    long long* mid_idx = c.take<long long>((size_t)kMergeGroups * 3 * kk);
+    double* mid_val = c.take<double>((size_t)kMergeGroups * 3 * kk);
 
     ScoreArgs a;
     a.n = model->n;
@@ -725,8 +739,14 @@ static int gp_score_impl(const MpoGpModel* model, const double* cand, int64_t m,
     const size_t lds = score_lds_bytes(bm, model->dp, model->np16);
     MPO_HIP(launch_score_dp(model->dp, bm, a, nblocks, lds, s));
     if (k > 0) {
-        hipLaunchKernelGGL(topk_merge_kernel, dim3(3), dim3(256), 0, s, part_idx, part_val, nblocks, k, flags,
-                           reinterpret_cast<long long*>(topk_idx), topk_val, k);
+        // stage 1: G groups of ~64 block-lists each; stage 2: one list
+        const int chunk = std::max(64, (nblocks + kMergeGroups - 1) / kMergeGroups);
+        const int G = (nblocks + chunk - 1) / chunk;
+        hipLaunchKernelGGL(topk_merge_kernel, dim3(G, 3), dim3(256), 0, s, part_idx, part_val, nblocks, chunk, k,
+                           flags, mid_idx, mid_val, k, 0);
+        MPO_LAUNCH_CHECK();
+        hipLaunchKernelGGL(topk_merge_kernel, dim3(1, 3), dim3(256), 0, s, mid_idx, mid_val, G, G, k, flags,
+                           reinterpret_cast<long long*>(topk_idx), topk_val, k, 1);
         MPO_LAUNCH_CHECK();
     }
     return MPO_OK;
@@ -753,6 +773,8 @@ int mpo_gp_ei_score(const MpoGpModel* model, const double* cand, int64_t m, doub
     const int64_t nblocks = (m + bm - 1) / bm;
     c.take<long long>((size_t)nblocks * 3);
     c.take<double>((size_t)nblocks * 3);
+    c.take<long long>((size_t)kMergeGroups * 3);
+    c.take<double>((size_t)kMergeGroups * 3);
     long long* tidx = c.take<long long>(3);
     double* tval = c.take<double>(3);
     hipStream_t s = static_cast<hipStream_t>(stream);
