@@ -122,6 +122,64 @@ int mpo_gp_ei_score(const MpoGpModel* model, const double* cand, int64_t m,
                     double y_opt, double xi, double* mu, double* sd, double* ei,
                     int64_t* argmax, void* ws, size_t ws_bytes, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Population training of ragged MNIST-CNN trials.
+ * Replaces ProcessBlock.train_model -> mpi_learn MPIKFoldManager.train()
+ * (process_block.py:71-96) for test_mnist (mpiLAPI.py:138-176): every member
+ * is one (trial, fold) pair; all members step together on one GPU.
+ * ---------------------------------------------------------------------- */
+
+/* One population member: the test_mnist hyper-parameters (option3:127-131)
+ * plus the optimizer/dropout settings that the device table carries per trial. */
+typedef struct MpoCnnSpec {
+    int32_t nb_filters;   /* F      Integer(10, 50)  */
+    int32_t kernel_size;  /* k      Integer(2, 10)   */
+    int32_t pool_size;    /* p      Integer(2, 10)   */
+    int32_t dense;        /* dense  Integer(50, 200) */
+    float lr;             /* Adam learning rate (reference: 1e-3)            */
+    float dropout;        /* dropout rate (reference: 0.25, mpiLAPI.py:151)   */
+    uint32_t seed;        /* dropout stream seed                             */
+    int32_t reserved;
+} MpoCnnSpec;
+
+typedef struct MpoPopSizes {
+    int64_t n_params;     /* floats in the parameter arena (also grads, adam m, adam v) */
+    int64_t act_floats;   /* floats in the activation arena                              */
+    int64_t table_bytes;  /* device bytes for the member table + work lists              */
+    int32_t n_members;
+    int32_t batch;
+} MpoPopSizes;
+
+/* Plan a population (host only: layouts, ragged work lists).  *handle owns host
+ * memory only; release with mpo_pop_destroy. */
+int mpo_pop_create(const MpoCnnSpec* specs, int n_members, int batch, void** handle);
+int mpo_pop_destroy(void* handle);
+int mpo_pop_sizes(const void* handle, MpoPopSizes* out);
+/* offsets[9] (floats into the parameter arena) of member's
+ * w1 (k,k,1,F), b1, w2 (k,k,F,F), b2, w3 (s*s*F, dense), b3, w4 (dense,10), b4, end.
+ * Keras weight shapes and order (Conv2D kernel (kh,kw,cin,cout), Dense (in,out)). */
+int mpo_pop_param_layout(const void* handle, int member, int64_t* offsets);
+/* Bind caller-owned device arenas (zero-initialised by the caller) and upload
+ * the work tables (async on `stream`). */
+int mpo_pop_bind(void* handle, float* params, float* grads, float* adam_m, float* adam_v, float* act,
+                 void* tables, void* stream);
+/* One training step of every member on batch rows [row0, row0+batch) of its
+ * sample order: sample = order[member*order_stride + row0 + b] indexes x
+ * [n][784] f32 and labels [n] i32 (the k-fold split is this index gather).
+ * step = global step counter (dropout stream; Adam t = step + 1).
+ * loss_out[member] = mean Keras binary_crossentropy of the batch. */
+int mpo_pop_train_step(void* handle, const float* x, const int32_t* labels, const int32_t* order,
+                       int64_t order_stride, int64_t row0, int32_t step, float* loss_out, void* stream);
+/* Validation forward (no dropout) of one batch: loss_sum[member] += sum of
+ * per-sample losses, correct[member] += argmax hits. */
+int mpo_pop_eval_step(void* handle, const float* x, const int32_t* labels, const int32_t* order,
+                      int64_t order_stride, int64_t row0, float* loss_sum, int32_t* correct, void* stream);
+
+/* k-fold index gather: out[r][:] = X[idx[r]][:] (the fold split
+ * that mpi_learn does with per-fold communicators becomes an index gather). */
+int mpo_kfold_gather(const float* X, const int32_t* idx, int64_t rows, int row_elems, float* out,
+                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

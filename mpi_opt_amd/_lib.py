@@ -35,6 +35,17 @@ class MpoGpModel(ctypes.Structure):
     ]
 
 
+class MpoCnnSpec(ctypes.Structure):
+    _fields_ = [("nb_filters", ctypes.c_int32), ("kernel_size", ctypes.c_int32), ("pool_size", ctypes.c_int32),
+                ("dense", ctypes.c_int32), ("lr", ctypes.c_float), ("dropout", ctypes.c_float),
+                ("seed", ctypes.c_uint32), ("reserved", ctypes.c_int32)]
+
+
+class MpoPopSizes(ctypes.Structure):
+    _fields_ = [("n_params", ctypes.c_int64), ("act_floats", ctypes.c_int64), ("table_bytes", ctypes.c_int64),
+                ("n_members", ctypes.c_int32), ("batch", ctypes.c_int32)]
+
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _I64 = ctypes.c_int64
@@ -55,6 +66,14 @@ SIGNATURES = {
     "mpo_gp_acq_score": (_I, [ctypes.POINTER(MpoGpModel), _P, _I64, _D, _D, _D, _U, _P, _P, _P, _I, _P, _P,
                               _P, _SZ, _P]),
     "mpo_gp_ei_score": (_I, [ctypes.POINTER(MpoGpModel), _P, _I64, _D, _D, _P, _P, _P, _P, _P, _SZ, _P]),
+    "mpo_pop_create": (_I, [ctypes.POINTER(MpoCnnSpec), _I, _I, ctypes.POINTER(ctypes.c_void_p)]),
+    "mpo_pop_destroy": (_I, [_P]),
+    "mpo_pop_sizes": (_I, [_P, ctypes.POINTER(MpoPopSizes)]),
+    "mpo_pop_param_layout": (_I, [_P, _I, ctypes.POINTER(ctypes.c_int64)]),
+    "mpo_pop_bind": (_I, [_P, _P, _P, _P, _P, _P, _P, _P]),
+    "mpo_pop_train_step": (_I, [_P, _P, _P, _P, _I64, _I64, ctypes.c_int32, _P, _P]),
+    "mpo_pop_eval_step": (_I, [_P, _P, _P, _P, _I64, _I64, _P, _P, _P]),
+    "mpo_kfold_gather": (_I, [_P, _P, _I64, _I, _P, _P]),
 }
 
 _LIB = None

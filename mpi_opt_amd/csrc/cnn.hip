@@ -1,0 +1,1150 @@
+// cnn.hip -- population training of ragged MNIST-CNN trials on gfx950 (MI355X).
+//
+// Hot path T2-T6 of SURVEY §8a: replaces ProcessBlock.train_model ->
+// mpi_learn MPIKFoldManager (/root/reference/process_block.py:71-96) for the
+// test_mnist model (/root/reference/mpiLAPI.py:138-176).  Every member of the
+// population is one (trial, fold) pair with its own widths (F, k, p, dense),
+// learning rate, dropout rate and dropout seed; one launch per op covers every
+// member through a host-built work list (grouped / ragged launches).
+//
+// Per training step (all members, batch B):
+//   conv_img<CONV1_FWD>   x[order] (k-fold index gather) -> a1 = relu(conv1)
+//   conv_img<CONV2_FWD>   a1 -> a2 = relu(conv2)
+//   pool_fwd              a2 -> pd = dropout(maxpool(a2)), argmax
+//   dense<D1_FWD>         pd -> h = relu(pd w3 + b3), hd = dropout(h)
+//   dense<D2_FWD>         hd -> z3 = hd w4 + b4
+//   softmax_bce           z3 -> loss, dz3
+//   dense<D2_WGRAD/DGRAD> dw4;  dh = dz3 w4^T * mask * (h>0)
+//   dense<D1_WGRAD/DGRAD> dw3;  dp = dh w3^T * mask
+//   pool_bwd              dp -> dz2 = unpool(dp) * (a2>0)
+//   flip_w2               w2 -> w2t (rotated, in/out swapped: dgrad weights)
+//   conv_img<CONV2_DGRAD> dz2 (virtually zero-padded) -> dz1 = conv(dz2, w2t) * (a1>0)
+//   conv_wgrad<CONV2>     a1, dz2 -> dw2 partial slabs (per sample group)
+//   conv_wgrad<CONV1>     x[order], dz1 -> dw1 partial slabs
+//   wgrad_reduce, colsum  slabs -> dw1, dw2; bias grads
+//   adam                  per-member lr, Keras-form Adam
+//
+// The convolutions are image-stationary implicit GEMMs: a workgroup stages
+// the input rows it needs for one sample (and one output row chunk) into LDS
+// once, and every MFMA A-fragment is an LDS gather at (pixel base + tap
+// offset) -- no im2col buffer, no k^2 re-reads from L2.  Arithmetic is f32 on
+// v_mfma_f32_16x16x4_f32 (exact f32, the reference's precision).
+
+#include "mpo_internal.h"
+
+#include <algorithm>
+#include <cmath>
+#include <memory>
+#include <vector>
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kImg = 28;
+constexpr int kClasses = 10;
+constexpr float kBceEps = 1e-7f;
+
+// ---- device member descriptor (mirrors the host plan) ----------------------
+struct Member {
+    int F, k, p, dense;
+    int H1, H2, s, K1;
+    float lr, rate, inv_keep;
+    unsigned seed;
+    unsigned drop_thr;  // keep iff (hash >> 8) >= drop_thr
+    int nt;             // ceil(F / 16)
+    int g1, g2;         // wgrad sample groups (conv1, conv2)
+    // parameter arena offsets (floats); the same offsets index grads / adam m / v
+    long long w1, b1, w2, b2, w3, b3, w4, b4, pend;
+    // activation arena offsets (floats)
+    long long a1, a2, pd, am, h, hd, z3, dz3, dh, dp, dz2, dz1, w2t, wp1, wp2;
+};
+
+struct ConvItem { int member, b, y0, R; };
+struct WgItem { int member, mg, b0, b1, group, R; };
+struct GemmItem { int member, m0, n0, pad; };
+struct MItem { int member, aux; };
+
+enum ConvOp { CONV1_FWD = 0, CONV2_FWD = 1, CONV2_DGRAD = 2 };
+enum WgOp { WG_CONV1 = 0, WG_CONV2 = 1 };
+enum DenseOp { D1_FWD = 0, D2_FWD = 1, D2_WGRAD = 2, D2_DGRAD = 3, D1_WGRAD = 4, D1_DGRAD = 5 };
+
+struct StepArgs {
+    const Member* mem;
+    const float* params;
+    float* grads;
+    float* act;
+    const float* x;          // [n_samples][784]
+    const int* labels;       // [n_samples]
+    const int* order;        // sample order per member
+    long long order_stride;  // entries per member row
+    long long row0;          // first row of this batch in the order
+    int B;
+    int step;                // dropout stream position
+    int train;               // 1 = training (dropout on), 0 = eval
+    float* loss_out;         // [n_members] mean batch loss (train)
+    float* loss_sum;         // [n_members] running loss sum (eval)
+    int* correct;            // [n_members] running correct count (eval)
+};
+
+// ---- dropout counter hash (identical in oracle/cnn.py) ---------------------
+__device__ __forceinline__ unsigned lowbias32(unsigned x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+__device__ __forceinline__ unsigned drop_base(unsigned seed, int step, int layer) {
+    unsigned b = lowbias32(seed ^ (unsigned)(layer * 0x9E3779B9u));
+    return lowbias32(b ^ (unsigned)step);
+}
+
+__device__ __forceinline__ bool drop_keep(unsigned base, unsigned elem, unsigned thr) {
+    return (lowbias32(elem ^ base) >> 8) >= thr;
+}
+
+__host__ __device__ constexpr inline int odd_stride(int c) { return (c == 1) ? 1 : (c | 1); }
+
+// ============================================================================
+// Image-stationary implicit-GEMM convolution (forward and input-gradient).
+//   out[b][y][x][n] = sum_{ky,kx,c} in_pad[b][y+ky][x+kx][c] * W[(ky*k+kx)*Cin+c][n]
+// One workgroup = (member, sample b, output rows [y0, y0+R)); M = R*Ho <= 128
+// output pixels = 8 m-tiles of 16 spread over 4 waves; N = F in NT tiles of 16.
+// ============================================================================
+constexpr int kConvBK = 64;  // B rows per LDS chunk
+
+__host__ __device__ constexpr inline int bn_stride(int nt) { return nt * 16 + ((nt & 1) ? 0 : 16); }
+
+template <int OP, int NT>
+__global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvItem* __restrict__ items) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const ConvItem it = items[blockIdx.x];
+    const Member& mb = a.mem[it.member];
+    const int k = mb.k, F = mb.F;
+    int Hin, Cin, pad, Ho;
+    const float* in;
+    const float* W;
+    const float* bias = nullptr;
+    float* out;
+    const float* relu_mask = nullptr;
+    if (OP == CONV1_FWD) {
+        Hin = kImg; Cin = 1; pad = 0; Ho = mb.H1;
+        const int sidx = a.order[(long long)it.member * a.order_stride + a.row0 + it.b];
+        in = a.x + (long long)sidx * (kImg * kImg);
+        W = a.params + mb.w1; bias = a.params + mb.b1;
+        out = a.act + mb.a1 + (long long)it.b * Ho * Ho * F;
+    } else if (OP == CONV2_FWD) {
+        Hin = mb.H1; Cin = F; pad = 0; Ho = mb.H2;
+        in = a.act + mb.a1 + (long long)it.b * Hin * Hin * F;
+        W = a.params + mb.w2; bias = a.params + mb.b2;
+        out = a.act + mb.a2 + (long long)it.b * Ho * Ho * F;
+    } else {
+        Hin = mb.H2; Cin = F; pad = k - 1; Ho = mb.H1;
+        in = a.act + mb.dz2 + (long long)it.b * Hin * Hin * F;
+        W = a.act + mb.w2t;
+        out = a.act + mb.dz1 + (long long)it.b * Ho * Ho * F;
+        relu_mask = a.act + mb.a1 + (long long)it.b * Ho * Ho * F;
+    }
+    const int N = F;
+    const int K = k * k * Cin;
+    const int Kp = (K + 3) & ~3;
+    const int Wp = Hin + 2 * pad;
+    const int Fp = odd_stride(Cin);
+    const int rows = it.R + k - 1;
+    const int M = it.R * Ho;
+    constexpr int BNs = bn_stride(NT);
+
+    float* img = smem;                                   // [rows][Wp][Fp]
+    const int img_elems = rows * Wp * Fp;
+    int* koff = reinterpret_cast<int*>(smem + ((img_elems + 3) & ~3));   // [Kp]
+    float* bs = smem + ((img_elems + 3) & ~3) + ((Kp + 3) & ~3);          // [kConvBK][BNs]
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+    // ---- stage the (virtually padded) input rows
+    for (int e = tid; e < img_elems; e += 256) img[e] = 0.f;
+    __syncthreads();
+    for (int r = 0; r < rows; ++r) {
+        const int gy = it.y0 + r - pad;
+        if (gy < 0 || gy >= Hin) continue;
+        const float* src = in + (long long)gy * Hin * Cin;
+        float* dst = img + (r * Wp + pad) * Fp;
+        for (int e = tid; e < Hin * Cin; e += 256) {
+            const int gx = e / Cin, c = e - gx * Cin;
+            dst[gx * Fp + c] = src[e];
+        }
+    }
+    for (int kk = tid; kk < Kp; kk += 256) {
+        int off = 0;
+        if (kk < K) {
+            const int kc = k * Cin;
+            const int ky = kk / kc, rem = kk - ky * kc;
+            const int kx = rem / Cin, c = rem - kx * Cin;
+            off = (ky * Wp + kx) * Fp + c;
+        }
+        koff[kk] = off;
+    }
+
+    // ---- per-lane pixel bases of this wave's m-tiles
+    const int mtiles = (M + 15) >> 4;
+    int pb[2];
+    bool has[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int mt = wave + 4 * i;
+        has[i] = mt < mtiles;
+        const int m = mt * 16 + (lane & 15);
+        int base = 0;
+        if (m < M) {
+            const int y = m / Ho, xx = m - y * Ho;
+            base = (y * Wp + xx) * Fp;
+        }
+        pb[i] = base;
+    }
+
+    f32x4 acc[2][NT];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int krow = lane >> 4, kcol = lane & 15;
+    for (int kc0 = 0; kc0 < Kp; kc0 += kConvBK) {
+        __syncthreads();
+        const int kn = min(kConvBK, Kp - kc0);
+        for (int e = tid; e < kConvBK * NT * 16; e += 256) {
+            const int r = e / (NT * 16), c = e - r * (NT * 16);
+            const int kk = kc0 + r;
+            bs[r * BNs + c] = (kk < K && c < N) ? W[(long long)kk * N + c] : 0.f;
+        }
+        __syncthreads();
+        if (!has[0]) continue;
+        for (int ks = 0; ks < kn; ks += 4) {
+            const int ko = koff[kc0 + ks + krow];
+            float bf[NT];
+#pragma unroll
+            for (int j = 0; j < NT; ++j) bf[j] = bs[(ks + krow) * BNs + j * 16 + kcol];
+            const float a0 = img[pb[0] + ko];
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bf[j], acc[0][j], 0, 0, 0);
+            if (has[1]) {
+                const float a1 = img[pb[1] + ko];
+#pragma unroll
+                for (int j = 0; j < NT; ++j) acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bf[j], acc[1][j], 0, 0, 0);
+            }
+        }
+    }
+
+    // ---- epilogue: C/D map col = lane & 15, row = (lane >> 4) * 4 + r
+    const long long pix0 = (long long)it.y0 * Ho;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        if (!has[i]) continue;
+        const int mt = wave + 4 * i;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int n = j * 16 + kcol;
+            if (n >= N) continue;
+            const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = mt * 16 + krow * 4 + r;
+                if (m >= M) continue;
+                const long long o = (pix0 + m) * N + n;
+                float v = acc[i][j][r];
+                if (OP == CONV2_DGRAD) {
+                    v = relu_mask[o] > 0.f ? v : 0.f;
+                } else {
+                    v = fmaxf(v + bv, 0.f);
+                }
+                out[o] = v;
+            }
+        }
+    }
+}
+
+// ============================================================================
+// Weight gradient: dW[(ky,kx,c)][n] = sum_{b,y,x} in[b][y+ky][x+kx][c] * dout[b][y][x][n]
+// One workgroup = (member, 128 rows of (ky,kx,c), a group of samples); loops
+// over its samples and output row chunks, staging input rows + dout rows in LDS.
+// Writes one partial slab per sample group (reduced deterministically later).
+// ============================================================================
+__host__ __device__ constexpr inline int dout_stride(int nt) { return bn_stride(nt); }
+
+template <int OP, int NT>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(StepArgs a, const WgItem* __restrict__ items) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const WgItem it = items[blockIdx.x];
+    const Member& mb = a.mem[it.member];
+    const int k = mb.k, F = mb.F;
+    int Hin, Cin, Ho;
+    long long dout_off, part_off;
+    if (OP == WG_CONV1) {
+        Hin = kImg; Cin = 1; Ho = mb.H1; dout_off = mb.dz1; part_off = mb.wp1;
+    } else {
+        Hin = mb.H1; Cin = F; Ho = mb.H2; dout_off = mb.dz2; part_off = mb.wp2;
+    }
+    const int N = F;
+    const int Kw = k * k * Cin;  // output rows
+    const int Fp = odd_stride(Cin);
+    constexpr int Fq = NT * 16 + ((NT & 1) ? 0 : 16);
+    const int R = it.R;
+    const int P = R * Ho;
+    const int P4 = (P + 3) & ~3;
+    const int rows = R + k - 1;
+    float* img = smem;                                   // [rows][Hin][Fp]
+    const int img_elems = rows * Hin * Fp;
+    float* dl = smem + ((img_elems + 3) & ~3);            // [P4][Fq]
+    int* poff = reinterpret_cast<int*>(dl + P4 * Fq);     // [P4]
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int krow = lane >> 4, kcol = lane & 15;
+
+    int toff[2];
+    bool has[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int mt = wave + 4 * i;
+        const int m0 = it.mg * 128 + mt * 16;
+        has[i] = m0 < Kw;
+        const int m = m0 + (lane & 15);
+        int off = 0;
+        if (m < Kw) {
+            const int kc = k * Cin;
+            const int ky = m / kc, rem = m - ky * kc;
+            const int kx = rem / Cin, c = rem - kx * Cin;
+            off = (ky * Hin + kx) * Fp + c;
+        }
+        toff[i] = off;
+    }
+    f32x4 acc[2][NT];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int b = it.b0; b < it.b1; ++b) {
+        const float* in;
+        if (OP == WG_CONV1) {
+            const int sidx = a.order[(long long)it.member * a.order_stride + a.row0 + b];
+            in = a.x + (long long)sidx * (kImg * kImg);
+        } else {
+            in = a.act + mb.a1 + (long long)b * Hin * Hin * Cin;
+        }
+        const float* dout = a.act + dout_off + (long long)b * Ho * Ho * N;
+        for (int y0 = 0; y0 < Ho; y0 += R) {
+            const int rcnt = min(R, Ho - y0);
+            const int pcnt = rcnt * Ho;
+            __syncthreads();
+            // input rows y0 .. y0 + rcnt + k - 2 (always inside the image)
+            const int irows = rcnt + k - 1;
+            const float* src = in + (long long)y0 * Hin * Cin;
+            if (Cin == Fp) {
+                for (int e = tid; e < irows * Hin * Cin; e += 256) img[e] = src[e];
+            } else {
+                for (int e = tid; e < irows * Hin * Cin; e += 256) {
+                    const int px = e / Cin, c = e - px * Cin;
+                    img[px * Fp + c] = src[e];
+                }
+            }
+            const float* dsrc = dout + (long long)y0 * Ho * N;
+            for (int e = tid; e < P4 * Fq; e += 256) {
+                const int px = e / Fq, c = e - px * Fq;
+                dl[e] = (px < pcnt && c < N) ? dsrc[px * N + c] : 0.f;
+            }
+            for (int px = tid; px < P4; px += 256) {
+                int off = 0;
+                if (px < pcnt) {
+                    const int y = px / Ho, xx = px - y * Ho;
+                    off = (y * Hin + xx) * Fp;
+                }
+                poff[px] = off;
+            }
+            __syncthreads();
+            if (!has[0]) continue;
+            const int pc4 = (pcnt + 3) & ~3;
+            for (int ks = 0; ks < pc4; ks += 4) {
+                const int po = poff[ks + krow];
+                float bf[NT];
+#pragma unroll
+                for (int j = 0; j < NT; ++j) bf[j] = dl[(ks + krow) * Fq + j * 16 + kcol];
+                const float a0 = img[toff[0] + po];
+#pragma unroll
+                for (int j = 0; j < NT; ++j) acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bf[j], acc[0][j], 0, 0, 0);
+                if (has[1]) {
+                    const float a1 = img[toff[1] + po];
+#pragma unroll
+                    for (int j = 0; j < NT; ++j) acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bf[j], acc[1][j], 0, 0, 0);
+                }
+            }
+        }
+    }
+    float* part = a.act + part_off + (long long)it.group * Kw * N;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        if (!has[i]) continue;
+        const int mt = wave + 4 * i;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int n = j * 16 + kcol;
+            if (n >= N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = it.mg * 128 + mt * 16 + krow * 4 + r;
+                if (m < Kw) part[(long long)m * N + n] = acc[i][j][r];
+            }
+        }
+    }
+}
+
+// Sum the per-group partial slabs (fixed order) into the weight gradients.
+__global__ void wgrad_reduce_kernel(StepArgs a, const MItem* __restrict__ items, int per_block) {
+    const MItem it = items[blockIdx.y];
+    const Member& mb = a.mem[it.member];
+    const int conv = it.aux;  // 0 conv1, 1 conv2
+    const long long S = conv ? (long long)mb.k * mb.k * mb.F * mb.F : (long long)mb.k * mb.k * mb.F;
+    const int G = conv ? mb.g2 : mb.g1;
+    const float* part = a.act + (conv ? mb.wp2 : mb.wp1);
+    float* g = a.grads + (conv ? mb.w2 : mb.w1);
+    for (long long i = (long long)blockIdx.x * per_block + threadIdx.x; i < S && i < (long long)(blockIdx.x + 1) * per_block;
+         i += blockDim.x) {
+        float s = 0.f;
+        for (int q = 0; q < G; ++q) s += part[q * S + i];
+        g[i] = s;
+    }
+}
+
+// w2t[(ky', kx', f)][c] = w2[(k-1-ky', k-1-kx', c)][f]: weights of the input-gradient conv.
+__global__ void flip_w2_kernel(StepArgs a, const MItem* __restrict__ items) {
+    const Member& mb = a.mem[items[blockIdx.y].member];
+    const int k = mb.k, F = mb.F;
+    const long long S = (long long)k * k * F * F;
+    const float* w2 = a.params + mb.w2;
+    float* w2t = a.act + mb.w2t;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < S; i += (long long)gridDim.x * blockDim.x) {
+        const int c = i % F;
+        const long long r = i / F;
+        const int f = r % F;
+        const int tap = r / F;
+        const int ky = tap / k, kx = tap % k;
+        const int src_tap = (k - 1 - ky) * k + (k - 1 - kx);
+        w2t[i] = w2[((long long)src_tap * F + c) * F + f];
+    }
+}
+
+// ============================================================================
+// Max-pool (floor mode, stride p) + dropout, and its backward.
+// ============================================================================
+__global__ __launch_bounds__(256) void pool_fwd_kernel(StepArgs a, const MItem* __restrict__ items) {
+    const MItem it = items[blockIdx.x];
+    const Member& mb = a.mem[it.member];
+    const int b = it.aux;
+    const int F = mb.F, p = mb.p, s = mb.s, H2 = mb.H2, K1 = mb.K1;
+    const float* a2 = a.act + mb.a2 + (long long)b * H2 * H2 * F;
+    float* pd = a.act + mb.pd + (long long)b * K1;
+    unsigned char* am = reinterpret_cast<unsigned char*>(a.act + mb.am) + (long long)b * K1;
+    const unsigned base = drop_base(mb.seed, a.step, 0);
+    for (int j = threadIdx.x; j < K1; j += blockDim.x) {
+        const int f = j % F, q = j / F;
+        const int px = q % s, py = q / s;
+        float best = -__builtin_huge_valf();
+        int arg = 0;
+        for (int dy = 0; dy < p; ++dy)
+            for (int dx = 0; dx < p; ++dx) {
+                const float v = a2[((py * p + dy) * H2 + (px * p + dx)) * F + f];
+                if (v > best) { best = v; arg = dy * p + dx; }
+            }
+        float o = best;
+        if (a.train) o = drop_keep(base, (unsigned)(b * K1 + j), mb.drop_thr) ? best * mb.inv_keep : 0.f;
+        pd[j] = o;
+        am[j] = (unsigned char)arg;
+    }
+}
+
+__global__ __launch_bounds__(256) void pool_bwd_kernel(StepArgs a, const MItem* __restrict__ items) {
+    const MItem it = items[blockIdx.x];
+    const Member& mb = a.mem[it.member];
+    const int b = it.aux;
+    const int F = mb.F, p = mb.p, s = mb.s, H2 = mb.H2, K1 = mb.K1;
+    const float* a2 = a.act + mb.a2 + (long long)b * H2 * H2 * F;
+    const float* dp = a.act + mb.dp + (long long)b * K1;
+    const unsigned char* am = reinterpret_cast<const unsigned char*>(a.act + mb.am) + (long long)b * K1;
+    float* dz2 = a.act + mb.dz2 + (long long)b * H2 * H2 * F;
+    const int n = H2 * H2 * F;
+    for (int e = threadIdx.x; e < n; e += blockDim.x) {
+        const int f = e % F, q = e / F;
+        const int x = q % H2, y = q / H2;
+        const int py = y / p, px = x / p;
+        float v = 0.f;
+        if (py < s && px < s) {
+            const int j = (py * s + px) * F + f;
+            if (am[j] == (y - py * p) * p + (x - px * p)) v = dp[j];
+        }
+        dz2[e] = a2[e] > 0.f ? v : 0.f;
+    }
+}
+
+// ============================================================================
+// Grouped dense GEMMs (MFMA f32 16x16x4), 64x64 tiles, 4 waves as 2x2 of 32x32.
+// ============================================================================
+template <int OP>
+struct DenseGeom {
+    int M, N, K;
+    const float* A; long long sai, sak;
+    const float* Bm; long long sbk, sbj;
+    float* C; long long ldc;
+};
+
+template <int OP>
+__device__ __forceinline__ DenseGeom<OP> dense_geom(const StepArgs& a, const Member& mb) {
+    DenseGeom<OP> g;
+    const int B = a.B;
+    const int K1 = mb.K1, D = mb.dense;
+    if (OP == D1_FWD) {
+        g.M = B; g.N = D; g.K = K1;
+        g.A = a.act + mb.pd; g.sai = K1; g.sak = 1;
+        g.Bm = a.params + mb.w3; g.sbk = D; g.sbj = 1;
+        g.C = a.act + mb.h; g.ldc = D;
+    } else if (OP == D2_FWD) {
+        g.M = B; g.N = kClasses; g.K = D;
+        g.A = a.act + mb.hd; g.sai = D; g.sak = 1;
+        g.Bm = a.params + mb.w4; g.sbk = kClasses; g.sbj = 1;
+        g.C = a.act + mb.z3; g.ldc = kClasses;
+    } else if (OP == D2_WGRAD) {
+        g.M = D; g.N = kClasses; g.K = B;
+        g.A = a.act + mb.hd; g.sai = 1; g.sak = D;
+        g.Bm = a.act + mb.dz3; g.sbk = kClasses; g.sbj = 1;
+        g.C = a.grads + mb.w4; g.ldc = kClasses;
+    } else if (OP == D2_DGRAD) {
+        g.M = B; g.N = D; g.K = kClasses;
+        g.A = a.act + mb.dz3; g.sai = kClasses; g.sak = 1;
+        g.Bm = a.params + mb.w4; g.sbk = 1; g.sbj = kClasses;
+        g.C = a.act + mb.dh; g.ldc = D;
+    } else if (OP == D1_WGRAD) {
+        g.M = K1; g.N = D; g.K = B;
+        g.A = a.act + mb.pd; g.sai = 1; g.sak = K1;
+        g.Bm = a.act + mb.dh; g.sbk = D; g.sbj = 1;
+        g.C = a.grads + mb.w3; g.ldc = D;
+    } else {  // D1_DGRAD
+        g.M = B; g.N = K1; g.K = D;
+        g.A = a.act + mb.dh; g.sai = D; g.sak = 1;
+        g.Bm = a.params + mb.w3; g.sbk = 1; g.sbj = D;
+        g.C = a.act + mb.dp; g.ldc = K1;
+    }
+    return g;
+}
+
+template <int OP>
+__global__ __launch_bounds__(256) void dense_kernel(StepArgs a, const GemmItem* __restrict__ items) {
+    constexpr int BM = 64, BN = 64, BK = 16;
+    __shared__ float As[BK][BM + 1];
+    __shared__ float Bs[BK][BN + 16];
+    const GemmItem it = items[blockIdx.x];
+    const Member& mb = a.mem[it.member];
+    const DenseGeom<OP> g = dense_geom<OP>(a, mb);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int krow = lane >> 4, kcol = lane & 15;
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < g.K; k0 += BK) {
+        __syncthreads();
+        for (int e = tid; e < BM * BK; e += 256) {
+            int i, kk;
+            if (g.sak == 1) { i = e / BK; kk = e % BK; } else { kk = e / BM; i = e % BM; }
+            const int gi = it.m0 + i, gk = k0 + kk;
+            As[kk][i] = (gi < g.M && gk < g.K) ? g.A[gi * g.sai + gk * g.sak] : 0.f;
+        }
+        for (int e = tid; e < BN * BK; e += 256) {
+            int j, kk;
+            if (g.sbj == 1) { kk = e / BN; j = e % BN; } else { j = e / BK; kk = e % BK; }
+            const int gj = it.n0 + j, gk = k0 + kk;
+            Bs[kk][j] = (gj < g.N && gk < g.K) ? g.Bm[gk * g.sbk + gj * g.sbj] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int ks = 0; ks < BK; ks += 4) {
+            float af[2], bf[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) af[i] = As[ks + krow][wr * 32 + i * 16 + kcol];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) bf[j] = Bs[ks + krow][wc * 32 + j * 16 + kcol];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    const unsigned base1 = drop_base(mb.seed, a.step, 1);
+    const unsigned base0 = drop_base(mb.seed, a.step, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gi = it.m0 + wr * 32 + i * 16 + krow * 4 + r;
+                const int gj = it.n0 + wc * 32 + j * 16 + kcol;
+                if (gi >= g.M || gj >= g.N) continue;
+                float v = acc[i][j][r];
+                const long long o = (long long)gi * g.ldc + gj;
+                if (OP == D1_FWD) {
+                    v = fmaxf(v + a.params[mb.b3 + gj], 0.f);
+                    g.C[o] = v;
+                    float hd = v;
+                    if (a.train) hd = drop_keep(base1, (unsigned)o, mb.drop_thr) ? v * mb.inv_keep : 0.f;
+                    a.act[mb.hd + o] = hd;
+                } else if (OP == D2_FWD) {
+                    g.C[o] = v + a.params[mb.b4 + gj];
+                } else if (OP == D2_DGRAD) {
+                    const bool keep = drop_keep(base1, (unsigned)o, mb.drop_thr);
+                    g.C[o] = (keep && a.act[mb.h + o] > 0.f) ? v * mb.inv_keep : 0.f;
+                } else if (OP == D1_DGRAD) {
+                    g.C[o] = drop_keep(base0, (unsigned)o, mb.drop_thr) ? v * mb.inv_keep : 0.f;
+                } else {
+                    g.C[o] = v;
+                }
+            }
+}
+
+// ============================================================================
+// softmax + Keras binary_crossentropy (clip 1e-7, mean over classes and batch)
+// One workgroup per member; one thread per sample row.
+// ============================================================================
+__global__ __launch_bounds__(256) void softmax_bce_kernel(StepArgs a, const MItem* __restrict__ items) {
+    __shared__ float red[256];
+    __shared__ int redc[256];
+    const int member = items[blockIdx.x].member;
+    const Member& mb = a.mem[member];
+    const int B = a.B;
+    const int tid = threadIdx.x;
+    float lsum = 0.f;
+    int corr = 0;
+    for (int b = tid; b < B; b += 256) {
+        const float* z = a.act + mb.z3 + (long long)b * kClasses;
+        const int sidx = a.order[(long long)member * a.order_stride + a.row0 + b];
+        const int y = a.labels[sidx];
+        float zm = z[0];
+        int am = 0;
+#pragma unroll
+        for (int c = 1; c < kClasses; ++c) if (z[c] > zm) { zm = z[c]; am = c; }
+        float e[kClasses], s = 0.f;
+#pragma unroll
+        for (int c = 0; c < kClasses; ++c) { e[c] = expf(z[c] - zm); s += e[c]; }
+        float l = 0.f, gdot = 0.f, gp[kClasses], pr[kClasses];
+#pragma unroll
+        for (int c = 0; c < kClasses; ++c) {
+            const float p = e[c] / s;
+            pr[c] = p;
+            const float t = (c == y) ? 1.f : 0.f;
+            const float pc = fminf(fmaxf(p, kBceEps), 1.f - kBceEps);
+            l += -(t * logf(pc) + (1.f - t) * logf(1.f - pc));
+            const bool inside = p > kBceEps && p < 1.f - kBceEps;
+            gp[c] = inside ? (pc - t) / (pc * (1.f - pc)) / (float)(kClasses * B) : 0.f;
+            gdot += gp[c] * p;
+        }
+        lsum += l / (float)kClasses;
+        corr += (am == y);
+        if (a.train) {
+            float* dz = a.act + mb.dz3 + (long long)b * kClasses;
+#pragma unroll
+            for (int c = 0; c < kClasses; ++c) dz[c] = pr[c] * (gp[c] - gdot);
+        }
+    }
+    red[tid] = lsum;
+    redc[tid] = corr;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (tid < s) { red[tid] += red[tid + s]; redc[tid] += redc[tid + s]; }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        if (a.train) {
+            a.loss_out[member] = red[0] / (float)B;
+        } else {
+            a.loss_sum[member] += red[0];
+            a.correct[member] += redc[0];
+        }
+    }
+}
+
+// ============================================================================
+// Bias gradients: column sums of dz1 / dz2 / dh / dz3 (deterministic).
+// item.aux: 0 b1 (dz1, B*H1^2 x F), 1 b2 (dz2, B*H2^2 x F), 2 b3 (dh, B x dense), 3 b4 (dz3, B x 10)
+// ============================================================================
+__global__ __launch_bounds__(256) void colsum_kernel(StepArgs a, const MItem* __restrict__ items) {
+    __shared__ float red[4][64];
+    const MItem it = items[blockIdx.x];
+    const Member& mb = a.mem[it.member];
+    const int B = a.B;
+    const float* src;
+    long long rows;
+    int N;
+    float* dst;
+    if (it.aux == 0) { src = a.act + mb.dz1; rows = (long long)B * mb.H1 * mb.H1; N = mb.F; dst = a.grads + mb.b1; }
+    else if (it.aux == 1) { src = a.act + mb.dz2; rows = (long long)B * mb.H2 * mb.H2; N = mb.F; dst = a.grads + mb.b2; }
+    else if (it.aux == 2) { src = a.act + mb.dh; rows = B; N = mb.dense; dst = a.grads + mb.b3; }
+    else { src = a.act + mb.dz3; rows = B; N = kClasses; dst = a.grads + mb.b4; }
+    const int tid = threadIdx.x;
+    const int rl = tid >> 6, cl = tid & 63;
+    for (int c0 = 0; c0 < N; c0 += 64) {
+        const int c = c0 + cl;
+        float s = 0.f;
+        if (c < N)
+            for (long long r = rl; r < rows; r += 4) s += src[r * N + c];
+        red[rl][cl] = s;
+        __syncthreads();
+        if (rl == 0 && c < N) dst[c] = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+        __syncthreads();
+    }
+}
+
+// ============================================================================
+// Adam (Keras form): lr_t = lr sqrt(1-b2^t)/(1-b1^t); p -= lr_t m / (sqrt(v) + eps)
+// ============================================================================
+__global__ __launch_bounds__(256) void adam_kernel(StepArgs a, const MItem* __restrict__ items, float* __restrict__ params,
+                                                   float* __restrict__ mo, float* __restrict__ vo, int t, float b1,
+                                                   float b2, float eps, int chunk) {
+    const MItem it = items[blockIdx.x];
+    const Member& mb = a.mem[it.member];
+    const double corr = sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t));
+    const float lr_t = (float)(mb.lr * corr);
+    const long long begin = mb.w1 + (long long)it.aux * chunk;
+    const long long end = min(mb.pend, begin + chunk);
+    for (long long i = begin + threadIdx.x; i < end; i += blockDim.x) {
+        const float g = a.grads[i];
+        const float m = b1 * mo[i] + (1.f - b1) * g;
+        const float v = b2 * vo[i] + (1.f - b2) * g * g;
+        mo[i] = m;
+        vo[i] = v;
+        params[i] -= lr_t * m / (sqrtf(v) + eps);
+    }
+}
+
+__global__ void kfold_gather_kernel(const float* __restrict__ X, const int* __restrict__ idx, long long rows, int row_elems,
+                                    float* __restrict__ out) {
+    const long long r = blockIdx.y + (long long)blockIdx.z * 65535;
+    if (r >= rows) return;
+    const float* src = X + (long long)idx[r] * row_elems;
+    float* dst = out + r * row_elems;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < row_elems; e += gridDim.x * blockDim.x) dst[e] = src[e];
+}
+
+// ============================================================================
+// Host-side plan
+// ============================================================================
+struct Bucketed {
+    // items sorted by NT (1..4); [begin, end) per NT
+    int begin[5] = {0, 0, 0, 0, 0}, end[5] = {0, 0, 0, 0, 0};
+};
+
+struct Plan {
+    int n = 0, B = 0;
+    std::vector<Member> mem;
+    long long n_params = 0, act_floats = 0;
+    std::vector<ConvItem> conv1, conv2, dgrad;
+    Bucketed bc1, bc2, bdg;
+    std::vector<WgItem> wg1, wg2;
+    Bucketed bw1, bw2;
+    std::vector<GemmItem> d1f, d2f, d2w, d2d, d1w, d1d;
+    std::vector<MItem> per_member, per_sample, colsum, wred, adam;
+    int adam_chunk = 8192;
+    int wred_per_block = 4096, wred_blocks = 1;
+    // device tables
+    char* table_base = nullptr;
+    size_t table_bytes = 0;
+    std::vector<char> host_tables;
+    size_t off_mem, off_conv1, off_conv2, off_dgrad, off_wg1, off_wg2, off_d1f, off_d2f, off_d2w, off_d2d,
+        off_d1w, off_d1d, off_pm, off_ps, off_cs, off_wr, off_adam;
+    float *params = nullptr, *grads = nullptr, *m = nullptr, *v = nullptr, *act = nullptr;
+    bool bound = false;
+    size_t lds_conv_max = 0, lds_wg_max = 0;
+};
+
+size_t conv_lds_bytes(int rows, int Wp, int Cin, int K, int nt) {
+    const int Fp = odd_stride(Cin);
+    const int img = (rows * Wp * Fp + 3) & ~3;
+    const int kp = ((K + 3) & ~3);
+    const int kpa = (kp + 3) & ~3;
+    return (size_t)(img + kpa + kConvBK * bn_stride(nt)) * sizeof(float);
+}
+
+size_t wg_lds_bytes(int rows, int Hin, int Cin, int P, int nt) {
+    const int Fp = odd_stride(Cin);
+    const int img = (rows * Hin * Fp + 3) & ~3;
+    const int P4 = (P + 3) & ~3;
+    return (size_t)(img + P4 * dout_stride(nt) + P4) * sizeof(float);
+}
+
+template <class T>
+void bucket_by_nt(std::vector<T>& items, Bucketed& bk, const std::vector<Member>& mem) {
+    std::stable_sort(items.begin(), items.end(), [&](const T& x, const T& y) { return mem[x.member].nt < mem[y.member].nt; });
+    for (int nt = 1; nt <= 4; ++nt) {
+        bk.begin[nt] = (int)(std::lower_bound(items.begin(), items.end(), nt,
+                                              [&](const T& x, int v) { return mem[x.member].nt < v; }) - items.begin());
+        bk.end[nt] = (int)(std::upper_bound(items.begin(), items.end(), nt,
+                                            [&](int v, const T& x) { return v < mem[x.member].nt; }) - items.begin());
+    }
+}
+
+int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
+    P.n = n;
+    P.B = B;
+    P.mem.resize(n);
+    long long po = 0, ao = 0;
+    auto palloc = [&](long long cnt) { long long o = po; po += (cnt + 63) / 64 * 64; return o; };
+    auto aalloc = [&](long long cnt) { long long o = ao; ao += (cnt + 63) / 64 * 64; return o; };
+    for (int i = 0; i < n; ++i) {
+        const MpoCnnSpec& s = specs[i];
+        Member& m = P.mem[i];
+        if (s.nb_filters < 1 || s.nb_filters > 64 || s.kernel_size < 1 || s.kernel_size > 13 || s.pool_size < 1 ||
+            s.dense < 1 || s.dense > 4096 || !(s.dropout >= 0.f && s.dropout < 1.f) || !(s.lr > 0.f)) {
+            mpo::set_error("mpo_pop_create: member %d has unsupported spec (F=%d k=%d p=%d dense=%d lr=%g dropout=%g)", i,
+                           s.nb_filters, s.kernel_size, s.pool_size, s.dense, s.lr, s.dropout);
+            return MPO_ENOTSUP;
+        }
+        m.F = s.nb_filters; m.k = s.kernel_size; m.p = s.pool_size; m.dense = s.dense;
+        m.H1 = kImg - m.k + 1;
+        m.H2 = m.H1 - m.k + 1;
+        if (m.H2 < 1) { mpo::set_error("mpo_pop_create: member %d kernel too large", i); return MPO_ENOTSUP; }
+        m.s = m.H2 / m.p;
+        if (m.s < 1) { mpo::set_error("mpo_pop_create: member %d pool larger than feature map", i); return MPO_ENOTSUP; }
+        m.K1 = m.s * m.s * m.F;
+        m.lr = s.lr; m.rate = s.dropout; m.inv_keep = 1.f / (1.f - s.dropout); m.seed = s.seed;
+        m.drop_thr = (unsigned)std::ceil((double)s.dropout * 16777216.0);
+        m.nt = (m.F + 15) / 16;
+        const int k = m.k, F = m.F, D = m.dense;
+        m.w1 = palloc((long long)k * k * F); m.b1 = palloc(F);
+        m.w2 = palloc((long long)k * k * F * F); m.b2 = palloc(F);
+        m.w3 = palloc((long long)m.K1 * D); m.b3 = palloc(D);
+        m.w4 = palloc((long long)D * kClasses); m.b4 = palloc(kClasses);
+        m.pend = po;
+        // wgrad sample groups: enough blocks to fill the chip, few partial slabs
+        const long long wg2_flops = 2LL * k * k * F * F * m.H2 * m.H2;   // per sample
+        m.g2 = (int)std::min<long long>(B, std::max<long long>(1, (wg2_flops * B) / (64LL << 20)));
+        m.g1 = (int)std::min<long long>(B, std::max<long long>(1, (2LL * k * k * F * m.H1 * m.H1 * B) / (64LL << 20)));
+        m.a1 = aalloc((long long)B * m.H1 * m.H1 * F);
+        m.a2 = aalloc((long long)B * m.H2 * m.H2 * F);
+        m.pd = aalloc((long long)B * m.K1);
+        m.am = aalloc(((long long)B * m.K1 + 3) / 4);
+        m.h = aalloc((long long)B * D);
+        m.hd = aalloc((long long)B * D);
+        m.z3 = aalloc((long long)B * kClasses);
+        m.dz3 = aalloc((long long)B * kClasses);
+        m.dh = aalloc((long long)B * D);
+        m.dp = aalloc((long long)B * m.K1);
+        m.dz2 = aalloc((long long)B * m.H2 * m.H2 * F);
+        m.dz1 = aalloc((long long)B * m.H1 * m.H1 * F);
+        m.w2t = aalloc((long long)k * k * F * F);
+        m.wp1 = aalloc((long long)m.g1 * k * k * F);
+        m.wp2 = aalloc((long long)m.g2 * k * k * F * F);
+    }
+    P.n_params = po;
+    P.act_floats = ao;
+
+    // ---- work lists
+    for (int i = 0; i < n; ++i) {
+        const Member& m = P.mem[i];
+        const int R1 = std::max(1, 128 / m.H1), R2 = std::max(1, 128 / m.H2), Rd = std::max(1, 128 / m.H1);
+        for (int b = 0; b < B; ++b) {
+            for (int y = 0; y < m.H1; y += R1) P.conv1.push_back({i, b, y, std::min(R1, m.H1 - y)});
+            for (int y = 0; y < m.H2; y += R2) P.conv2.push_back({i, b, y, std::min(R2, m.H2 - y)});
+            for (int y = 0; y < m.H1; y += Rd) P.dgrad.push_back({i, b, y, std::min(Rd, m.H1 - y)});
+            P.per_sample.push_back({i, b});
+        }
+        P.lds_conv_max = std::max({P.lds_conv_max, conv_lds_bytes(R1 + m.k - 1, kImg, 1, m.k * m.k, m.nt),
+                                   conv_lds_bytes(R2 + m.k - 1, m.H1, m.F, m.k * m.k * m.F, m.nt),
+                                   conv_lds_bytes(Rd + m.k - 1, m.H2 + 2 * (m.k - 1), m.F, m.k * m.k * m.F, m.nt)});
+        // wgrad items
+        const int Rw2 = std::max(1, 128 / m.H2), Rw1 = std::max(1, 128 / m.H1);
+        const int K2 = m.k * m.k * m.F, K1w = m.k * m.k;
+        for (int g = 0; g < m.g2; ++g) {
+            const int b0 = (int)((long long)B * g / m.g2), b1 = (int)((long long)B * (g + 1) / m.g2);
+            for (int mg = 0; mg * 128 < K2; ++mg) P.wg2.push_back({i, mg, b0, b1, g, Rw2});
+        }
+        for (int g = 0; g < m.g1; ++g) {
+            const int b0 = (int)((long long)B * g / m.g1), b1 = (int)((long long)B * (g + 1) / m.g1);
+            for (int mg = 0; mg * 128 < K1w; ++mg) P.wg1.push_back({i, mg, b0, b1, g, Rw1});
+        }
+        P.lds_wg_max = std::max({P.lds_wg_max, wg_lds_bytes(Rw2 + m.k - 1, m.H1, m.F, Rw2 * m.H2, m.nt),
+                                 wg_lds_bytes(Rw1 + m.k - 1, kImg, 1, Rw1 * m.H1, m.nt)});
+        auto tiles = [&](std::vector<GemmItem>& v, int M, int N) {
+            for (int m0 = 0; m0 < M; m0 += 64)
+                for (int n0 = 0; n0 < N; n0 += 64) v.push_back({i, m0, n0, 0});
+        };
+        tiles(P.d1f, B, m.dense);
+        tiles(P.d2f, B, kClasses);
+        tiles(P.d2w, m.dense, kClasses);
+        tiles(P.d2d, B, m.dense);
+        tiles(P.d1w, m.K1, m.dense);
+        tiles(P.d1d, B, m.K1);
+        P.per_member.push_back({i, 0});
+        for (int c = 0; c < 4; ++c) P.colsum.push_back({i, c});
+        P.wred.push_back({i, 0});
+        P.wred.push_back({i, 1});
+        const long long np_ = m.pend - m.w1;
+        for (long long c = 0; c * P.adam_chunk < np_; ++c) P.adam.push_back({i, (int)c});
+    }
+    if (P.lds_conv_max > 160 * 1024 || P.lds_wg_max > 160 * 1024) {
+        mpo::set_error("mpo_pop_create: LDS plan exceeds 160 KiB (conv %zu, wgrad %zu)", P.lds_conv_max, P.lds_wg_max);
+        return MPO_ENOTSUP;
+    }
+    long long wmax = 0;
+    for (auto& m : P.mem) wmax = std::max(wmax, (long long)m.k * m.k * m.F * m.F);
+    P.wred_blocks = (int)((wmax + P.wred_per_block - 1) / P.wred_per_block);
+    bucket_by_nt(P.conv1, P.bc1, P.mem);
+    bucket_by_nt(P.conv2, P.bc2, P.mem);
+    bucket_by_nt(P.dgrad, P.bdg, P.mem);
+    bucket_by_nt(P.wg1, P.bw1, P.mem);
+    bucket_by_nt(P.wg2, P.bw2, P.mem);
+
+    // ---- serialise tables (one device upload)
+    size_t off = 0;
+    auto put = [&](const void* src, size_t bytes) {
+        off = mpo::align_up(off, 256);
+        const size_t o = off;
+        P.host_tables.resize(off + bytes);
+        if (bytes) std::copy_n(static_cast<const char*>(src), bytes, P.host_tables.data() + o);
+        off += bytes;
+        return o;
+    };
+    P.off_mem = put(P.mem.data(), P.mem.size() * sizeof(Member));
+    P.off_conv1 = put(P.conv1.data(), P.conv1.size() * sizeof(ConvItem));
+    P.off_conv2 = put(P.conv2.data(), P.conv2.size() * sizeof(ConvItem));
+    P.off_dgrad = put(P.dgrad.data(), P.dgrad.size() * sizeof(ConvItem));
+    P.off_wg1 = put(P.wg1.data(), P.wg1.size() * sizeof(WgItem));
+    P.off_wg2 = put(P.wg2.data(), P.wg2.size() * sizeof(WgItem));
+    P.off_d1f = put(P.d1f.data(), P.d1f.size() * sizeof(GemmItem));
+    P.off_d2f = put(P.d2f.data(), P.d2f.size() * sizeof(GemmItem));
+    P.off_d2w = put(P.d2w.data(), P.d2w.size() * sizeof(GemmItem));
+    P.off_d2d = put(P.d2d.data(), P.d2d.size() * sizeof(GemmItem));
+    P.off_d1w = put(P.d1w.data(), P.d1w.size() * sizeof(GemmItem));
+    P.off_d1d = put(P.d1d.data(), P.d1d.size() * sizeof(GemmItem));
+    P.off_pm = put(P.per_member.data(), P.per_member.size() * sizeof(MItem));
+    P.off_ps = put(P.per_sample.data(), P.per_sample.size() * sizeof(MItem));
+    P.off_cs = put(P.colsum.data(), P.colsum.size() * sizeof(MItem));
+    P.off_wr = put(P.wred.data(), P.wred.size() * sizeof(MItem));
+    P.off_adam = put(P.adam.data(), P.adam.size() * sizeof(MItem));
+    P.table_bytes = mpo::align_up(off, 256);
+    P.host_tables.resize(P.table_bytes);
+    return MPO_OK;
+}
+
+template <class T>
+const T* dev_table(const Plan& P, size_t off) {
+    return reinterpret_cast<const T*>(P.table_base + off);
+}
+
+template <int OP, int NT>
+hipError_t launch_conv_nt(const StepArgs& a, const ConvItem* items, int count, size_t lds, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    auto kern = conv_img_kernel<OP, NT>;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(count), dim3(256), lds, s, a, items);
+    return hipGetLastError();
+}
+
+template <int OP>
+hipError_t launch_conv(const Plan& P, const StepArgs& a, size_t table_off, const Bucketed& bk, hipStream_t s) {
+    const ConvItem* base = dev_table<ConvItem>(P, table_off);
+    hipError_t e;
+    if ((e = launch_conv_nt<OP, 1>(a, base + bk.begin[1], bk.end[1] - bk.begin[1], P.lds_conv_max, s))) return e;
+    if ((e = launch_conv_nt<OP, 2>(a, base + bk.begin[2], bk.end[2] - bk.begin[2], P.lds_conv_max, s))) return e;
+    if ((e = launch_conv_nt<OP, 3>(a, base + bk.begin[3], bk.end[3] - bk.begin[3], P.lds_conv_max, s))) return e;
+    return launch_conv_nt<OP, 4>(a, base + bk.begin[4], bk.end[4] - bk.begin[4], P.lds_conv_max, s);
+}
+
+template <int OP, int NT>
+hipError_t launch_wg_nt(const StepArgs& a, const WgItem* items, int count, size_t lds, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    auto kern = conv_wgrad_kernel<OP, NT>;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(count), dim3(256), lds, s, a, items);
+    return hipGetLastError();
+}
+
+template <int OP>
+hipError_t launch_wg(const Plan& P, const StepArgs& a, size_t table_off, const Bucketed& bk, hipStream_t s) {
+    const WgItem* base = dev_table<WgItem>(P, table_off);
+    hipError_t e;
+    if ((e = launch_wg_nt<OP, 1>(a, base + bk.begin[1], bk.end[1] - bk.begin[1], P.lds_wg_max, s))) return e;
+    if ((e = launch_wg_nt<OP, 2>(a, base + bk.begin[2], bk.end[2] - bk.begin[2], P.lds_wg_max, s))) return e;
+    if ((e = launch_wg_nt<OP, 3>(a, base + bk.begin[3], bk.end[3] - bk.begin[3], P.lds_wg_max, s))) return e;
+    return launch_wg_nt<OP, 4>(a, base + bk.begin[4], bk.end[4] - bk.begin[4], P.lds_wg_max, s);
+}
+
+template <int OP>
+hipError_t launch_dense(const Plan& P, const StepArgs& a, size_t off, size_t count, hipStream_t s) {
+    if (!count) return hipSuccess;
+    hipLaunchKernelGGL(dense_kernel<OP>, dim3((unsigned)count), dim3(256), 0, s, a, dev_table<GemmItem>(P, off));
+    return hipGetLastError();
+}
+
+StepArgs make_args(const Plan& P, const float* x, const int* labels, const int* order, long long order_stride,
+                   long long row0, int step, int train) {
+    StepArgs a;
+    a.mem = dev_table<Member>(P, P.off_mem);
+    a.params = P.params;
+    a.grads = P.grads;
+    a.act = P.act;
+    a.x = x;
+    a.labels = labels;
+    a.order = order;
+    a.order_stride = order_stride;
+    a.row0 = row0;
+    a.B = P.B;
+    a.step = step;
+    a.train = train;
+    a.loss_out = nullptr;
+    a.loss_sum = nullptr;
+    a.correct = nullptr;
+    return a;
+}
+
+int forward(const Plan& P, const StepArgs& a, hipStream_t s) {
+    MPO_HIP(launch_conv<CONV1_FWD>(P, a, P.off_conv1, P.bc1, s));
+    MPO_HIP(launch_conv<CONV2_FWD>(P, a, P.off_conv2, P.bc2, s));
+    hipLaunchKernelGGL(pool_fwd_kernel, dim3((unsigned)P.per_sample.size()), dim3(256), 0, s, a,
+                       dev_table<MItem>(P, P.off_ps));
+    MPO_LAUNCH_CHECK();
+    MPO_HIP(launch_dense<D1_FWD>(P, a, P.off_d1f, P.d1f.size(), s));
+    MPO_HIP(launch_dense<D2_FWD>(P, a, P.off_d2f, P.d2f.size(), s));
+    hipLaunchKernelGGL(softmax_bce_kernel, dim3((unsigned)P.n), dim3(256), 0, s, a, dev_table<MItem>(P, P.off_pm));
+    MPO_LAUNCH_CHECK();
+    return MPO_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+extern "C" {
+
+int mpo_pop_create(const MpoCnnSpec* specs, int n_members, int batch, void** handle) {
+    MPO_GUARD_BEGIN
+    MPO_CHECK_ARG(specs && handle, "mpo_pop_create: null pointer");
+    MPO_CHECK_ARG(n_members > 0 && batch > 0 && batch <= 256, "mpo_pop_create: n_members=%d batch=%d (1..256)",
+                  n_members, batch);
+    auto P = std::make_unique<Plan>();
+    int rc = build_plan(*P, specs, n_members, batch);
+    if (rc) return rc;
+    *handle = P.release();
+    return MPO_OK;
+    MPO_GUARD_END
+}
+
+int mpo_pop_destroy(void* handle) {
+    delete static_cast<Plan*>(handle);
+    return MPO_OK;
+}
+
+int mpo_pop_sizes(const void* handle, MpoPopSizes* out) {
+    MPO_CHECK_ARG(handle && out, "mpo_pop_sizes: null pointer");
+    const Plan& P = *static_cast<const Plan*>(handle);
+    out->n_params = P.n_params;
+    out->act_floats = P.act_floats;
+    out->table_bytes = (int64_t)P.table_bytes;
+    out->n_members = P.n;
+    out->batch = P.B;
+    return MPO_OK;
+}
+
+int mpo_pop_param_layout(const void* handle, int member, int64_t* offsets) {
+    MPO_CHECK_ARG(handle && offsets, "mpo_pop_param_layout: null pointer");
+    const Plan& P = *static_cast<const Plan*>(handle);
+    MPO_CHECK_ARG(member >= 0 && member < P.n, "mpo_pop_param_layout: member %d out of range", member);
+    const Member& m = P.mem[member];
+    const long long o[9] = {m.w1, m.b1, m.w2, m.b2, m.w3, m.b3, m.w4, m.b4, m.pend};
+    for (int i = 0; i < 9; ++i) offsets[i] = o[i];
+    return MPO_OK;
+}
+
+int mpo_pop_bind(void* handle, float* params, float* grads, float* adam_m, float* adam_v, float* act, void* tables,
+                 void* stream) {
+    MPO_GUARD_BEGIN
+    MPO_CHECK_ARG(handle && params && grads && adam_m && adam_v && act && tables, "mpo_pop_bind: null pointer");
+    Plan& P = *static_cast<Plan*>(handle);
+    P.params = params;
+    P.grads = grads;
+    P.m = adam_m;
+    P.v = adam_v;
+    P.act = act;
+    P.table_base = static_cast<char*>(tables);
+    MPO_HIP(hipMemcpyAsync(tables, P.host_tables.data(), P.table_bytes, hipMemcpyHostToDevice,
+                           static_cast<hipStream_t>(stream)));
+    P.bound = true;
+    return MPO_OK;
+    MPO_GUARD_END
+}
+
+int mpo_pop_train_step(void* handle, const float* x, const int32_t* labels, const int32_t* order, int64_t order_stride,
+                       int64_t row0, int32_t step, float* loss_out, void* stream) {
+    MPO_GUARD_BEGIN
+    MPO_CHECK_ARG(handle && x && labels && order && loss_out, "mpo_pop_train_step: null pointer");
+    Plan& P = *static_cast<Plan*>(handle);
+    MPO_CHECK_ARG(P.bound, "mpo_pop_train_step: call mpo_pop_bind first");
+    MPO_CHECK_ARG(step >= 0, "mpo_pop_train_step: step must be >= 0");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    StepArgs a = make_args(P, x, labels, order, order_stride, row0, step, 1);
+    a.loss_out = loss_out;
+    int rc = forward(P, a, s);
+    if (rc) return rc;
+    // backward
+    MPO_HIP(launch_dense<D2_WGRAD>(P, a, P.off_d2w, P.d2w.size(), s));
+    MPO_HIP(launch_dense<D2_DGRAD>(P, a, P.off_d2d, P.d2d.size(), s));
+    MPO_HIP(launch_dense<D1_WGRAD>(P, a, P.off_d1w, P.d1w.size(), s));
+    MPO_HIP(launch_dense<D1_DGRAD>(P, a, P.off_d1d, P.d1d.size(), s));
+    hipLaunchKernelGGL(pool_bwd_kernel, dim3((unsigned)P.per_sample.size()), dim3(256), 0, s, a,
+                       dev_table<MItem>(P, P.off_ps));
+    MPO_LAUNCH_CHECK();
+    hipLaunchKernelGGL(flip_w2_kernel, dim3(64, (unsigned)P.n), dim3(256), 0, s, a, dev_table<MItem>(P, P.off_pm));
+    MPO_LAUNCH_CHECK();
+    MPO_HIP(launch_conv<CONV2_DGRAD>(P, a, P.off_dgrad, P.bdg, s));
+    MPO_HIP(launch_wg<WG_CONV2>(P, a, P.off_wg2, P.bw2, s));
+    MPO_HIP(launch_wg<WG_CONV1>(P, a, P.off_wg1, P.bw1, s));
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)P.wred_blocks, (unsigned)P.wred.size()), dim3(256), 0, s, a,
+                       dev_table<MItem>(P, P.off_wr), P.wred_per_block);
+    MPO_LAUNCH_CHECK();
+    hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)P.colsum.size()), dim3(256), 0, s, a, dev_table<MItem>(P, P.off_cs));
+    MPO_LAUNCH_CHECK();
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)P.adam.size()), dim3(256), 0, s, a, dev_table<MItem>(P, P.off_adam),
+                       P.params, P.m, P.v, step + 1, 0.9f, 0.999f, 1e-8f, P.adam_chunk);
+    MPO_LAUNCH_CHECK();
+    return MPO_OK;
+    MPO_GUARD_END
+}
+
+int mpo_pop_eval_step(void* handle, const float* x, const int32_t* labels, const int32_t* order, int64_t order_stride,
+                      int64_t row0, float* loss_sum, int32_t* correct, void* stream) {
+    MPO_GUARD_BEGIN
+    MPO_CHECK_ARG(handle && x && labels && order && loss_sum && correct, "mpo_pop_eval_step: null pointer");
+    Plan& P = *static_cast<Plan*>(handle);
+    MPO_CHECK_ARG(P.bound, "mpo_pop_eval_step: call mpo_pop_bind first");
+    StepArgs a = make_args(P, x, labels, order, order_stride, row0, 0, 0);
+    a.loss_sum = loss_sum;
+    a.correct = correct;
+    return forward(P, a, static_cast<hipStream_t>(stream));
+    MPO_GUARD_END
+}
+
+int mpo_kfold_gather(const float* X, const int32_t* idx, int64_t rows, int row_elems, float* out, void* stream) {
+    MPO_GUARD_BEGIN
+    MPO_CHECK_ARG(X && idx && out, "mpo_kfold_gather: null pointer");
+    MPO_CHECK_ARG(rows >= 0 && row_elems > 0, "mpo_kfold_gather: bad shape");
+    if (rows == 0) return MPO_OK;
+    const unsigned gy = (unsigned)std::min<int64_t>(rows, 65535);
+    const unsigned gz = (unsigned)((rows + 65534) / 65535);
+    const unsigned gx = (unsigned)std::min(8, (row_elems + 255) / 256);
+    hipLaunchKernelGGL(kfold_gather_kernel, dim3(gx, gy, gz), dim3(256), 0, static_cast<hipStream_t>(stream), X, idx,
+                       (long long)rows, row_elems, out);
+    MPO_LAUNCH_CHECK();
+    return MPO_OK;
+    MPO_GUARD_END
+}
+
+}  // extern "C"

@@ -1,0 +1,266 @@
+"""Device-resident population engine for MNIST-CNN trials.
+
+Replaces the ``process_block`` / ``mpi_learn`` block-master + worker ranks
+(/root/reference/process_block.py:71-96, 104-121): instead of one MPI block per
+candidate network, every (trial, fold) pair is a *member* of one population
+that trains on a single GPU in lock-step, ragged widths and all, through
+``libmpo.so`` (csrc/cnn.hip).  torch only owns the device arenas.
+
+Public surface:
+
+* :class:`TrialSpec` -- test_mnist hyper-parameters + per-trial lr / dropout;
+* :class:`PopulationEngine` -- low level: ``train_step`` / ``eval_step`` on
+  caller-supplied batch orders (the k-fold index gather);
+* :func:`kfold_split` -- the fold split (contiguous KFold, no shuffle);
+* :meth:`PopulationEngine.fit_folds` -- full training of every member over
+  ``epochs`` with a validation pass per epoch; returns per-member histories.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr
+
+IMG = 28
+NUM_CLASSES = 10
+PARAM_NAMES = ("w1", "b1", "w2", "b2", "w3", "b3", "w4", "b4")
+
+
+@dataclass
+class TrialSpec:
+    """One test_mnist trial (mpiLAPI.py:138-176; space option3:127-131)."""
+
+    nb_filters: int = 32
+    kernel_size: int = 3
+    pool_size: int = 2
+    dense: int = 128
+    lr: float = 1e-3
+    dropout: float = 0.25
+    seed: int = 0
+
+    def geometry(self):
+        H1 = IMG - self.kernel_size + 1
+        H2 = H1 - self.kernel_size + 1
+        s = H2 // self.pool_size
+        return dict(H1=H1, H2=H2, s=s, K1=s * s * self.nb_filters)
+
+    def param_shapes(self):
+        F, k, D = self.nb_filters, self.kernel_size, self.dense
+        K1 = self.geometry()["K1"]
+        return {"w1": (k, k, 1, F), "b1": (F,), "w2": (k, k, F, F), "b2": (F,),
+                "w3": (K1, D), "b3": (D,), "w4": (D, NUM_CLASSES), "b4": (NUM_CLASSES,)}
+
+    def flops_per_sample_fwd(self):
+        F, k, D = self.nb_filters, self.kernel_size, self.dense
+        g = self.geometry()
+        return 2 * k * k * F * g["H1"] ** 2 + 2 * k * k * F * F * g["H2"] ** 2 + 2 * g["K1"] * D + 2 * D * NUM_CLASSES
+
+    def flops_per_sample_train(self):
+        k, F = self.kernel_size, self.nb_filters
+        return 3 * self.flops_per_sample_fwd() - 2 * k * k * F * self.geometry()["H1"] ** 2
+
+
+MpoCnnSpec = _lib.MpoCnnSpec
+MpoPopSizes = _lib.MpoPopSizes
+
+
+def glorot_uniform_init(spec: TrialSpec, seed: int):
+    """Keras defaults: glorot_uniform kernels, zero biases (float32)."""
+    rng = np.random.RandomState(seed)
+    out = {}
+    for name, shape in spec.param_shapes().items():
+        if name.startswith("w"):
+            if len(shape) == 4:
+                rf = shape[0] * shape[1]
+                fan_in, fan_out = rf * shape[2], rf * shape[3]
+            else:
+                fan_in, fan_out = shape
+            lim = np.sqrt(6.0 / (fan_in + fan_out))
+            out[name] = rng.uniform(-lim, lim, size=shape).astype(np.float32)
+        else:
+            out[name] = np.zeros(shape, dtype=np.float32)
+    return out
+
+
+def kfold_split(n_samples: int, n_fold: int, fold: int):
+    """Fold split as an index gather.
+
+    n_fold == 1 mirrors option3's file split (first 70 % train, rest validation,
+    hyperparameter_search_option3.py:136-139); n_fold > 1 is a contiguous KFold
+    without shuffle: fold sizes n//k (+1 for the first n%k folds)."""
+    idx = np.arange(n_samples, dtype=np.int32)
+    if n_fold <= 1:
+        cut = int(n_samples * 0.70)
+        return idx[:cut], idx[cut:]
+    sizes = np.full(n_fold, n_samples // n_fold, dtype=np.int64)
+    sizes[: n_samples % n_fold] += 1
+    starts = np.concatenate([[0], np.cumsum(sizes)])
+    v0, v1 = starts[fold], starts[fold + 1]
+    return np.concatenate([idx[:v0], idx[v1:]]), idx[v0:v1]
+
+
+class PopulationEngine:
+    """A population of ragged CNN members resident on one GPU."""
+
+    def __init__(self, specs, batch=100, device=None, init=None, init_seed=0):
+        self.specs = [s if isinstance(s, TrialSpec) else TrialSpec(**s) for s in specs]
+        self.n = len(self.specs)
+        self.batch = int(batch)
+        self.device = torch.device(device if device is not None else "cuda")
+        L = lib()
+        arr = (MpoCnnSpec * self.n)()
+        for i, s in enumerate(self.specs):
+            arr[i] = MpoCnnSpec(int(s.nb_filters), int(s.kernel_size), int(s.pool_size), int(s.dense),
+                                float(s.lr), float(s.dropout), int(s.seed) & 0xFFFFFFFF, 0)
+        h = ctypes.c_void_p()
+        check(L.mpo_pop_create(arr, self.n, self.batch, ctypes.byref(h)), "mpo_pop_create")
+        self._h = h
+        sz = MpoPopSizes()
+        check(L.mpo_pop_sizes(h, ctypes.byref(sz)), "mpo_pop_sizes")
+        self.n_params = int(sz.n_params)
+        self.layout = []
+        offs = (ctypes.c_int64 * 9)()
+        for i in range(self.n):
+            check(L.mpo_pop_param_layout(h, i, offs), "mpo_pop_param_layout")
+            self.layout.append([int(v) for v in offs])
+        dev = self.device
+        self.params = torch.zeros(self.n_params, dtype=torch.float32, device=dev)
+        self.grads = torch.zeros_like(self.params)
+        self.adam_m = torch.zeros_like(self.params)
+        self.adam_v = torch.zeros_like(self.params)
+        self.act = torch.zeros(int(sz.act_floats), dtype=torch.float32, device=dev)
+        self.tables = torch.empty(int(sz.table_bytes), dtype=torch.uint8, device=dev)
+        self.loss = torch.zeros(self.n, dtype=torch.float32, device=dev)
+        self.val_loss_sum = torch.zeros(self.n, dtype=torch.float32, device=dev)
+        self.val_correct = torch.zeros(self.n, dtype=torch.int32, device=dev)
+        with torch.cuda.device(dev):
+            check(L.mpo_pop_bind(h, ptr(self.params), ptr(self.grads), ptr(self.adam_m), ptr(self.adam_v),
+                                 ptr(self.act), ptr(self.tables), _lib.stream_handle(dev)), "mpo_pop_bind")
+        if init is None:
+            init = [glorot_uniform_init(s, init_seed + i) for i, s in enumerate(self.specs)]
+        for i, p in enumerate(init):
+            self.set_params(i, p)
+        self.step_count = 0
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().mpo_pop_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    # -- parameters -------------------------------------------------------------
+    def _slices(self, i):
+        o = self.layout[i]
+        shapes = self.specs[i].param_shapes()
+        return {n: (o[j], shapes[n]) for j, n in enumerate(PARAM_NAMES)}
+
+    def set_params(self, i, params):
+        flat = []
+        for n, (off, shape) in self._slices(i).items():
+            a = np.asarray(params[n], dtype=np.float32).reshape(shape)
+            cnt = int(np.prod(shape))
+            self.params[off:off + cnt].copy_(torch.from_numpy(a.reshape(-1)))
+            flat.append(cnt)
+
+    def get_params(self, i):
+        out = {}
+        host = self.params.cpu().numpy()
+        for n, (off, shape) in self._slices(i).items():
+            cnt = int(np.prod(shape))
+            out[n] = host[off:off + cnt].reshape(shape).copy()
+        return out
+
+    def reset_optimizer(self):
+        self.adam_m.zero_()
+        self.adam_v.zero_()
+        self.step_count = 0
+
+    # -- steps --------------------------------------------------------------------
+    def train_step(self, x, labels, order, row0, step=None):
+        """x [n,784] f32, labels [n] i32, order [n_members, L] i32 (device)."""
+        step = self.step_count if step is None else int(step)
+        with torch.cuda.device(self.device):
+            check(lib().mpo_pop_train_step(self._h, ptr(x), ptr(labels), ptr(order), int(order.shape[1]), int(row0),
+                                           step, ptr(self.loss), _lib.stream_handle(self.device)),
+                  "mpo_pop_train_step")
+        self.step_count = step + 1
+        return self.loss
+
+    def eval_reset(self):
+        self.val_loss_sum.zero_()
+        self.val_correct.zero_()
+
+    def eval_step(self, x, labels, order, row0):
+        with torch.cuda.device(self.device):
+            check(lib().mpo_pop_eval_step(self._h, ptr(x), ptr(labels), ptr(order), int(order.shape[1]), int(row0),
+                                          ptr(self.val_loss_sum), ptr(self.val_correct),
+                                          _lib.stream_handle(self.device)), "mpo_pop_eval_step")
+
+    # -- full k-fold training -----------------------------------------------------
+    def fit_folds(self, x, labels, folds, n_fold, epochs, record_train_loss=False):
+        """Train every member for ``epochs`` on its fold's training indices (in
+        order, no shuffle), validating once per epoch (validate_every =
+        count/batch, option3:260).  ``folds[i]`` is member i's fold index.
+        Returns {"val_loss": [n, epochs], "val_acc": [n, epochs], "train_loss": ...}."""
+        n_samples = x.shape[0]
+        B = self.batch
+        tr, va = [], []
+        for i in range(self.n):
+            t, v = kfold_split(n_samples, n_fold, int(folds[i]))
+            tr.append(t)
+            va.append(v)
+        n_tr = min(len(t) for t in tr)
+        n_va = min(len(v) for v in va)
+        steps_per_epoch = n_tr // B
+        val_batches = n_va // B
+        order_tr = torch.from_numpy(np.stack([t[:n_tr] for t in tr])).to(self.device)
+        order_va = torch.from_numpy(np.stack([v[:n_va] for v in va])).to(self.device)
+        val_loss = torch.zeros(self.n, epochs, dtype=torch.float32, device=self.device)
+        val_acc = torch.zeros(self.n, epochs, dtype=torch.float32, device=self.device)
+        tl = []
+        for ep in range(epochs):
+            for st in range(steps_per_epoch):
+                loss = self.train_step(x, labels, order_tr, st * B)
+                if record_train_loss:
+                    tl.append(loss.clone())
+            self.eval_reset()
+            for vb in range(val_batches):
+                self.eval_step(x, labels, order_va, vb * B)
+            denom = float(val_batches * B)
+            val_loss[:, ep] = self.val_loss_sum / denom
+            val_acc[:, ep] = self.val_correct.to(torch.float32) / denom
+        out = {"val_loss": val_loss.cpu().numpy(), "val_acc": val_acc.cpu().numpy(),
+               "steps_per_epoch": steps_per_epoch, "val_batches": val_batches}
+        if record_train_loss:
+            out["train_loss"] = torch.stack(tl, 1).cpu().numpy() if tl else np.zeros((self.n, 0))
+        return out
+
+
+def kfold_gather(X, idx, out=None):
+    """``mpo_kfold_gather``: out[r] = X[idx[r]] on device."""
+    rows = idx.shape[0]
+    row_elems = int(np.prod(X.shape[1:]))
+    if out is None:
+        out = torch.empty((rows,) + tuple(X.shape[1:]), dtype=X.dtype, device=X.device)
+    with torch.cuda.device(X.device):
+        check(lib().mpo_kfold_gather(ptr(X), ptr(idx), int(rows), row_elems, ptr(out),
+                                     _lib.stream_handle(X.device)), "mpo_kfold_gather")
+    return out
+
+
+def synthetic_mnist(n=60000, seed=0, device=None):
+    """x ~ U[0,1] f32 (n, 784), labels uniform 0..9, generated on device."""
+    g = torch.Generator(device=device if device is not None else "cuda")
+    g.manual_seed(seed)
+    dev = torch.device(device if device is not None else "cuda")
+    x = torch.rand(n, IMG * IMG, generator=g, device=dev, dtype=torch.float32)
+    y = torch.randint(0, NUM_CLASSES, (n,), generator=g, device=dev, dtype=torch.int32)
+    return x, y

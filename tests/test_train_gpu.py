@@ -1,0 +1,139 @@
+"""GPU parity of the population training engine (csrc/cnn.hip) against the fp64
+numpy oracle (oracle/cnn.py) on identical seeded init weights, data order and
+dropout masks.  Bar (BASELINE.json north_star): per-step training loss within
+1e-3 relative.  Gradients are additionally checked tensor by tensor."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import cnn as C
+
+pytestmark = pytest.mark.gpu
+
+# (F, k, p, dense, lr, dropout, fold): extremes of the option3 mnist space,
+# every NT bucket (F <= 16, 32, 48, 64) and s = 1 pooling
+MEMBERS = [
+    (10, 2, 2, 50, 1e-3, 0.25, 0),
+    (50, 10, 10, 200, 1e-3, 0.25, 1),
+    (33, 5, 3, 77, 2e-3, 0.25, 2),
+    (17, 3, 7, 120, 1e-3, 0.1, 3),
+    (50, 2, 2, 200, 1e-3, 0.25, 4),
+    (16, 7, 4, 64, 3e-3, 0.5, 0),
+]
+N_SAMPLES, N_FOLD, BATCH = 500, 5, 100
+
+
+def dataset(seed=0):
+    rng = np.random.RandomState(seed)
+    x = rng.uniform(size=(N_SAMPLES, 784)).astype(np.float32)
+    y = rng.randint(0, 10, size=N_SAMPLES).astype(np.int32)
+    return x, y
+
+
+def make_engine(members=MEMBERS):
+    from mpi_opt_amd.population import PopulationEngine, TrialSpec, glorot_uniform_init
+
+    specs = [TrialSpec(F, k, p, d, lr, dr, seed=1000 + i) for i, (F, k, p, d, lr, dr, _) in enumerate(members)]
+    init = [glorot_uniform_init(s, 7 + i) for i, s in enumerate(specs)]
+    eng = PopulationEngine(specs, batch=BATCH, init=init)
+    return eng, specs, init
+
+
+def oracle_for(spec, init):
+    return C.TrialOracle(spec.nb_filters, spec.kernel_size, spec.pool_size, spec.dense,
+                         {n: v.astype(np.float64) for n, v in init.items()}, lr=spec.lr,
+                         dropout=spec.dropout, seed=spec.seed)
+
+
+def orders(members, x):
+    from mpi_opt_amd.population import kfold_split
+
+    tr, va = [], []
+    for m in members:
+        t, v = kfold_split(x.shape[0], N_FOLD, m[-1])
+        tr.append(t)
+        va.append(v)
+    return np.stack(tr), np.stack(va)
+
+
+def test_eval_forward_matches_oracle():
+    x, y = dataset()
+    eng, specs, init = make_engine()
+    tr, va = orders(MEMBERS, x)
+    xd, yd = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    ova = torch.from_numpy(va).cuda()
+    eng.eval_reset()
+    eng.eval_step(xd, yd, ova, 0)
+    got = eng.val_loss_sum.cpu().numpy() / BATCH
+    for i, s in enumerate(specs):
+        ref = oracle_for(s, init[i]).eval_loss(x[va[i]], y[va[i]])
+        assert abs(got[i] - ref) <= 1e-5 * abs(ref), (i, got[i], ref)
+
+
+def test_one_step_gradients_match_oracle():
+    x, y = dataset(1)
+    eng, specs, init = make_engine()
+    tr, va = orders(MEMBERS, x)
+    xd, yd = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    otr = torch.from_numpy(tr).cuda()
+    loss = eng.train_step(xd, yd, otr, 0).cpu().numpy()
+    grads = eng.grads.cpu().numpy()
+    for i, s in enumerate(specs):
+        o = oracle_for(s, init[i])
+        ref_loss, _, _, cache = o.forward(x[tr[i][:BATCH]], y[tr[i][:BATCH]], step=0, train=True)
+        g = o.backward(cache)
+        assert abs(loss[i] - ref_loss) <= 1e-5 * abs(ref_loss), (i, loss[i], ref_loss)
+        for j, (name, (off, shape)) in enumerate(eng._slices(i).items()):
+            cnt = int(np.prod(shape))
+            gd = grads[off:off + cnt].reshape(shape)
+            scale = np.abs(g[name]).max() + 1e-30
+            err = np.abs(gd - g[name]).max() / scale
+            assert err < 2e-4, (i, name, err)
+
+
+@pytest.mark.parametrize("epochs", [2])
+def test_multistep_losses_within_1e3(epochs):
+    x, y = dataset(2)
+    eng, specs, init = make_engine()
+    tr, va = orders(MEMBERS, x)
+    xd, yd = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    hist = eng.fit_folds(xd, yd, [m[-1] for m in MEMBERS], N_FOLD, epochs, record_train_loss=True)
+    steps = hist["steps_per_epoch"]
+    for i, s in enumerate(specs):
+        o = oracle_for(s, init[i])
+        ref_tl, ref_vl = [], []
+        step = 0
+        for ep in range(epochs):
+            for st in range(steps):
+                rows = tr[i][st * BATCH:(st + 1) * BATCH]
+                ref_tl.append(o.train_step(x[rows], y[rows], step))
+                step += 1
+            ref_vl.append(o.eval_loss(x[va[i]], y[va[i]]))
+        rel = np.abs(hist["train_loss"][i] - np.array(ref_tl)) / np.abs(ref_tl)
+        assert rel.max() < 1e-3, (i, rel)
+        relv = np.abs(hist["val_loss"][i] - np.array(ref_vl)) / np.abs(ref_vl)
+        assert relv.max() < 1e-3, (i, relv)
+
+
+def test_kfold_gather_kernel():
+    from mpi_opt_amd.population import kfold_gather
+
+    x, _ = dataset(3)
+    xd = torch.from_numpy(x).cuda()
+    idx = np.random.RandomState(0).permutation(N_SAMPLES)[:123].astype(np.int32)
+    out = kfold_gather(xd, torch.from_numpy(idx).cuda())
+    np.testing.assert_array_equal(out.cpu().numpy(), x[idx])
+
+
+def test_population_isolation():
+    """A member's trajectory does not depend on who else is in the population."""
+    x, y = dataset(4)
+    xd, yd = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    eng_all, specs, init = make_engine()
+    tr, _ = orders(MEMBERS, x)
+    eng_one, _, _ = make_engine(MEMBERS[2:3])
+    eng_one.set_params(0, init[2])
+    for st in range(3):
+        la = eng_all.train_step(xd, yd, torch.from_numpy(tr).cuda(), st * BATCH).cpu().numpy()
+        lo = eng_one.train_step(xd, yd, torch.from_numpy(tr[2:3]).cuda(), st * BATCH).cpu().numpy()
+        assert la[2] == lo[0]
