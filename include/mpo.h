@@ -159,6 +159,10 @@ int mpo_pop_sizes(const void* handle, MpoPopSizes* out);
  * w1 (k,k,1,F), b1, w2 (k,k,F,F), b2, w3 (s*s*F, dense), b3, w4 (dense,10), b4, end.
  * Keras weight shapes and order (Conv2D kernel (kh,kw,cin,cout), Dense (in,out)). */
 int mpo_pop_param_layout(const void* handle, int member, int64_t* offsets);
+/* offsets[15] (floats into the activation arena) of member's a1, a2, pd,
+ * argmax (bytes at that float offset), h, hd, z3, dz3, dh, dp, dz2, dz1, w2t,
+ * conv1 / conv2 weight-gradient partial slabs (diagnostics and tests). */
+int mpo_pop_act_layout(const void* handle, int member, int64_t* offsets);
 /* Bind caller-owned device arenas (zero-initialised by the caller) and upload
  * the work tables (async on `stream`). */
 int mpo_pop_bind(void* handle, float* params, float* grads, float* adam_m, float* adam_v, float* act,

@@ -70,6 +70,7 @@ SIGNATURES = {
     "mpo_pop_destroy": (_I, [_P]),
     "mpo_pop_sizes": (_I, [_P, ctypes.POINTER(MpoPopSizes)]),
     "mpo_pop_param_layout": (_I, [_P, _I, ctypes.POINTER(ctypes.c_int64)]),
+    "mpo_pop_act_layout": (_I, [_P, _I, ctypes.POINTER(ctypes.c_int64)]),
     "mpo_pop_bind": (_I, [_P, _P, _P, _P, _P, _P, _P, _P]),
     "mpo_pop_train_step": (_I, [_P, _P, _P, _P, _I64, _I64, ctypes.c_int32, _P, _P]),
     "mpo_pop_eval_step": (_I, [_P, _P, _P, _P, _I64, _I64, _P, _P, _P]),

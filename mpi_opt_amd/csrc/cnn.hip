@@ -1064,6 +1064,16 @@ int mpo_pop_param_layout(const void* handle, int member, int64_t* offsets) {
     return MPO_OK;
 }
 
+int mpo_pop_act_layout(const void* handle, int member, int64_t* offsets) {
+    MPO_CHECK_ARG(handle && offsets, "mpo_pop_act_layout: null pointer");
+    const Plan& P = *static_cast<const Plan*>(handle);
+    MPO_CHECK_ARG(member >= 0 && member < P.n, "mpo_pop_act_layout: member %d out of range", member);
+    const Member& m = P.mem[member];
+    const long long o[15] = {m.a1, m.a2, m.pd, m.am, m.h, m.hd, m.z3, m.dz3, m.dh, m.dp, m.dz2, m.dz1, m.w2t, m.wp1, m.wp2};
+    for (int i = 0; i < 15; ++i) offsets[i] = o[i];
+    return MPO_OK;
+}
+
 int mpo_pop_bind(void* handle, float* params, float* grads, float* adam_m, float* adam_v, float* act, void* tables,
                  void* stream) {
     MPO_GUARD_BEGIN

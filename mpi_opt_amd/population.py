@@ -29,6 +29,7 @@ from ._lib import check, lib, ptr
 IMG = 28
 NUM_CLASSES = 10
 PARAM_NAMES = ("w1", "b1", "w2", "b2", "w3", "b3", "w4", "b4")
+ACT_NAMES = ("a1", "a2", "pd", "am", "h", "hd", "z3", "dz3", "dh", "dp", "dz2", "dz1", "w2t", "wp1", "wp2")
 
 
 @dataclass
@@ -128,6 +129,11 @@ class PopulationEngine:
         for i in range(self.n):
             check(L.mpo_pop_param_layout(h, i, offs), "mpo_pop_param_layout")
             self.layout.append([int(v) for v in offs])
+        self.act_layout = []
+        aoffs = (ctypes.c_int64 * 15)()
+        for i in range(self.n):
+            check(L.mpo_pop_act_layout(h, i, aoffs), "mpo_pop_act_layout")
+            self.act_layout.append(dict(zip(ACT_NAMES, [int(v) for v in aoffs])))
         dev = self.device
         self.params = torch.zeros(self.n_params, dtype=torch.float32, device=dev)
         self.grads = torch.zeros_like(self.params)
@@ -177,6 +183,20 @@ class PopulationEngine:
             cnt = int(np.prod(shape))
             out[n] = host[off:off + cnt].reshape(shape).copy()
         return out
+
+    def activation(self, i, name, shape):
+        """Copy of member i's activation tensor ``name`` (diagnostics / tests)."""
+        off = self.act_layout[i][name]
+        cnt = int(np.prod(shape))
+        return self.act[off:off + cnt].reshape(shape).cpu().numpy()
+
+    def argmax_table(self, i):
+        """Member i's max-pool argmax (uint8, [batch, s*s*F]) of the last forward."""
+        K1 = self.specs[i].geometry()["K1"]
+        off = self.act_layout[i]["am"] * 4
+        n = self.batch * K1
+        raw = self.act.view(torch.uint8)[off:off + n]
+        return raw.cpu().numpy().reshape(self.batch, K1)
 
     def reset_optimizer(self):
         self.adam_m.zero_()

@@ -30,11 +30,11 @@ def dataset(seed=0):
     return x, y
 
 
-def make_engine(members=MEMBERS):
+def make_engine(members=MEMBERS, first=0):
     from mpi_opt_amd.population import PopulationEngine, TrialSpec, glorot_uniform_init
 
-    specs = [TrialSpec(F, k, p, d, lr, dr, seed=1000 + i) for i, (F, k, p, d, lr, dr, _) in enumerate(members)]
-    init = [glorot_uniform_init(s, 7 + i) for i, s in enumerate(specs)]
+    specs = [TrialSpec(F, k, p, d, lr, dr, seed=1000 + first + i) for i, (F, k, p, d, lr, dr, _) in enumerate(members)]
+    init = [glorot_uniform_init(s, 7 + first + i) for i, s in enumerate(specs)]
     eng = PopulationEngine(specs, batch=BATCH, init=init)
     return eng, specs, init
 
@@ -70,6 +70,17 @@ def test_eval_forward_matches_oracle():
         assert abs(got[i] - ref) <= 1e-5 * abs(ref), (i, got[i], ref)
 
 
+def device_decisions(eng, i, spec):
+    """The device forward's discrete choices (argmax, ReLU gates) for member i."""
+    g = spec.geometry()
+    F, D = spec.nb_filters, spec.dense
+    am = eng.argmax_table(i).reshape(BATCH, g["s"], g["s"], F).astype(np.int64)
+    return {"arg": am,
+            "a1_pos": eng.activation(i, "a1", (BATCH, g["H1"], g["H1"], F)) > 0,
+            "a2_pos": eng.activation(i, "a2", (BATCH, g["H2"], g["H2"], F)) > 0,
+            "h_pos": eng.activation(i, "h", (BATCH, D)) > 0}
+
+
 def test_one_step_gradients_match_oracle():
     x, y = dataset(1)
     eng, specs, init = make_engine()
@@ -78,17 +89,24 @@ def test_one_step_gradients_match_oracle():
     otr = torch.from_numpy(tr).cuda()
     loss = eng.train_step(xd, yd, otr, 0).cpu().numpy()
     grads = eng.grads.cpu().numpy()
+    report = []
     for i, s in enumerate(specs):
         o = oracle_for(s, init[i])
         ref_loss, _, _, cache = o.forward(x[tr[i][:BATCH]], y[tr[i][:BATCH]], step=0, train=True)
-        g = o.backward(cache)
+        g, absg = o.backward(cache, abs_terms=True, decisions=device_decisions(eng, i, s))
         assert abs(loss[i] - ref_loss) <= 1e-5 * abs(ref_loss), (i, loss[i], ref_loss)
         for j, (name, (off, shape)) in enumerate(eng._slices(i).items()):
             cnt = int(np.prod(shape))
             gd = grads[off:off + cnt].reshape(shape)
-            scale = np.abs(g[name]).max() + 1e-30
-            err = np.abs(gd - g[name]).max() / scale
-            assert err < 2e-4, (i, name, err)
+            # f32 bound: error of an n-term f32 reduction of already-f32-rounded
+            # terms is O(1e-6) of the sum of |terms|, plus 1e-4 of the tensor scale
+            err = np.abs(gd - g[name])
+            bound = 1e-4 * np.abs(g[name]).max() + 2e-5 * absg[name]
+            report.append((i, name, float((err / (np.abs(g[name]).max() + 1e-30)).max()),
+                           float((err / (absg[name] + 1e-30)).max()), bool(np.all(err <= bound))))
+    for r in report:
+        print("member %d %-3s err/max %.2e err/sum|terms| %.2e ok=%s" % r)
+    assert all(r[-1] for r in report)
 
 
 @pytest.mark.parametrize("epochs", [2])
@@ -131,8 +149,7 @@ def test_population_isolation():
     xd, yd = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
     eng_all, specs, init = make_engine()
     tr, _ = orders(MEMBERS, x)
-    eng_one, _, _ = make_engine(MEMBERS[2:3])
-    eng_one.set_params(0, init[2])
+    eng_one, _, _ = make_engine(MEMBERS[2:3], first=2)
     for st in range(3):
         la = eng_all.train_step(xd, yd, torch.from_numpy(tr).cuda(), st * BATCH).cpu().numpy()
         lo = eng_one.train_step(xd, yd, torch.from_numpy(tr[2:3]).cuda(), st * BATCH).cpu().numpy()
