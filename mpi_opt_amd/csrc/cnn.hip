@@ -114,9 +114,24 @@ __host__ __device__ constexpr inline int odd_stride(int c) { return (c == 1) ? 1
 // One workgroup = (member, sample b, output rows [y0, y0+R)); M = R*Ho <= 128
 // output pixels = 8 m-tiles of 16 spread over 4 waves; N = F in NT tiles of 16.
 // ============================================================================
-constexpr int kConvBK = 64;  // B rows per LDS chunk
+constexpr int kConvBK = 32;  // B rows per LDS chunk (8 k-steps), double-buffered
 
 __host__ __device__ constexpr inline int bn_stride(int nt) { return nt * 16 + ((nt & 1) ? 0 : 16); }
+__host__ __device__ constexpr inline int align4(int x) { return (x + 3) & ~3; }
+
+// Copy n contiguous floats (pixels of cin channels) into an LDS image with
+// pixel stride fp, without a per-element integer division.
+__device__ __forceinline__ void stage_row(const float* __restrict__ src, float* __restrict__ dst, int n, int cin,
+                                          int fp, int tid) {
+    const int q = 256 / cin, r = 256 - q * cin;
+    int gx = tid / cin, c = tid - gx * cin;
+    for (int e = tid; e < n; e += 256) {
+        dst[gx * fp + c] = src[e];
+        c += r;
+        gx += q;
+        if (c >= cin) { c -= cin; ++gx; }
+    }
+}
 
 template <int OP, int NT>
 __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvItem* __restrict__ items) {
@@ -150,19 +165,41 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
     }
     const int N = F;
     const int K = k * k * Cin;
-    const int Kp = (K + 3) & ~3;
+    const int Kp = (K + kConvBK - 1) / kConvBK * kConvBK;
     const int Wp = Hin + 2 * pad;
     const int Fp = odd_stride(Cin);
     const int rows = it.R + k - 1;
     const int M = it.R * Ho;
     constexpr int BNs = bn_stride(NT);
+    constexpr int BPT = kConvBK * NT * 16 / 256;  // B prefetch floats per thread
 
     float* img = smem;                                   // [rows][Wp][Fp]
     const int img_elems = rows * Wp * Fp;
-    int* koff = reinterpret_cast<int*>(smem + ((img_elems + 3) & ~3));   // [Kp]
-    float* bs = smem + ((img_elems + 3) & ~3) + ((Kp + 3) & ~3);          // [kConvBK][BNs]
+    int* koff = reinterpret_cast<int*>(smem + align4(img_elems));   // [Kp], 16-k groups as [krow][4 k-steps]
+    float* bs = smem + align4(img_elems) + Kp;                       // [2][kConvBK][BNs]
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int krow = lane >> 4, kcol = lane & 15;
+
+    float breg[BPT];
+    auto load_b = [&](int kc0) {
+#pragma unroll
+        for (int q = 0; q < BPT; ++q) {
+            const int e = tid + 256 * q;
+            const int r = e / (NT * 16), c = e - r * (NT * 16);
+            const int kk = kc0 + r;
+            breg[q] = (kk < K && c < N) ? W[(long long)kk * N + c] : 0.f;
+        }
+    };
+    auto store_b = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < BPT; ++q) {
+            const int e = tid + 256 * q;
+            const int r = e / (NT * 16), c = e - r * (NT * 16);
+            bs[(buf * kConvBK + r) * BNs + c] = breg[q];
+        }
+    };
+    load_b(0);
 
     // ---- stage the (virtually padded) input rows
     for (int e = tid; e < img_elems; e += 256) img[e] = 0.f;
@@ -172,9 +209,10 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
         if (gy < 0 || gy >= Hin) continue;
         const float* src = in + (long long)gy * Hin * Cin;
         float* dst = img + (r * Wp + pad) * Fp;
-        for (int e = tid; e < Hin * Cin; e += 256) {
-            const int gx = e / Cin, c = e - gx * Cin;
-            dst[gx * Fp + c] = src[e];
+        if (Cin == 1) {
+            for (int e = tid; e < Hin; e += 256) dst[e] = src[e];
+        } else {
+            stage_row(src, dst, Hin * Cin, Cin, Fp, tid);
         }
     }
     for (int kk = tid; kk < Kp; kk += 256) {
@@ -185,8 +223,10 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
             const int kx = rem / Cin, c = rem - kx * Cin;
             off = (ky * Wp + kx) * Fp + c;
         }
-        koff[kk] = off;
+        const int g = kk >> 4, w = kk & 15;        // k = 16 g + 4 u + krow
+        koff[g * 16 + (w & 3) * 4 + (w >> 2)] = off;
     }
+    store_b(0);
 
     // ---- per-lane pixel bases of this wave's m-tiles
     const int mtiles = (M + 15) >> 4;
@@ -210,32 +250,39 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
 
-    const int krow = lane >> 4, kcol = lane & 15;
-    for (int kc0 = 0; kc0 < Kp; kc0 += kConvBK) {
-        __syncthreads();
-        const int kn = min(kConvBK, Kp - kc0);
-        for (int e = tid; e < kConvBK * NT * 16; e += 256) {
-            const int r = e / (NT * 16), c = e - r * (NT * 16);
-            const int kk = kc0 + r;
-            bs[r * BNs + c] = (kk < K && c < N) ? W[(long long)kk * N + c] : 0.f;
-        }
-        __syncthreads();
-        if (!has[0]) continue;
-        for (int ks = 0; ks < kn; ks += 4) {
-            const int ko = koff[kc0 + ks + krow];
-            float bf[NT];
+    const int nchunks = Kp / kConvBK;
+    for (int c = 0; c < nchunks; ++c) {
+        const bool more = c + 1 < nchunks;
+        if (more) load_b((c + 1) * kConvBK);
+        if (has[0]) {
+            const float* bb = bs + (c & 1) * kConvBK * BNs;
 #pragma unroll
-            for (int j = 0; j < NT; ++j) bf[j] = bs[(ks + krow) * BNs + j * 16 + kcol];
-            const float a0 = img[pb[0] + ko];
+            for (int g = 0; g < kConvBK / 16; ++g) {
+                const int4 ko4 = *reinterpret_cast<const int4*>(koff + (c * (kConvBK / 16) + g) * 16 + krow * 4);
+                const int kov[4] = {ko4.x, ko4.y, ko4.z, ko4.w};
 #pragma unroll
-            for (int j = 0; j < NT; ++j) acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bf[j], acc[0][j], 0, 0, 0);
-            if (has[1]) {
-                const float a1 = img[pb[1] + ko];
+                for (int u = 0; u < 4; ++u) {
+                    const int kr = g * 16 + u * 4 + krow;
+                    float bf[NT];
 #pragma unroll
-                for (int j = 0; j < NT; ++j) acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bf[j], acc[1][j], 0, 0, 0);
+                    for (int j = 0; j < NT; ++j) bf[j] = bb[kr * BNs + j * 16 + kcol];
+                    const float a0 = img[pb[0] + kov[u]];
+#pragma unroll
+                    for (int j = 0; j < NT; ++j)
+                        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bf[j], acc[0][j], 0, 0, 0);
+                    if (has[1]) {
+                        const float a1 = img[pb[1] + kov[u]];
+#pragma unroll
+                        for (int j = 0; j < NT; ++j)
+                            acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bf[j], acc[1][j], 0, 0, 0);
+                    }
+                }
             }
         }
+        if (more) store_b((c + 1) & 1);
+        __syncthreads();
     }
 
     // ---- epilogue: C/D map col = lane & 15, row = (lane >> 4) * 4 + r
@@ -288,7 +335,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(StepArgs a, const WgIte
         Hin = mb.H1; Cin = F; Ho = mb.H2; dout_off = mb.dz2; part_off = mb.wp2;
     }
     const int N = F;
-    const int Kw = k * k * Cin;  // output rows
+    const int Kw = k * k * Cin;  // weight rows; row Kw is the bias gradient (an all-ones A row)
     const int Fp = odd_stride(Cin);
     constexpr int Fq = NT * 16 + ((NT & 1) ? 0 : 16);
     const int R = it.R;
@@ -303,14 +350,15 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(StepArgs a, const WgIte
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int krow = lane >> 4, kcol = lane & 15;
 
-    int toff[2];
-    bool has[2];
+    int toff[4];
+    bool has[4], ones[4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 4; ++i) {
         const int mt = wave + 4 * i;
-        const int m0 = it.mg * 128 + mt * 16;
-        has[i] = m0 < Kw;
+        const int m0 = it.mg * 256 + mt * 16;
+        has[i] = m0 <= Kw;
         const int m = m0 + (lane & 15);
+        ones[i] = m == Kw;
         int off = 0;
         if (m < Kw) {
             const int kc = k * Cin;
@@ -320,9 +368,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(StepArgs a, const WgIte
         }
         toff[i] = off;
     }
-    f32x4 acc[2][NT];
+    f32x4 acc[4][NT];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -345,15 +393,18 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(StepArgs a, const WgIte
             if (Cin == Fp) {
                 for (int e = tid; e < irows * Hin * Cin; e += 256) img[e] = src[e];
             } else {
-                for (int e = tid; e < irows * Hin * Cin; e += 256) {
-                    const int px = e / Cin, c = e - px * Cin;
-                    img[px * Fp + c] = src[e];
-                }
+                stage_row(src, img, irows * Hin * Cin, Cin, Fp, tid);
             }
             const float* dsrc = dout + (long long)y0 * Ho * N;
-            for (int e = tid; e < P4 * Fq; e += 256) {
-                const int px = e / Fq, c = e - px * Fq;
-                dl[e] = (px < pcnt && c < N) ? dsrc[px * N + c] : 0.f;
+            stage_row(dsrc, dl, pcnt * N, N, Fq, tid);
+            // zero the channel padding of the staged pixels and the padded pixels
+            for (int e = tid; e < P4 * (Fq - N); e += 256) {
+                const int px = e / (Fq - N), c = N + (e - px * (Fq - N));
+                dl[px * Fq + c] = 0.f;
+            }
+            for (int e = pcnt * N + tid; e < P4 * N; e += 256) {
+                const int px = e / N, c = e - px * N;
+                dl[px * Fq + c] = 0.f;
             }
             for (int px = tid; px < P4; px += 256) {
                 int off = 0;
@@ -371,20 +422,20 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(StepArgs a, const WgIte
                 float bf[NT];
 #pragma unroll
                 for (int j = 0; j < NT; ++j) bf[j] = dl[(ks + krow) * Fq + j * 16 + kcol];
-                const float a0 = img[toff[0] + po];
 #pragma unroll
-                for (int j = 0; j < NT; ++j) acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bf[j], acc[0][j], 0, 0, 0);
-                if (has[1]) {
-                    const float a1 = img[toff[1] + po];
+                for (int i = 0; i < 4; ++i) {
+                    if (!has[i]) break;   // tiles are assigned in order: has[] is a prefix
+                    const float av = ones[i] ? 1.f : img[toff[i] + po];
 #pragma unroll
-                    for (int j = 0; j < NT; ++j) acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bf[j], acc[1][j], 0, 0, 0);
+                    for (int j = 0; j < NT; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bf[j], acc[i][j], 0, 0, 0);
                 }
             }
         }
     }
-    float* part = a.act + part_off + (long long)it.group * Kw * N;
+    float* part = a.act + part_off + (long long)it.group * (Kw + 1) * N;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 4; ++i) {
         if (!has[i]) continue;
         const int mt = wave + 4 * i;
 #pragma unroll
@@ -393,8 +444,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(StepArgs a, const WgIte
             if (n >= N) continue;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int m = it.mg * 128 + mt * 16 + krow * 4 + r;
-                if (m < Kw) part[(long long)m * N + n] = acc[i][j][r];
+                const int m = it.mg * 256 + mt * 16 + krow * 4 + r;
+                if (m <= Kw) part[(long long)m * N + n] = acc[i][j][r];
             }
         }
     }
@@ -405,15 +456,17 @@ __global__ void wgrad_reduce_kernel(StepArgs a, const MItem* __restrict__ items,
     const MItem it = items[blockIdx.y];
     const Member& mb = a.mem[it.member];
     const int conv = it.aux;  // 0 conv1, 1 conv2
-    const long long S = conv ? (long long)mb.k * mb.k * mb.F * mb.F : (long long)mb.k * mb.k * mb.F;
+    const long long Sw = conv ? (long long)mb.k * mb.k * mb.F * mb.F : (long long)mb.k * mb.k * mb.F;
+    const long long S = Sw + mb.F;   // weight rows + the bias row
     const int G = conv ? mb.g2 : mb.g1;
     const float* part = a.act + (conv ? mb.wp2 : mb.wp1);
-    float* g = a.grads + (conv ? mb.w2 : mb.w1);
+    float* gw = a.grads + (conv ? mb.w2 : mb.w1);
+    float* gb = a.grads + (conv ? mb.b2 : mb.b1);
     for (long long i = (long long)blockIdx.x * per_block + threadIdx.x; i < S && i < (long long)(blockIdx.x + 1) * per_block;
          i += blockDim.x) {
         float s = 0.f;
         for (int q = 0; q < G; ++q) s += part[q * S + i];
-        g[i] = s;
+        if (i < Sw) gw[i] = s; else gb[i - Sw] = s;
     }
 }
 
@@ -740,8 +793,9 @@ __global__ void kfold_gather_kernel(const float* __restrict__ X, const int* __re
 // Host-side plan
 // ============================================================================
 struct Bucketed {
-    // items sorted by NT (1..4); [begin, end) per NT
+    // items sorted by NT (1..4); [begin, end) per NT; dynamic LDS per NT bucket
     int begin[5] = {0, 0, 0, 0, 0}, end[5] = {0, 0, 0, 0, 0};
+    size_t lds[5] = {0, 0, 0, 0, 0};
 };
 
 struct Plan {
@@ -769,17 +823,30 @@ struct Plan {
 
 size_t conv_lds_bytes(int rows, int Wp, int Cin, int K, int nt) {
     const int Fp = odd_stride(Cin);
-    const int img = (rows * Wp * Fp + 3) & ~3;
-    const int kp = ((K + 3) & ~3);
-    const int kpa = (kp + 3) & ~3;
-    return (size_t)(img + kpa + kConvBK * bn_stride(nt)) * sizeof(float);
+    const int img = align4(rows * Wp * Fp);
+    const int kp = (K + kConvBK - 1) / kConvBK * kConvBK;
+    return (size_t)(img + kp + 2 * kConvBK * bn_stride(nt)) * sizeof(float);
 }
 
 size_t wg_lds_bytes(int rows, int Hin, int Cin, int P, int nt) {
     const int Fp = odd_stride(Cin);
-    const int img = (rows * Hin * Fp + 3) & ~3;
+    const int img = align4(rows * Hin * Fp);
     const int P4 = (P + 3) & ~3;
     return (size_t)(img + P4 * dout_stride(nt) + P4) * sizeof(float);
+}
+
+// Row-chunk height: as many output rows as fit M = R*Ho <= 128 pixels, shrunk
+// (down to half of that) to fit 3 or 2 workgroups per CU when possible.
+template <class Fn>
+int choose_rows(int Ho, Fn lds_of) {
+    const int rmax = std::max(1, std::min(Ho, 128 / Ho));
+    const int rmin = std::max(1, rmax / 2);
+    for (size_t budget : {(size_t)52 << 10, (size_t)78 << 10})
+        for (int R = rmax; R >= rmin; --R)
+            if (lds_of(R) <= budget) return R;
+    for (int R = rmax; R >= 1; --R)
+        if (lds_of(R) <= ((size_t)160 << 10)) return R;
+    return 1;
 }
 
 template <class T>
@@ -825,10 +892,10 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         m.w3 = palloc((long long)m.K1 * D); m.b3 = palloc(D);
         m.w4 = palloc((long long)D * kClasses); m.b4 = palloc(kClasses);
         m.pend = po;
-        // wgrad sample groups: enough blocks to fill the chip, few partial slabs
-        const long long wg2_flops = 2LL * k * k * F * F * m.H2 * m.H2;   // per sample
-        m.g2 = (int)std::min<long long>(B, std::max<long long>(1, (wg2_flops * B) / (64LL << 20)));
-        m.g1 = (int)std::min<long long>(B, std::max<long long>(1, (2LL * k * k * F * m.H1 * m.H1 * B) / (64LL << 20)));
+        // wgrad sample groups (partial slabs reduced in a fixed order): ~10
+        // samples per conv2 block, ~4 per conv1 block (its GEMM is tiny)
+        m.g2 = std::max(1, std::min(B, (B + 9) / 10));
+        m.g1 = std::max(1, std::min(B, (B + 3) / 4));
         m.a1 = aalloc((long long)B * m.H1 * m.H1 * F);
         m.a2 = aalloc((long long)B * m.H2 * m.H2 * F);
         m.pd = aalloc((long long)B * m.K1);
@@ -842,8 +909,8 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         m.dz2 = aalloc((long long)B * m.H2 * m.H2 * F);
         m.dz1 = aalloc((long long)B * m.H1 * m.H1 * F);
         m.w2t = aalloc((long long)k * k * F * F);
-        m.wp1 = aalloc((long long)m.g1 * k * k * F);
-        m.wp2 = aalloc((long long)m.g2 * k * k * F * F);
+        m.wp1 = aalloc((long long)m.g1 * (k * k + 1) * F);
+        m.wp2 = aalloc((long long)m.g2 * (k * k * F + 1) * F);
     }
     P.n_params = po;
     P.act_floats = ao;
@@ -851,29 +918,40 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
     // ---- work lists
     for (int i = 0; i < n; ++i) {
         const Member& m = P.mem[i];
-        const int R1 = std::max(1, 128 / m.H1), R2 = std::max(1, 128 / m.H2), Rd = std::max(1, 128 / m.H1);
+        const int k = m.k, F = m.F, nt = m.nt;
+        const int R1 = choose_rows(m.H1, [&](int R) { return conv_lds_bytes(R + k - 1, kImg, 1, k * k, nt); });
+        const int R2 = choose_rows(m.H2, [&](int R) { return conv_lds_bytes(R + k - 1, m.H1, F, k * k * F, nt); });
+        const int Rd = choose_rows(m.H1, [&](int R) { return conv_lds_bytes(R + k - 1, m.H2 + 2 * (k - 1), F, k * k * F, nt); });
+        const size_t l1 = conv_lds_bytes(R1 + k - 1, kImg, 1, k * k, nt);
+        const size_t l2 = conv_lds_bytes(R2 + k - 1, m.H1, F, k * k * F, nt);
+        const size_t ld = conv_lds_bytes(Rd + k - 1, m.H2 + 2 * (k - 1), F, k * k * F, nt);
+        P.bc1.lds[nt] = std::max(P.bc1.lds[nt], l1);
+        P.bc2.lds[nt] = std::max(P.bc2.lds[nt], l2);
+        P.bdg.lds[nt] = std::max(P.bdg.lds[nt], ld);
         for (int b = 0; b < B; ++b) {
             for (int y = 0; y < m.H1; y += R1) P.conv1.push_back({i, b, y, std::min(R1, m.H1 - y)});
             for (int y = 0; y < m.H2; y += R2) P.conv2.push_back({i, b, y, std::min(R2, m.H2 - y)});
             for (int y = 0; y < m.H1; y += Rd) P.dgrad.push_back({i, b, y, std::min(Rd, m.H1 - y)});
             P.per_sample.push_back({i, b});
         }
-        P.lds_conv_max = std::max({P.lds_conv_max, conv_lds_bytes(R1 + m.k - 1, kImg, 1, m.k * m.k, m.nt),
-                                   conv_lds_bytes(R2 + m.k - 1, m.H1, m.F, m.k * m.k * m.F, m.nt),
-                                   conv_lds_bytes(Rd + m.k - 1, m.H2 + 2 * (m.k - 1), m.F, m.k * m.k * m.F, m.nt)});
+        P.lds_conv_max = std::max({P.lds_conv_max, l1, l2, ld});
         // wgrad items
-        const int Rw2 = std::max(1, 128 / m.H2), Rw1 = std::max(1, 128 / m.H1);
-        const int K2 = m.k * m.k * m.F, K1w = m.k * m.k;
+        const int Rw2 = choose_rows(m.H2, [&](int R) { return wg_lds_bytes(R + k - 1, m.H1, F, R * m.H2, nt); });
+        const int Rw1 = choose_rows(m.H1, [&](int R) { return wg_lds_bytes(R + k - 1, kImg, 1, R * m.H1, nt); });
+        const size_t lw2 = wg_lds_bytes(Rw2 + k - 1, m.H1, F, Rw2 * m.H2, nt);
+        const size_t lw1 = wg_lds_bytes(Rw1 + k - 1, kImg, 1, Rw1 * m.H1, nt);
+        P.bw2.lds[nt] = std::max(P.bw2.lds[nt], lw2);
+        P.bw1.lds[nt] = std::max(P.bw1.lds[nt], lw1);
+        const int K2 = k * k * F, K1w = k * k;
         for (int g = 0; g < m.g2; ++g) {
             const int b0 = (int)((long long)B * g / m.g2), b1 = (int)((long long)B * (g + 1) / m.g2);
-            for (int mg = 0; mg * 128 < K2; ++mg) P.wg2.push_back({i, mg, b0, b1, g, Rw2});
+            for (int mg = 0; mg * 256 <= K2; ++mg) P.wg2.push_back({i, mg, b0, b1, g, Rw2});
         }
         for (int g = 0; g < m.g1; ++g) {
             const int b0 = (int)((long long)B * g / m.g1), b1 = (int)((long long)B * (g + 1) / m.g1);
-            for (int mg = 0; mg * 128 < K1w; ++mg) P.wg1.push_back({i, mg, b0, b1, g, Rw1});
+            for (int mg = 0; mg * 256 <= K1w; ++mg) P.wg1.push_back({i, mg, b0, b1, g, Rw1});
         }
-        P.lds_wg_max = std::max({P.lds_wg_max, wg_lds_bytes(Rw2 + m.k - 1, m.H1, m.F, Rw2 * m.H2, m.nt),
-                                 wg_lds_bytes(Rw1 + m.k - 1, kImg, 1, Rw1 * m.H1, m.nt)});
+        P.lds_wg_max = std::max({P.lds_wg_max, lw2, lw1});
         auto tiles = [&](std::vector<GemmItem>& v, int M, int N) {
             for (int m0 = 0; m0 < M; m0 += 64)
                 for (int n0 = 0; n0 < N; n0 += 64) v.push_back({i, m0, n0, 0});
@@ -885,7 +963,7 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         tiles(P.d1w, m.K1, m.dense);
         tiles(P.d1d, B, m.K1);
         P.per_member.push_back({i, 0});
-        for (int c = 0; c < 4; ++c) P.colsum.push_back({i, c});
+        for (int c = 2; c < 4; ++c) P.colsum.push_back({i, c});
         P.wred.push_back({i, 0});
         P.wred.push_back({i, 1});
         const long long np_ = m.pend - m.w1;
@@ -896,7 +974,7 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         return MPO_ENOTSUP;
     }
     long long wmax = 0;
-    for (auto& m : P.mem) wmax = std::max(wmax, (long long)m.k * m.k * m.F * m.F);
+    for (auto& m : P.mem) wmax = std::max(wmax, (long long)m.k * m.k * m.F * m.F + m.F);
     P.wred_blocks = (int)((wmax + P.wred_per_block - 1) / P.wred_per_block);
     bucket_by_nt(P.conv1, P.bc1, P.mem);
     bucket_by_nt(P.conv2, P.bc2, P.mem);
@@ -954,10 +1032,10 @@ template <int OP>
 hipError_t launch_conv(const Plan& P, const StepArgs& a, size_t table_off, const Bucketed& bk, hipStream_t s) {
     const ConvItem* base = dev_table<ConvItem>(P, table_off);
     hipError_t e;
-    if ((e = launch_conv_nt<OP, 1>(a, base + bk.begin[1], bk.end[1] - bk.begin[1], P.lds_conv_max, s))) return e;
-    if ((e = launch_conv_nt<OP, 2>(a, base + bk.begin[2], bk.end[2] - bk.begin[2], P.lds_conv_max, s))) return e;
-    if ((e = launch_conv_nt<OP, 3>(a, base + bk.begin[3], bk.end[3] - bk.begin[3], P.lds_conv_max, s))) return e;
-    return launch_conv_nt<OP, 4>(a, base + bk.begin[4], bk.end[4] - bk.begin[4], P.lds_conv_max, s);
+    if ((e = launch_conv_nt<OP, 1>(a, base + bk.begin[1], bk.end[1] - bk.begin[1], bk.lds[1], s))) return e;
+    if ((e = launch_conv_nt<OP, 2>(a, base + bk.begin[2], bk.end[2] - bk.begin[2], bk.lds[2], s))) return e;
+    if ((e = launch_conv_nt<OP, 3>(a, base + bk.begin[3], bk.end[3] - bk.begin[3], bk.lds[3], s))) return e;
+    return launch_conv_nt<OP, 4>(a, base + bk.begin[4], bk.end[4] - bk.begin[4], bk.lds[4], s);
 }
 
 template <int OP, int NT>
@@ -973,10 +1051,10 @@ template <int OP>
 hipError_t launch_wg(const Plan& P, const StepArgs& a, size_t table_off, const Bucketed& bk, hipStream_t s) {
     const WgItem* base = dev_table<WgItem>(P, table_off);
     hipError_t e;
-    if ((e = launch_wg_nt<OP, 1>(a, base + bk.begin[1], bk.end[1] - bk.begin[1], P.lds_wg_max, s))) return e;
-    if ((e = launch_wg_nt<OP, 2>(a, base + bk.begin[2], bk.end[2] - bk.begin[2], P.lds_wg_max, s))) return e;
-    if ((e = launch_wg_nt<OP, 3>(a, base + bk.begin[3], bk.end[3] - bk.begin[3], P.lds_wg_max, s))) return e;
-    return launch_wg_nt<OP, 4>(a, base + bk.begin[4], bk.end[4] - bk.begin[4], P.lds_wg_max, s);
+    if ((e = launch_wg_nt<OP, 1>(a, base + bk.begin[1], bk.end[1] - bk.begin[1], bk.lds[1], s))) return e;
+    if ((e = launch_wg_nt<OP, 2>(a, base + bk.begin[2], bk.end[2] - bk.begin[2], bk.lds[2], s))) return e;
+    if ((e = launch_wg_nt<OP, 3>(a, base + bk.begin[3], bk.end[3] - bk.begin[3], bk.lds[3], s))) return e;
+    return launch_wg_nt<OP, 4>(a, base + bk.begin[4], bk.end[4] - bk.begin[4], bk.lds[4], s);
 }
 
 template <int OP>

@@ -1,0 +1,57 @@
+"""Time the population train step on one GPU (diagnostic; bench.py has the contract)."""
+import argparse
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+from mpi_opt_amd.population import PopulationEngine, TrialSpec, kfold_split, synthetic_mnist  # noqa: E402
+
+
+def sample_trials(n, seed=13579):
+    rng = np.random.RandomState(seed)
+    out = []
+    for i in range(n):
+        out.append(TrialSpec(nb_filters=int(rng.randint(10, 51)), pool_size=int(rng.randint(2, 11)),
+                             kernel_size=int(rng.randint(2, 11)), dense=int(rng.randint(50, 201)), seed=i))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--trials", type=int, default=64)
+    ap.add_argument("--folds", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
+    args = ap.parse_args()
+    trials = sample_trials(args.trials)
+    members = []
+    folds = []
+    for t in trials:
+        for f in range(args.folds):
+            members.append(TrialSpec(t.nb_filters, t.kernel_size, t.pool_size, t.dense, t.lr, t.dropout, seed=len(members)))
+            folds.append(f)
+    t0 = time.time()
+    eng = PopulationEngine(members, batch=100)
+    x, y = synthetic_mnist(60000, seed=0)
+    tr = np.stack([kfold_split(60000, args.folds, f)[0] for f in folds])
+    order = torch.from_numpy(tr).cuda()
+    torch.cuda.synchronize()
+    print("setup %.1fs members=%d params=%.1fM act=%.2fGB" % (time.time() - t0, len(members), eng.n_params / 1e6,
+                                                              eng.act.numel() * 4 / 1e9), flush=True)
+    for s in range(2):
+        eng.train_step(x, y, order, s * 100)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    for s in range(args.steps):
+        eng.train_step(x, y, order, (s + 2) * 100)
+    torch.cuda.synchronize()
+    dt = (time.time() - t0) / args.steps
+    flops = sum(m.flops_per_sample_train() for m in members) * 100
+    print("train step %.2f ms  %.1f TFLOP/s  (%.1f%% of 157.3)" % (dt * 1e3, flops / dt / 1e12, flops / dt / 157.3e12 * 100))
+    print("loss", eng.loss[:5].cpu().numpy())
+
+
+if __name__ == "__main__":
+    main()
