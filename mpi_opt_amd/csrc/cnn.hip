@@ -58,6 +58,7 @@ struct Member {
     long long w1, b1, w2, b2, w3, b3, w4, b4, pend;
     // activation arena offsets (floats)
     long long a1, a2, pd, am, h, hd, z3, dz3, dh, dp, dz2, dz1, w2t, wp1, wp2;
+    long long w1p, w2p;  // zero-padded forward weights [K16][16*NT] (+16 rows slack)
 };
 
 struct ConvItem { int member, b, y0, R; };
@@ -106,7 +107,14 @@ __device__ __forceinline__ bool drop_keep(unsigned base, unsigned elem, unsigned
     return (lowbias32(elem ^ base) >> 8) >= thr;
 }
 
-__host__ __device__ constexpr inline int odd_stride(int c) { return (c == 1) ? 1 : (c | 1); }
+// LDS pixel strides chosen for conflict-free MFMA operand reads (ds_read_b32 banks
+// = dword index mod 32 per 32-lane half):
+//  * forward conv: lanes 0-15 read 16 pixels at stride fp, lanes 16-31 the next
+//    channel (+1): fp = 2 (mod 4) puts the two halves on the even / odd banks;
+//  * weight gradient: lanes 0-15 read 16 channels (+1 each), lanes 16-31 the next
+//    pixel (+fp): fp = 16 (mod 32) puts them on banks 0-15 / 16-31.
+__host__ __device__ constexpr inline int fwd_fp(int c) { return c == 1 ? 1 : c + ((6 - (c & 3)) & 3); }
+__host__ __device__ constexpr inline int wg_fp(int c) { return c == 1 ? 1 : c + ((48 - (c & 31)) & 31); }
 
 // ============================================================================
 // Image-stationary implicit-GEMM convolution (forward and input-gradient).
@@ -118,6 +126,10 @@ constexpr int kConvBK = 32;  // B rows per LDS chunk (8 k-steps), double-buffere
 
 __host__ __device__ constexpr inline int bn_stride(int nt) { return nt * 16 + ((nt & 1) ? 0 : 16); }
 __host__ __device__ constexpr inline int align4(int x) { return (x + 3) & ~3; }
+
+// dgrad image pixel stride: >= F rounded to 4 (zero channels for the 16-channel
+// k blocks) and = 2 (mod 4), which makes the 4x4-tile A reads bank-conflict free.
+__host__ __device__ constexpr inline int dgrad_fp(int F) { return ((F + 3) & ~3) + 2; }
 
 // Copy n contiguous floats (pixels of cin channels) into an LDS image with
 // pixel stride fp, without a per-element integer division.
@@ -139,83 +151,50 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
     const ConvItem it = items[blockIdx.x];
     const Member& mb = a.mem[it.member];
     const int k = mb.k, F = mb.F;
-    int Hin, Cin, pad, Ho;
+    int Hin, Cin, Ho;
     const float* in;
     const float* W;
-    const float* bias = nullptr;
+    const float* bias;
     float* out;
-    const float* relu_mask = nullptr;
     if (OP == CONV1_FWD) {
-        Hin = kImg; Cin = 1; pad = 0; Ho = mb.H1;
+        Hin = kImg; Cin = 1; Ho = mb.H1;
         const int sidx = a.order[(long long)it.member * a.order_stride + a.row0 + it.b];
         in = a.x + (long long)sidx * (kImg * kImg);
-        W = a.params + mb.w1; bias = a.params + mb.b1;
+        W = a.act + mb.w1p; bias = a.params + mb.b1;
         out = a.act + mb.a1 + (long long)it.b * Ho * Ho * F;
-    } else if (OP == CONV2_FWD) {
-        Hin = mb.H1; Cin = F; pad = 0; Ho = mb.H2;
-        in = a.act + mb.a1 + (long long)it.b * Hin * Hin * F;
-        W = a.params + mb.w2; bias = a.params + mb.b2;
-        out = a.act + mb.a2 + (long long)it.b * Ho * Ho * F;
     } else {
-        Hin = mb.H2; Cin = F; pad = k - 1; Ho = mb.H1;
-        in = a.act + mb.dz2 + (long long)it.b * Hin * Hin * F;
-        W = a.act + mb.w2t;
-        out = a.act + mb.dz1 + (long long)it.b * Ho * Ho * F;
-        relu_mask = a.act + mb.a1 + (long long)it.b * Ho * Ho * F;
+        Hin = mb.H1; Cin = F; Ho = mb.H2;
+        in = a.act + mb.a1 + (long long)it.b * Hin * Hin * F;
+        W = a.act + mb.w2p; bias = a.params + mb.b2;
+        out = a.act + mb.a2 + (long long)it.b * Ho * Ho * F;
     }
     const int N = F;
+    constexpr int N16 = NT * 16;
     const int K = k * k * Cin;
-    const int Kp = (K + kConvBK - 1) / kConvBK * kConvBK;
-    const int Wp = Hin + 2 * pad;
-    const int Fp = odd_stride(Cin);
+    const int K16 = (K + 15) & ~15;
+    const int Wp = Hin;
+    const int Fp = fwd_fp(Cin);
     const int rows = it.R + k - 1;
     const int M = it.R * Ho;
-    constexpr int BNs = bn_stride(NT);
-    constexpr int BPT = kConvBK * NT * 16 / 256;  // B prefetch floats per thread
 
-    float* img = smem;                                   // [rows][Wp][Fp]
+    float* img = smem;                                               // [rows][Wp][Fp]
     const int img_elems = rows * Wp * Fp;
-    int* koff = reinterpret_cast<int*>(smem + align4(img_elems));   // [Kp], 16-k groups as [krow][4 k-steps]
-    float* bs = smem + align4(img_elems) + Kp;                       // [2][kConvBK][BNs]
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int* koff = reinterpret_cast<int*>(smem + align4(img_elems));   // [K16], groups of 16 as [krow][4]
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int krow = lane >> 4, kcol = lane & 15;
 
-    float breg[BPT];
-    auto load_b = [&](int kc0) {
-#pragma unroll
-        for (int q = 0; q < BPT; ++q) {
-            const int e = tid + 256 * q;
-            const int r = e / (NT * 16), c = e - r * (NT * 16);
-            const int kk = kc0 + r;
-            breg[q] = (kk < K && c < N) ? W[(long long)kk * N + c] : 0.f;
-        }
-    };
-    auto store_b = [&](int buf) {
-#pragma unroll
-        for (int q = 0; q < BPT; ++q) {
-            const int e = tid + 256 * q;
-            const int r = e / (NT * 16), c = e - r * (NT * 16);
-            bs[(buf * kConvBK + r) * BNs + c] = breg[q];
-        }
-    };
-    load_b(0);
-
-    // ---- stage the (virtually padded) input rows
-    for (int e = tid; e < img_elems; e += 256) img[e] = 0.f;
-    __syncthreads();
+    // ---- stage the input rows + the tap-offset table (the only barrier)
     for (int r = 0; r < rows; ++r) {
-        const int gy = it.y0 + r - pad;
-        if (gy < 0 || gy >= Hin) continue;
-        const float* src = in + (long long)gy * Hin * Cin;
-        float* dst = img + (r * Wp + pad) * Fp;
+        const float* src = in + (long long)(it.y0 + r) * Hin * Cin;
+        float* dst = img + r * Wp * Fp;
         if (Cin == 1) {
             for (int e = tid; e < Hin; e += 256) dst[e] = src[e];
         } else {
             stage_row(src, dst, Hin * Cin, Cin, Fp, tid);
         }
     }
-    for (int kk = tid; kk < Kp; kk += 256) {
+    for (int kk = tid; kk < K16; kk += 256) {
         int off = 0;
         if (kk < K) {
             const int kc = k * Cin;
@@ -226,9 +205,7 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
         const int g = kk >> 4, w = kk & 15;        // k = 16 g + 4 u + krow
         koff[g * 16 + (w & 3) * 4 + (w >> 2)] = off;
     }
-    store_b(0);
 
-    // ---- per-lane pixel bases of this wave's m-tiles
     const int mtiles = (M + 15) >> 4;
     int pb[2];
     bool has[2];
@@ -244,45 +221,54 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
         }
         pb[i] = base;
     }
-
     f32x4 acc[2][NT];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     __syncthreads();
+    if (!has[0]) return;   // wave-uniform; no barriers below
 
-    const int nchunks = Kp / kConvBK;
-    for (int c = 0; c < nchunks; ++c) {
-        const bool more = c + 1 < nchunks;
-        if (more) load_b((c + 1) * kConvBK);
-        if (has[0]) {
-            const float* bb = bs + (c & 1) * kConvBK * BNs;
+    // ---- K loop: groups of 16 k (4 k-steps); weights stream from L2 into
+    // ping-pong registers (padded [K16+16][N16] copy: no bounds selects)
+    const int ngroups = K16 >> 4;
+    auto load_group = [&](int g, float (&dst)[4][NT]) {
+        const float* src = W + (long long)(g * 16 + krow) * N16 + kcol;
 #pragma unroll
-            for (int g = 0; g < kConvBK / 16; ++g) {
-                const int4 ko4 = *reinterpret_cast<const int4*>(koff + (c * (kConvBK / 16) + g) * 16 + krow * 4);
-                const int kov[4] = {ko4.x, ko4.y, ko4.z, ko4.w};
+        for (int u = 0; u < 4; ++u)
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int kr = g * 16 + u * 4 + krow;
-                    float bf[NT];
+            for (int j = 0; j < NT; ++j) dst[u][j] = src[u * 4 * N16 + j * 16];
+    };
+    auto compute = [&](int g, const float (&bw)[4][NT]) {
+        const int4 ko4 = *reinterpret_cast<const int4*>(koff + g * 16 + krow * 4);
+        const int kov[4] = {ko4.x, ko4.y, ko4.z, ko4.w};
+        float av[4][2];
 #pragma unroll
-                    for (int j = 0; j < NT; ++j) bf[j] = bb[kr * BNs + j * 16 + kcol];
-                    const float a0 = img[pb[0] + kov[u]];
+        for (int u = 0; u < 4; ++u) {
+            av[u][0] = img[pb[0] + kov[u]];
+            av[u][1] = img[pb[1] + kov[u]];
+        }
 #pragma unroll
-                    for (int j = 0; j < NT; ++j)
-                        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bf[j], acc[0][j], 0, 0, 0);
-                    if (has[1]) {
-                        const float a1 = img[pb[1] + kov[u]];
+        for (int u = 0; u < 4; ++u) {
 #pragma unroll
-                        for (int j = 0; j < NT; ++j)
-                            acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bf[j], acc[1][j], 0, 0, 0);
-                    }
-                }
+            for (int j = 0; j < NT; ++j)
+                acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][0], bw[u][j], acc[0][j], 0, 0, 0);
+            if (has[1]) {
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][1], bw[u][j], acc[1][j], 0, 0, 0);
             }
         }
-        if (more) store_b((c + 1) & 1);
-        __syncthreads();
+    };
+    float b0[4][NT], b1[4][NT];
+    load_group(0, b0);
+    for (int g = 0; g < ngroups; g += 2) {
+        // the +16-row slack keeps the one-past-the-end prefetch in bounds
+        load_group(g + 1, b1);
+        compute(g, b0);
+        if (g + 1 >= ngroups) break;
+        load_group(g + 2, b0);
+        compute(g + 1, b1);
     }
 
     // ---- epilogue: C/D map col = lane & 15, row = (lane >> 4) * 4 + r
@@ -295,19 +281,173 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
         for (int j = 0; j < NT; ++j) {
             const int n = j * 16 + kcol;
             if (n >= N) continue;
-            const float bv = bias ? bias[n] : 0.f;
+            const float bv = bias[n];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int m = mt * 16 + krow * 4 + r;
                 if (m >= M) continue;
                 const long long o = (pix0 + m) * N + n;
-                float v = acc[i][j][r];
-                if (OP == CONV2_DGRAD) {
-                    v = relu_mask[o] > 0.f ? v : 0.f;
-                } else {
-                    v = fmaxf(v + bv, 0.f);
-                }
-                out[o] = v;
+                out[o] = fmaxf(acc[i][j][r] + bv, 0.f);
+            }
+        }
+    }
+}
+
+// ============================================================================
+// Input gradient of conv2 (tap-major, halo-skipping):
+//   dz1[b][y][x][c] = (a1 > 0) * sum_{ky',kx',f} dz2pad[y+ky'][x+kx'][f] * w2t[(ky',kx',f)][c]
+// dz2pad is dz2 with a virtual zero halo of k-1; w2t the rotated weights.  Each
+// 16-pixel MFMA tile is a 4x4 spatial patch, so a tap whose receptive field lies
+// entirely in the halo for that patch is skipped (wave-uniform branch) -- the
+// padded formulation otherwise multiplies zeros for (H1/H2)^2 of its work.
+// One workgroup = (member, sample, output rows [y0, y0+R)), R = 4 or 8;
+// K loop = taps (one LDS weight slice of F4 rows per tap, double-buffered).
+// ============================================================================
+template <int NT>
+__global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvItem* __restrict__ items) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const ConvItem it = items[blockIdx.x];
+    const Member& mb = a.mem[it.member];
+    const int k = mb.k, F = mb.F, H2 = mb.H2, Ho = mb.H1;
+    const int pad = k - 1;
+    const int Wp = H2 + 2 * pad;
+    const int F4 = (F + 3) & ~3;
+    const int Fp = dgrad_fp(F);
+    const int N = F;
+    const int R = it.R, y0 = it.y0;
+    const int rows = R + k - 1;
+    const float* in = a.act + mb.dz2 + (long long)it.b * H2 * H2 * F;
+    const float* W = a.act + mb.w2t;
+    float* out = a.act + mb.dz1 + (long long)it.b * Ho * Ho * F;
+    const float* relu_mask = a.act + mb.a1 + (long long)it.b * Ho * Ho * F;
+
+    float* img = smem;  // [rows][Wp][Fp], channels >= F zero (+16 floats of slack)
+    const int img_elems = rows * Wp * Fp + 16;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: tile logic stays scalar
+    const int krow = lane >> 4, kcol = lane & 15;
+
+    for (int e = tid; e < img_elems; e += 256) img[e] = 0.f;
+    __syncthreads();
+    for (int r = 0; r < rows; ++r) {
+        const int gy = y0 + r - pad;
+        if (gy < 0 || gy >= H2) continue;
+        stage_row(in + (long long)gy * H2 * F, img + (r * Wp + pad) * Fp, H2 * F, F, Fp, tid);
+    }
+
+    // ---- this wave's 4x4 tiles, their tap rectangles and the wave's union rectangle
+    const int CT = (Ho + 3) >> 2;
+    const int bands = (R + 3) >> 2;
+    const int T = bands * CT;
+    int pb[4], kylo[4], kyhi[4], kxlo[4], kxhi[4];
+    bool has[4];
+    int uy0 = k, uy1 = 0, ux0 = k, ux1 = 0;
+    const int dy = (lane & 15) >> 2, dx = lane & 3;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int ti = wave + 4 * i;
+        has[i] = ti < T;
+        const int band = ti / CT, ct = ti - band * CT;
+        const int ty0 = y0 + 4 * band, tx0 = 4 * ct;
+        const int ty1 = min(ty0 + 4, y0 + R), tx1 = min(tx0 + 4, Ho);
+        kylo[i] = max(0, pad - (ty1 - 1));
+        kyhi[i] = min(k, pad + H2 - ty0);
+        kxlo[i] = max(0, pad - (tx1 - 1));
+        kxhi[i] = min(k, pad + H2 - tx0);
+        if (has[i]) {
+            uy0 = min(uy0, kylo[i]); uy1 = max(uy1, kyhi[i]);
+            ux0 = min(ux0, kxlo[i]); ux1 = max(ux1, kxhi[i]);
+        }
+        const int y = ty0 + dy, x = tx0 + dx;
+        pb[i] = (y < ty1 && x < tx1) ? ((y - y0) * Wp + x) * Fp : 0;
+    }
+    f32x4 acc[4][NT];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();  // image staged; no further barriers
+
+    // Weight fragments straight from L2: group = (tap, 16-channel block), 4 k-steps;
+    // ping-pong register buffers (loop unrolled by two), loads unconditional.
+    const int CB = (F4 + 15) >> 4;
+    const int nx = ux1 - ux0;
+    const int ngroups = (uy1 > uy0 && nx > 0) ? (uy1 - uy0) * nx * CB : 0;
+    constexpr int N16 = NT * 16;
+    auto load_group = [&](int ky, int kx, int cb, float (&dst)[4][NT]) {
+        // w2t is [k*k][F4][N16], zero padded (+16 rows of slack): no bounds select,
+        // so the loads stay in flight until the MFMAs of the group consume them
+        const float* src = W + ((long long)(ky * k + kx) * F4 + cb * 16 + krow) * N16 + kcol;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) dst[u][j] = src[u * 4 * N16 + j * 16];
+    };
+    auto advance = [&](int& ky, int& kx, int& cb) {
+        if (++cb == CB) { cb = 0; if (++kx == ux1) { kx = ux0; ++ky; } }
+    };
+    auto compute = [&](int ky, int kx, int cb, const float (&bw)[4][NT]) {
+        bool live[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            live[i] = has[i] && ky >= kylo[i] && ky < kyhi[i] && kx >= kxlo[i] && kx < kxhi[i];
+        const int toff = (ky * Wp + kx) * Fp + cb * 16 + krow;
+        float av[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) av[u][i] = img[pb[i] + toff + u * 4];
+        const int nu = min(4, (F4 - cb * 16) >> 2);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (u >= nu) break;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (!live[i]) continue;
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][i], bw[u][j], acc[i][j], 0, 0, 0);
+            }
+        }
+    };
+    float b0[4][NT], b1[4][NT];
+    int cky = uy0, ckx = ux0, ccb = 0;   // group g
+    int nky = uy0, nkx = ux0, ncb = 0;   // group g + 1
+    if (ngroups) {
+        load_group(cky, ckx, ccb, b0);
+        advance(nky, nkx, ncb);
+    }
+    for (int g = 0; g < ngroups; g += 2) {
+        if (g + 1 < ngroups) load_group(nky, nkx, ncb, b1);
+        compute(cky, ckx, ccb, b0);
+        if (g + 1 >= ngroups) break;
+        cky = nky; ckx = nkx; ccb = ncb;
+        advance(nky, nkx, ncb);
+        if (g + 2 < ngroups) load_group(nky, nkx, ncb, b0);
+        compute(cky, ckx, ccb, b1);
+        cky = nky; ckx = nkx; ccb = ncb;
+        advance(nky, nkx, ncb);
+    }
+
+    // ---- epilogue: accumulator row p = krow*4 + r is tile pixel (p>>2, p&3)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (!has[i]) continue;
+        const int ti = wave + 4 * i;
+        const int band = ti / CT, ct = ti - band * CT;
+        const int ty0 = y0 + 4 * band, tx0 = 4 * ct;
+        const int ty1 = min(ty0 + 4, y0 + R), tx1 = min(tx0 + 4, Ho);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int n = j * 16 + kcol;
+            if (n >= N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int p = krow * 4 + r;
+                const int y = ty0 + (p >> 2), x = tx0 + (p & 3);
+                if (y >= ty1 || x >= tx1) continue;
+                const long long o = ((long long)y * Ho + x) * N + n;
+                out[o] = relu_mask[o] > 0.f ? acc[i][j][r] : 0.f;
             }
         }
     }
@@ -336,18 +476,19 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(StepArgs a, const WgIte
     }
     const int N = F;
     const int Kw = k * k * Cin;  // weight rows; row Kw is the bias gradient (an all-ones A row)
-    const int Fp = odd_stride(Cin);
+    const int Fp = wg_fp(Cin);
     constexpr int Fq = NT * 16 + ((NT & 1) ? 0 : 16);
     const int R = it.R;
     const int P = R * Ho;
-    const int P4 = (P + 3) & ~3;
+    const int P4 = (P + 15) & ~15;   // pixel rows padded to whole 16-pixel read groups
     const int rows = R + k - 1;
     float* img = smem;                                   // [rows][Hin][Fp]
     const int img_elems = rows * Hin * Fp;
     float* dl = smem + ((img_elems + 3) & ~3);            // [P4][Fq]
     int* poff = reinterpret_cast<int*>(dl + P4 * Fq);     // [P4]
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int krow = lane >> 4, kcol = lane & 15;
 
     int toff[4];
@@ -417,18 +558,28 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(StepArgs a, const WgIte
             __syncthreads();
             if (!has[0]) continue;
             const int pc4 = (pcnt + 3) & ~3;
-            for (int ks = 0; ks < pc4; ks += 4) {
-                const int po = poff[ks + krow];
-                float bf[NT];
+            const int p16 = (pc4 + 15) & ~15;   // poff/dl are padded to 16 pixels
+            for (int ks0 = 0; ks0 < p16; ks0 += 16) {
+                float bf[4][NT], av[4][4];
 #pragma unroll
-                for (int j = 0; j < NT; ++j) bf[j] = dl[(ks + krow) * Fq + j * 16 + kcol];
+                for (int u = 0; u < 4; ++u) {
+                    const int ks = ks0 + 4 * u;
+                    const int po = poff[ks + krow];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if (!has[i]) break;   // tiles are assigned in order: has[] is a prefix
-                    const float av = ones[i] ? 1.f : img[toff[i] + po];
+                    for (int j = 0; j < NT; ++j) bf[u][j] = dl[(ks + krow) * Fq + j * 16 + kcol];
 #pragma unroll
-                    for (int j = 0; j < NT; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bf[j], acc[i][j], 0, 0, 0);
+                    for (int i = 0; i < 4; ++i) av[u][i] = ones[i] ? 1.f : img[toff[i] + po];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (ks0 + 4 * u >= pc4) break;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        if (!has[i]) break;   // tiles are assigned in order: has[] is a prefix
+#pragma unroll
+                        for (int j = 0; j < NT; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][i], bf[u][j], acc[i][j], 0, 0, 0);
+                    }
                 }
             }
         }
@@ -470,21 +621,40 @@ __global__ void wgrad_reduce_kernel(StepArgs a, const MItem* __restrict__ items,
     }
 }
 
-// w2t[(ky', kx', f)][c] = w2[(k-1-ky', k-1-kx', c)][f]: weights of the input-gradient conv.
+// w2t[(ky', kx')][f][c] = w2[(k-1-ky', k-1-kx', c)][f]: weights of the input-gradient
+// conv, zero-padded to [k*k][F4][16*NT] so every dgrad fragment load is in bounds.
 __global__ void flip_w2_kernel(StepArgs a, const MItem* __restrict__ items) {
     const Member& mb = a.mem[items[blockIdx.y].member];
     const int k = mb.k, F = mb.F;
-    const long long S = (long long)k * k * F * F;
+    const int F4 = (F + 3) & ~3, N16 = mb.nt * 16;
+    const long long S = (long long)k * k * F4 * N16;
     const float* w2 = a.params + mb.w2;
     float* w2t = a.act + mb.w2t;
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < S; i += (long long)gridDim.x * blockDim.x) {
-        const int c = i % F;
-        const long long r = i / F;
-        const int f = r % F;
-        const int tap = r / F;
+        const int c = i % N16;
+        const long long r = i / N16;
+        const int f = r % F4;
+        const int tap = r / F4;
         const int ky = tap / k, kx = tap % k;
         const int src_tap = (k - 1 - ky) * k + (k - 1 - kx);
-        w2t[i] = w2[((long long)src_tap * F + c) * F + f];
+        w2t[i] = (f < F && c < F) ? w2[((long long)src_tap * F + c) * F + f] : 0.f;
+    }
+    // forward weights, zero-padded to [K16 + 16][N16]
+    const int K2 = k * k * F, K1 = k * k;
+    const long long S2 = (long long)(((K2 + 15) & ~15) + 16) * N16;
+    const long long S1 = (long long)(((K1 + 15) & ~15) + 16) * N16;
+    float* w2p = a.act + mb.w2p;
+    float* w1p = a.act + mb.w1p;
+    const float* w1 = a.params + mb.w1;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < S2; i += (long long)gridDim.x * blockDim.x) {
+        const int c = i % N16;
+        const long long r = i / N16;
+        w2p[i] = (r < K2 && c < F) ? w2[r * F + c] : 0.f;
+    }
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < S1; i += (long long)gridDim.x * blockDim.x) {
+        const int c = i % N16;
+        const long long r = i / N16;
+        w1p[i] = (r < K1 && c < F) ? w1[r * F + c] : 0.f;
     }
 }
 
@@ -822,16 +992,21 @@ struct Plan {
 };
 
 size_t conv_lds_bytes(int rows, int Wp, int Cin, int K, int nt) {
-    const int Fp = odd_stride(Cin);
-    const int img = align4(rows * Wp * Fp);
-    const int kp = (K + kConvBK - 1) / kConvBK * kConvBK;
-    return (size_t)(img + kp + 2 * kConvBK * bn_stride(nt)) * sizeof(float);
+    (void)nt;
+    const int Fp = fwd_fp(Cin);
+    return (size_t)(align4(rows * Wp * Fp) + ((K + 15) & ~15)) * sizeof(float);
+}
+
+size_t dgrad_lds_bytes(int R, int k, int F, int nt) {
+    (void)nt;
+    const int Wp = kImg;  // H2 + 2(k-1) == 28
+    return (size_t)align4((R + k - 1) * Wp * dgrad_fp(F) + 16) * sizeof(float);
 }
 
 size_t wg_lds_bytes(int rows, int Hin, int Cin, int P, int nt) {
-    const int Fp = odd_stride(Cin);
+    const int Fp = wg_fp(Cin);
     const int img = align4(rows * Hin * Fp);
-    const int P4 = (P + 3) & ~3;
+    const int P4 = (P + 15) & ~15;
     return (size_t)(img + P4 * dout_stride(nt) + P4) * sizeof(float);
 }
 
@@ -908,7 +1083,9 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         m.dp = aalloc((long long)B * m.K1);
         m.dz2 = aalloc((long long)B * m.H2 * m.H2 * F);
         m.dz1 = aalloc((long long)B * m.H1 * m.H1 * F);
-        m.w2t = aalloc((long long)k * k * F * F);
+        m.w2t = aalloc((long long)(k * k * ((F + 3) & ~3) + 16) * (m.nt * 16));
+        m.w1p = aalloc((long long)(((k * k + 15) & ~15) + 16) * (m.nt * 16));
+        m.w2p = aalloc((long long)(((k * k * F + 15) & ~15) + 16) * (m.nt * 16));
         m.wp1 = aalloc((long long)m.g1 * (k * k + 1) * F);
         m.wp2 = aalloc((long long)m.g2 * (k * k * F + 1) * F);
     }
@@ -921,10 +1098,11 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         const int k = m.k, F = m.F, nt = m.nt;
         const int R1 = choose_rows(m.H1, [&](int R) { return conv_lds_bytes(R + k - 1, kImg, 1, k * k, nt); });
         const int R2 = choose_rows(m.H2, [&](int R) { return conv_lds_bytes(R + k - 1, m.H1, F, k * k * F, nt); });
-        const int Rd = choose_rows(m.H1, [&](int R) { return conv_lds_bytes(R + k - 1, m.H2 + 2 * (k - 1), F, k * k * F, nt); });
+        // dgrad: 4x4-pixel tiles in bands of 4 rows; 8-row chunks unless only 4 fit 2 blocks/CU
+        const int Rd = (dgrad_lds_bytes(8, k, F, nt) <= ((size_t)78 << 10) || dgrad_lds_bytes(4, k, F, nt) > ((size_t)78 << 10)) ? 8 : 4;
         const size_t l1 = conv_lds_bytes(R1 + k - 1, kImg, 1, k * k, nt);
         const size_t l2 = conv_lds_bytes(R2 + k - 1, m.H1, F, k * k * F, nt);
-        const size_t ld = conv_lds_bytes(Rd + k - 1, m.H2 + 2 * (k - 1), F, k * k * F, nt);
+        const size_t ld = dgrad_lds_bytes(Rd, k, F, nt);
         P.bc1.lds[nt] = std::max(P.bc1.lds[nt], l1);
         P.bc2.lds[nt] = std::max(P.bc2.lds[nt], l2);
         P.bdg.lds[nt] = std::max(P.bdg.lds[nt], ld);
@@ -1038,6 +1216,25 @@ hipError_t launch_conv(const Plan& P, const StepArgs& a, size_t table_off, const
     return launch_conv_nt<OP, 4>(a, base + bk.begin[4], bk.end[4] - bk.begin[4], bk.lds[4], s);
 }
 
+template <int NT>
+hipError_t launch_dgrad_nt(const StepArgs& a, const ConvItem* items, int count, size_t lds, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    auto kern = conv_dgrad_kernel<NT>;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(count), dim3(256), lds, s, a, items);
+    return hipGetLastError();
+}
+
+hipError_t launch_dgrad(const Plan& P, const StepArgs& a, hipStream_t s) {
+    const ConvItem* base = dev_table<ConvItem>(P, P.off_dgrad);
+    const Bucketed& bk = P.bdg;
+    hipError_t e;
+    if ((e = launch_dgrad_nt<1>(a, base + bk.begin[1], bk.end[1] - bk.begin[1], bk.lds[1], s))) return e;
+    if ((e = launch_dgrad_nt<2>(a, base + bk.begin[2], bk.end[2] - bk.begin[2], bk.lds[2], s))) return e;
+    if ((e = launch_dgrad_nt<3>(a, base + bk.begin[3], bk.end[3] - bk.begin[3], bk.lds[3], s))) return e;
+    return launch_dgrad_nt<4>(a, base + bk.begin[4], bk.end[4] - bk.begin[4], bk.lds[4], s);
+}
+
 template <int OP, int NT>
 hipError_t launch_wg_nt(const StepArgs& a, const WgItem* items, int count, size_t lds, hipStream_t s) {
     if (count <= 0) return hipSuccess;
@@ -1086,6 +1283,9 @@ StepArgs make_args(const Plan& P, const float* x, const int* labels, const int* 
 }
 
 int forward(const Plan& P, const StepArgs& a, hipStream_t s) {
+    // padded / rotated weight copies for this step's convolutions
+    hipLaunchKernelGGL(flip_w2_kernel, dim3(64, (unsigned)P.n), dim3(256), 0, s, a, dev_table<MItem>(P, P.off_pm));
+    MPO_LAUNCH_CHECK();
     MPO_HIP(launch_conv<CONV1_FWD>(P, a, P.off_conv1, P.bc1, s));
     MPO_HIP(launch_conv<CONV2_FWD>(P, a, P.off_conv2, P.bc2, s));
     hipLaunchKernelGGL(pool_fwd_kernel, dim3((unsigned)P.per_sample.size()), dim3(256), 0, s, a,
@@ -1190,9 +1390,7 @@ int mpo_pop_train_step(void* handle, const float* x, const int32_t* labels, cons
     hipLaunchKernelGGL(pool_bwd_kernel, dim3((unsigned)P.per_sample.size()), dim3(256), 0, s, a,
                        dev_table<MItem>(P, P.off_ps));
     MPO_LAUNCH_CHECK();
-    hipLaunchKernelGGL(flip_w2_kernel, dim3(64, (unsigned)P.n), dim3(256), 0, s, a, dev_table<MItem>(P, P.off_pm));
-    MPO_LAUNCH_CHECK();
-    MPO_HIP(launch_conv<CONV2_DGRAD>(P, a, P.off_dgrad, P.bdg, s));
+    MPO_HIP(launch_dgrad(P, a, s));
     MPO_HIP(launch_wg<WG_CONV2>(P, a, P.off_wg2, P.bw2, s));
     MPO_HIP(launch_wg<WG_CONV1>(P, a, P.off_wg1, P.bw1, s));
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)P.wred_blocks, (unsigned)P.wred.size()), dim3(256), 0, s, a,
