@@ -82,15 +82,15 @@ def cpu_baseline_ei(n=200, d=10, sample=150_000):
 
 
 def bench_ei(args, torch, dist, ws, rank, dev):
-    from oracle import gp_ei as O  # noqa: F401  (only for the fixed synthetic recipe)
+    from mpi_opt_amd import synthetic
     from mpi_opt_amd.gp import DeviceGP
 
     n, d, m, k = 200, 10, args.candidates, 5
-    X, y = O.synthetic_problem(n, d, 0)
+    X, y = synthetic.gp_problem(n, d, 0)
     # hyper-parameters as fitted by sklearn on this data (tests/golden/gp_ei_n200_d10.npz)
     ls = np.array([16.2, 1.91, 1.65, 9.84, 1.84, 2.94, 2.45, 9.09, 8.13, 1.94])
     g = DeviceGP(X, y, 17.4955, ls, 0.0465, device=dev)
-    cand = torch.from_numpy(O.synthetic_candidates(m, d, seed=1 + rank)).to(dev)
+    cand = torch.from_numpy(synthetic.gp_candidates(m, d, seed=1 + rank)).to(dev)
     y_opt = float(np.min(y))
     torch.cuda.synchronize(dev)
 
@@ -166,13 +166,137 @@ def bench_ei(args, torch, dist, ws, rank, dev):
     return res
 
 
+def sample_trials(n, seed):
+    """Trials drawn from the option3 mnist space (option3:127-131): nb_filters,
+    pool_size, kernel_size, dense (the dead `dropout` dimension trains at 0.25)."""
+    from mpi_opt_amd.population import TrialSpec
+
+    rng = np.random.RandomState(seed)
+    return [TrialSpec(nb_filters=int(rng.randint(10, 51)), pool_size=int(rng.randint(2, 11)),
+                      kernel_size=int(rng.randint(2, 11)), dense=int(rng.randint(50, 201)), seed=i)
+            for i in range(n)]
+
+
+def cpu_baseline_train(trials, budget_s=12.0):
+    """fp64 numpy restatement (oracle/cnn.py) of single-trial training on the host,
+    timed on a bounded sample of train steps and extrapolated to whole trials
+    (5-fold, 10 epochs, 60k samples: 24 000 train steps + 6 000 validation batches)."""
+    from oracle import cnn as C
+    from mpi_opt_amd.population import glorot_uniform_init
+
+    rng = np.random.RandomState(5)
+    x = rng.uniform(size=(100, 784)).astype(np.float32)
+    y = rng.randint(0, 10, size=100)
+    t_tr, t_ev, n = 0.0, 0.0, 0
+    t_start = time.perf_counter()
+    for t in trials:
+        o = C.TrialOracle(t.nb_filters, t.kernel_size, t.pool_size, t.dense,
+                          {k: v.astype(np.float64) for k, v in glorot_uniform_init(t, 0).items()}, seed=1)
+        t0 = time.perf_counter()
+        o.train_step(x, y, 0)
+        t1 = time.perf_counter()
+        o.forward(x, y, train=False)
+        t2 = time.perf_counter()
+        t_tr += t1 - t0
+        t_ev += t2 - t1
+        n += 1
+        if time.perf_counter() - t_start > budget_s:
+            break
+    sec_per_trial = (24000 * t_tr + 6000 * t_ev) / n
+    cores = int(os.environ.get("OMP_NUM_THREADS", len(os.sched_getaffinity(0))))
+    return {"value": 3600.0 / sec_per_trial, "unit": "trials/hour", "cores": cores, "kind": "port",
+            "sample": f"1 train step + 1 validation batch (batch 100) of each of the first {n} sampled trials, "
+                      f"fp64 numpy restatement (oracle/cnn.py, BLAS threads = {cores}), extrapolated to "
+                      f"24000 train steps + 6000 validation batches per trial ({time.perf_counter() - t_start:.1f} s)"}
+
+
+def bench_train(args, torch, dist, ws, rank, dev):
+    from mpi_opt_amd.population import PopulationEngine, TrialSpec, kfold_split, synthetic_mnist
+
+    n_trials, n_fold, B = args.train_trials, 5, 100
+    trials = sample_trials(n_trials, seed=13579 + rank)
+    members, folds = [], []
+    for t in trials:
+        for f in range(n_fold):
+            members.append(TrialSpec(t.nb_filters, t.kernel_size, t.pool_size, t.dense, t.lr, t.dropout,
+                                     seed=len(members)))
+            folds.append(f)
+    eng = PopulationEngine(members, batch=B, device=dev)
+    x, yl = synthetic_mnist(60000, seed=rank, device=dev)
+    tr = np.stack([kfold_split(60000, n_fold, f)[0] for f in folds])
+    va = np.stack([kfold_split(60000, n_fold, f)[1] for f in folds])
+    otr = torch.from_numpy(tr).to(dev)
+    ova = torch.from_numpy(va).to(dev)
+    steps_per_epoch, val_batches = tr.shape[1] // B, va.shape[1] // B   # 480, 120
+    ratio = steps_per_epoch // val_batches                              # 4 train steps per val batch
+    state = {"st": 0, "vb": 0}
+
+    def macro_step():
+        for _ in range(ratio):
+            eng.train_step(x, yl, otr, (state["st"] % steps_per_epoch) * B)
+            state["st"] += 1
+        eng.eval_step(x, yl, ova, (state["vb"] % val_batches) * B)
+        state["vb"] += 1
+
+    for _ in range(args.train_warmup):
+        macro_step()
+    torch.cuda.synchronize(dev)
+    if ws > 1:
+        dist.barrier()
+    stream = torch.cuda.current_stream(dev)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.train_steps):
+        macro_step()
+    e1.record(stream)
+    if ws > 1:   # the per-BO-round exchange: all-gather of per-(trial, fold) validation losses
+        g = torch.empty(ws * len(members), dtype=torch.float32, device=dev)
+        dist.all_gather_into_tensor(g, eng.val_loss_sum)
+    torch.cuda.synchronize(dev)
+    if ws > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    t_gpu = e0.elapsed_time(e1) / 1e3
+    if ws > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    t_macro = dt / args.train_steps
+    macro_per_trial = steps_per_epoch // ratio * 10        # 120 macro-steps/epoch x 10 epochs
+    trials_per_hour = ws * n_trials * 3600.0 / (t_macro * macro_per_trial)
+    flops = (ratio * B * sum(m.flops_per_sample_train() for m in members)
+             + B * sum(m.flops_per_sample_fwd() for m in members))
+    achieved = flops / (t_gpu / args.train_steps) / 1e12
+    return {
+        "metric": "MNIST-CNN trials/hour (5-fold CV, 10 epochs, 60k samples/trial-fold split)",
+        "value": trials_per_hour, "unit": "trials/hour", "n_gpus": ws, "steps": args.train_steps,
+        "warmup": args.train_warmup, "ms_per_step": t_macro * 1e3, "scaling": "weak", "dtype": "f32",
+        "data": "synthetic MNIST-shape x~U[0,1] (60000x784 f32), uniform labels; glorot init",
+        "config": {"workload": f"BASELINE configs[2]/[3]: {n_trials} ragged test_mnist trials x {n_fold} folds "
+                               f"= {len(members)} population members per GPU; step = {ratio} train batches "
+                               f"+ 1 validation batch (1/{steps_per_epoch // ratio} epoch)",
+                   "trials_per_gpu": n_trials, "folds": n_fold, "batch": B, "epochs": 10,
+                   "parallelism": f"trials sharded, {ws} GPU(s), all-gather of fold losses"},
+        "roofline": {"kernel": "population step (all conv/dense MFMA kernels)", "bound": "mfma",
+                     "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None,
+                     "algorithmic_flops_per_step": flops},
+        "_trials": trials,
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="ei", choices=["ei"])
+    ap.add_argument("--workload", default="all", choices=["ei", "train", "all"])
     ap.add_argument("--candidates", type=int, default=1_000_000)
+    ap.add_argument("--train-trials", type=int, default=64)
+    ap.add_argument("--train-steps", type=int, default=5)
+    ap.add_argument("--train-warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -189,12 +313,19 @@ def main():
     if ws == 1 and args.gpus != 1:
         print(f"warning: --gpus {args.gpus} without torch.distributed.run; running 1 GPU", file=sys.stderr)
 
-    res = bench_ei(args, torch, dist, ws, rank, dev)
+    res = bench_ei(args, torch, dist, ws, rank, dev) if args.workload in ("ei", "all") else None
+    train = bench_train(args, torch, dist, ws, rank, dev) if args.workload in ("train", "all") else None
     if rank == 0:
-        if ws == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline_ei()
+        cpu = ws == 1 and not args.no_cpu_baseline
+        if train is not None:
+            trials = train.pop("_trials")
+            train["cpu_baseline"] = cpu_baseline_train(trials) if cpu else None
+        if res is None:
+            res, train = train, None
         else:
-            res["cpu_baseline"] = None
+            res["cpu_baseline"] = cpu_baseline_ei() if cpu else None
+            if train is not None:
+                res["train"] = train
         print(json.dumps(res), flush=True)
     if ws > 1:
         dist.barrier()
