@@ -1,0 +1,244 @@
+"""Trial evaluation: the replacement for ProcessBlock + mpi_learn.
+
+Reference (/root/reference/process_block.py:9-121): every block of MPI ranks
+loops barrier -> recv params from rank 0 -> build the Keras model ->
+``MPIKFoldManager(...).train()`` -> ``figure_of_merit()`` -> record details ->
+``isend`` the FOM to rank 0.  Here:
+
+* :class:`TrialEvaluator` trains a *batch* of trials x folds as one device
+  population (:class:`~mpi_opt_amd.population.PopulationEngine`) and returns one
+  FOM per trial: the fold-averaged validation loss after the last epoch (the
+  ``hist["history"]["0"]["val_loss"][-1]`` convention of option0:71-82),
+  non-finite losses clamped to the clipped-BCE ceiling 16.12 (a diverged trial
+  must never hang or poison the GP);
+* :class:`PopulationComm` is an MPI-communicator stand-in for the unchanged
+  :class:`~mpi_opt_amd.coordinator.Coordinator`: ``send`` records the
+  parameters each rank of a block receives (tag 4), ``irecv`` from a block
+  master returns a request whose ``test()`` answers "not done" while some block
+  is still idle and, once every block is busy, trains all launched blocks
+  together -- the blocks the reference runs concurrently on MPI ranks run
+  concurrently as population members on the GPU;
+* :class:`DistributedEvaluator` shards (trial, fold) units over the ranks of a
+  torch.distributed group (RCCL over xGMI) by longest-processing-time on the
+  per-unit FLOPs, with no data-path collective: rank 0 broadcasts the batch of
+  suggestions, every rank trains its shard, the per-unit FOMs are all-gathered.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import math
+import os
+
+import numpy as np
+
+from .tag_lookup import tag_lookup
+
+FOM_CEILING = -math.log(1e-7)   # clipped binary cross-entropy cannot exceed this
+
+
+def lpt_assign(costs, n_bins):
+    """Longest-processing-time-first: returns bin index per item."""
+    order = sorted(range(len(costs)), key=lambda i: -costs[i])
+    load = [0.0] * n_bins
+    out = [0] * len(costs)
+    for i in order:
+        b = min(range(n_bins), key=lambda j: (load[j], j))
+        out[i] = b
+        load[b] += costs[i]
+    return out
+
+
+class TrialEvaluator:
+    """Trains trials (parameter lists of ``model_provider``'s space) on one GPU."""
+
+    def __init__(self, model_provider, x, y, n_fold=1, epochs=10, batch=100, lr=1e-3, device=None,
+                 history_dir=None, init_seed=0):
+        self.model_provider = model_provider
+        self.x, self.y = x, y
+        self.n_fold, self.epochs, self.batch, self.lr = n_fold, epochs, batch, lr
+        self.device = device
+        self.history_dir = history_dir
+        self.init_seed = init_seed
+        self.n_evaluated = 0
+
+    def units(self, params_list):
+        """(trial index, fold) pairs with their training FLOPs (LPT cost)."""
+        out = []
+        folds = max(1, self.n_fold)
+        for t, params in enumerate(params_list):
+            spec = self.model_provider.builder(*params).spec(lr=self.lr)
+            cost = spec.flops_per_sample_train()
+            for f in range(folds):
+                out.append((t, f, spec, cost))
+        return out
+
+    def train_units(self, units, seed_base=0):
+        """Train the given (trial, fold, spec) units as one population; returns
+        {(trial, fold): history dict}."""
+        from .population import PopulationEngine, TrialSpec
+
+        if not units:
+            return {}
+        from .population import glorot_uniform_init
+
+        specs, folds, init = [], [], []
+        for (t, f, spec, _) in units:
+            # seeds depend on the unit's identity only, never on how units are
+            # sharded or batched: results are independent of the world size
+            uid = (self.init_seed + 1000003 * (seed_base + t) + f) & 0x7FFFFFFF
+            s = TrialSpec(spec.nb_filters, spec.kernel_size, spec.pool_size, spec.dense, spec.lr, spec.dropout,
+                          seed=uid)
+            specs.append(s)
+            folds.append(f)
+            init.append(glorot_uniform_init(s, uid))
+        eng = PopulationEngine(specs, batch=self.batch, device=self.device, init=init)
+        hist = eng.fit_folds(self.x, self.y, folds, self.n_fold, self.epochs)
+        out = {}
+        for i, (t, f, _, _) in enumerate(units):
+            out[(t, f)] = {"val_loss": [float(v) for v in hist["val_loss"][i]],
+                           "val_acc": [float(v) for v in hist["val_acc"][i]]}
+        return out
+
+    def foms(self, params_list, results):
+        folds = max(1, self.n_fold)
+        foms = []
+        for t, params in enumerate(params_list):
+            vals = [results[(t, f)]["val_loss"][-1] for f in range(folds)]
+            fom = float(np.mean(vals))
+            if not math.isfinite(fom):
+                fom = FOM_CEILING
+            foms.append(fom)
+            self._record(params, [results[(t, f)] for f in range(folds)])
+        return foms
+
+    def evaluate(self, params_list):
+        units = self.units(params_list)
+        results = self.train_units(units, seed_base=self.n_evaluated)
+        self.n_evaluated += len(params_list)
+        return self.foms(params_list, results)
+
+    def _record(self, params, fold_hists):
+        """Per-trial history JSON in the schema option0/1 parse (process_block.py:93-94)."""
+        if not self.history_dir:
+            return
+        os.makedirs(self.history_dir, exist_ok=True)
+        h = hashlib.md5(json.dumps([float(p) if not isinstance(p, str) else p for p in params]).encode()).hexdigest()
+        doc = {"history": {str(i): fh for i, fh in enumerate(fold_hists)},
+               "meta": {"parameters": [float(p) for p in params], "fold": len(fold_hists)}}
+        with open(os.path.join(self.history_dir, f"{h}.json"), "w") as f:
+            json.dump(doc, f)
+
+
+class _Request:
+    def __init__(self, comm, block):
+        self.comm, self.block = comm, block
+
+    def test(self):
+        c = self.comm
+        if self.block not in c.results:
+            if len(c.busy) < c.num_blocks:
+                return False, None      # another block is idle: let the coordinator fill it first
+            c.evaluate_pending()
+        c.busy.discard(self.block)
+        return True, c.results.pop(self.block)
+
+
+class PopulationComm:
+    """MPI-communicator stand-in for :class:`Coordinator` (size = 1 + blocks x block_size)."""
+
+    def __init__(self, num_blocks, block_size, evaluator):
+        self.num_blocks, self.block_size, self.evaluator = num_blocks, block_size, evaluator
+        self.received = {}       # rank -> last params
+        self.pending = {}        # block -> params launched, not yet trained
+        self.results = {}        # block -> fom
+        self.exited = set()
+        self.busy = set()        # launched blocks whose result has not been collected
+        self.batches = []        # sizes of the populations trained
+
+    def Get_size(self):
+        return 1 + self.num_blocks * self.block_size
+
+    def Get_rank(self):
+        return 0
+
+    def _block_of(self, rank):
+        return (rank - 1) // self.block_size + 1
+
+    def send(self, obj, dest, tag):
+        if tag != tag_lookup("params"):
+            raise ValueError(f"unexpected tag {tag}")
+        if obj is None:
+            self.exited.add(dest)
+            return
+        self.received[dest] = list(obj)
+        b = self._block_of(dest)
+        first = (b - 1) * self.block_size + 1
+        ranks = range(first, first + self.block_size)
+        if all(self.received.get(r) == list(obj) for r in ranks):
+            self.pending[b] = list(obj)
+            self.busy.add(b)
+
+    def irecv(self, source, tag):
+        if tag != tag_lookup("result"):
+            raise ValueError(f"unexpected tag {tag}")
+        return _Request(self, self._block_of(source))
+
+    def evaluate_pending(self):
+        blocks = sorted(self.pending)
+        params = [self.pending.pop(b) for b in blocks]
+        foms = self.evaluator.evaluate(params)
+        self.batches.append(len(params))
+        for b, f in zip(blocks, foms):
+            self.results[b] = f
+
+    def Barrier(self):
+        pass
+
+
+class DistributedEvaluator:
+    """Shards (trial, fold) units over torch.distributed ranks; rank 0 drives."""
+
+    def __init__(self, local, group=None):
+        import torch.distributed as dist
+
+        self.local = local
+        self.dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.n_evaluated = 0
+
+    def _round(self, params_list):
+        dist = self.dist
+        box = [params_list]
+        dist.broadcast_object_list(box, src=0, group=self.group)
+        params_list = box[0]
+        if params_list is None:
+            return None
+        units = self.local.units(params_list)
+        owner = lpt_assign([u[3] for u in units], self.world)
+        mine = [u for u, o in zip(units, owner) if o == self.rank]
+        res = self.local.train_units(mine, seed_base=self.n_evaluated)
+        self.n_evaluated += len(params_list)
+        gathered = [None] * self.world
+        dist.all_gather_object(gathered, {k: v for k, v in res.items()}, group=self.group)
+        merged = {}
+        for g in gathered:
+            merged.update(g)
+        return params_list, merged
+
+    def evaluate(self, params_list):
+        """Rank 0: evaluate a batch over all ranks."""
+        out = self._round(list(params_list))
+        params_list, merged = out
+        return self.local.foms(params_list, merged)
+
+    def serve(self):
+        """Ranks > 0: train shards until rank 0 sends None."""
+        while self._round(None) is not None:
+            pass
+
+    def shutdown(self):
+        if self.rank == 0:
+            self._round(None)

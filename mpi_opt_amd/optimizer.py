@@ -1,0 +1,317 @@
+"""Bayesian optimizer with the ``skopt.Optimizer`` interface the reference drives.
+
+The reference constructs ``skopt.Optimizer(dimensions=..., random_state=13579)``
+(/root/reference/coordinator.py:33) and calls ``ask(n)`` (:49), ``tell(X, Y)``
+(:69) and pickles it (:52-61); threaded_skopt.py:162-171 shows the same class
+with explicit ``base_estimator``/``acq_func``/``acq_optimizer``.  scikit-optimize
+is un-vendored and unpinned; its published ``Optimizer`` algorithm is restated:
+
+* ``n_initial_points`` (10) random points, then a GP surrogate
+  ``C(1,(0.01,1000)) * Matern(ones(D),(0.01,100),nu=2.5) + White``,
+  ``normalize_y=True``, ``n_restarts_optimizer=2`` (``cook_estimator("GP")``);
+* acquisition ``gp_hedge`` over {EI, LCB, PI} (xi=0.01, kappa=1.96), each
+  scored on ``n_points=10000`` random candidates, the best
+  ``n_restarts_optimizer=5`` polished with L-BFGS-B (maxiter 20) -- the
+  ``acq_optimizer="auto"`` -> ``"lbfgs"`` path -- and one of the three picked by
+  softmax(gains) (``eta=1``) with a multinomial draw;
+* ``ask(n, strategy="cl_min")`` = constant-liar batch through a copy.
+
+MI355X mapping: the candidate scoring (posterior + EI/PI/LCB + top-k over the
+candidate batch) runs in ``libmpo.so`` on the GPU (:class:`~mpi_opt_amd.gp.DeviceGP`),
+together with the GP factorisation.  The LML hyper-parameter search (sklearn's
+L-BFGS-B on ~15 parameters) and the 5 x 20-iteration polish of single points stay
+on the host -- they are the reference's host-side control flow, not the
+per-candidate hot path (SURVEY §8f rank 1 moves the LML fit on device next).
+"""
+from __future__ import annotations
+
+import copy as _copy
+import math
+
+import numpy as np
+from scipy.optimize import fmin_l_bfgs_b
+from scipy.stats import norm
+
+from .space import Space, check_random_state
+
+SQRT5 = math.sqrt(5.0)
+
+
+# --------------------------------------------------------------------------
+# GP hyper-parameter fit (host, sklearn -- the arithmetic base skopt subclasses)
+# --------------------------------------------------------------------------
+def fit_gp_hyperparameters(Xt, y, random_state=None, n_restarts_optimizer=2):
+    """skopt's GP fit: sklearn GaussianProcessRegressor with the cook_estimator
+    kernel + WhiteKernel, normalize_y.  Returns (amp, length_scale, noise)."""
+    from sklearn.gaussian_process import GaussianProcessRegressor
+    from sklearn.gaussian_process.kernels import ConstantKernel, Matern, WhiteKernel
+
+    D = Xt.shape[1]
+    kern = ConstantKernel(1.0, (0.01, 1000.0)) * Matern(
+        length_scale=np.ones(D), length_scale_bounds=[(0.01, 100)] * D, nu=2.5) + WhiteKernel()
+    gpr = GaussianProcessRegressor(kernel=kern, normalize_y=True, n_restarts_optimizer=n_restarts_optimizer,
+                                   random_state=random_state)
+    gpr.fit(Xt, y)
+    p = gpr.kernel_.get_params()
+    return float(p["k1__k1__constant_value"]), np.atleast_1d(p["k1__k2__length_scale"]).astype(float), \
+        float(p["k2__noise_level"])
+
+
+class GPModel:
+    """A fitted surrogate: hyper-parameters + its device posterior (rebuilt lazily,
+    so the model pickles without device state)."""
+
+    def __init__(self, Xt, y, amp, length_scale, noise, device=None):
+        self.Xt = np.asarray(Xt, dtype=float)
+        self.y = np.asarray(y, dtype=float)
+        self.amp, self.length_scale, self.noise = float(amp), np.asarray(length_scale, float), float(noise)
+        self.device = device
+        self._dev = None
+        self._host = None
+
+    def __getstate__(self):
+        d = dict(self.__dict__)
+        d["_dev"] = None
+        d["_host"] = None
+        return d
+
+    @property
+    def dev(self):
+        if self._dev is None:
+            from .gp import DeviceGP
+
+            self._dev = DeviceGP(self.Xt, self.y, self.amp, self.length_scale, self.noise, device=self.device)
+        return self._dev
+
+    # host copy of the (small) factor, for single-point predictions with gradients
+    def _host_state(self):
+        if self._host is None:
+            g = self.dev
+            self._host = (g.L_inverse().cpu().numpy(), g.alpha().cpu().numpy(), g.y_mean, g.y_std)
+        return self._host
+
+    def predict_grad(self, x):
+        """mu, sd and their gradients at one transformed point (skopt
+        GaussianProcessRegressor.predict(return_mean_grad, return_std_grad))."""
+        W, alpha, y_mean, y_std = self._host_state()
+        ls2 = self.length_scale ** 2
+        diff = x[None, :] - self.Xt                       # (n, d)
+        r = np.sqrt(np.sum(diff * diff / ls2, axis=1))
+        t = SQRT5 * r
+        e = np.exp(-t)
+        k = self.amp * (1.0 + t + t * t / 3.0) * e
+        dk = (-5.0 / 3.0) * self.amp * (1.0 + t)[:, None] * e[:, None] * diff / ls2   # dk/dx (n, d)
+        mu_n = k @ alpha
+        v = W @ k
+        var = self.amp - v @ v
+        sd_n = math.sqrt(var) if var > 0 else 0.0
+        mu = y_std * mu_n + y_mean
+        mu_grad = y_std * (dk.T @ alpha)
+        if sd_n > 0:
+            sd_grad = -y_std * (dk.T @ (W.T @ v)) / sd_n
+        else:
+            sd_grad = np.zeros_like(x)
+        return mu, sd_n * y_std, mu_grad, sd_grad
+
+    def predict_mean(self, X):
+        mu, _ = self.dev.predict(np.atleast_2d(X))
+        return mu
+
+
+def _acq_and_grad(model, x, y_opt, acq, xi, kappa):
+    """skopt gaussian_acquisition_1D: the minimised value and its gradient."""
+    mu, sd, mu_g, sd_g = model.predict_grad(np.asarray(x, dtype=float))
+    if acq == "LCB":
+        return mu - kappa * sd, mu_g - kappa * sd_g
+    if sd <= 0:
+        return 0.0, np.zeros_like(mu_g)
+    improve = y_opt - xi - mu
+    z = improve / sd
+    cdf, pdf = norm.cdf(z), norm.pdf(z)
+    improve_grad = (-mu_g * sd - sd_g * improve) / sd ** 2
+    if acq == "PI":
+        return -cdf, -(improve_grad * pdf)
+    ei = improve * cdf + sd * pdf
+    cdf_grad = improve_grad * pdf
+    pdf_grad = -improve * cdf_grad
+    grad = (-mu_g * cdf - pdf_grad) + (sd_g * pdf + pdf_grad)
+    return -ei, -grad
+
+
+class OptimizeResult(dict):
+    __getattr__ = dict.get
+
+    def __setattr__(self, k, v):
+        self[k] = v
+
+
+class Optimizer:
+    """Drop-in for ``skopt.Optimizer`` (GP base estimator, device acquisition)."""
+
+    def __init__(self, dimensions, base_estimator="gp", n_random_starts=None, n_initial_points=10,
+                 initial_point_generator="random", acq_func="gp_hedge", acq_optimizer="auto",
+                 random_state=None, model_queue_size=None, acq_func_kwargs=None, acq_optimizer_kwargs=None,
+                 device=None):
+        self.rng = check_random_state(random_state)
+        self.space = Space(dimensions)
+        if n_random_starts is not None:
+            n_initial_points = n_random_starts
+        if isinstance(base_estimator, str):
+            base_estimator = base_estimator.lower()
+        if base_estimator not in ("gp", "dummy"):
+            raise ValueError(f"base_estimator {base_estimator!r}: this build supports 'gp' and 'dummy'")
+        self.base_estimator_ = base_estimator
+        if acq_func not in ("gp_hedge", "EI", "PI", "LCB"):
+            raise ValueError(f"acq_func {acq_func!r} not supported")
+        self.acq_func = acq_func
+        self.acq_func_kwargs = dict(acq_func_kwargs or {})
+        self.eta = self.acq_func_kwargs.get("eta", 1.0)
+        if acq_optimizer == "auto":
+            acq_optimizer = "lbfgs"
+        if acq_optimizer not in ("lbfgs", "sampling"):
+            raise ValueError(f"acq_optimizer {acq_optimizer!r} not supported")
+        self.acq_optimizer = acq_optimizer
+        self.acq_optimizer_kwargs = dict(acq_optimizer_kwargs or {})
+        self.n_points = self.acq_optimizer_kwargs.get("n_points", 10000)
+        self.n_restarts_optimizer = self.acq_optimizer_kwargs.get("n_restarts_optimizer", 5)
+        self.n_initial_points_ = n_initial_points
+        self._n_initial_points = n_initial_points
+        self._initial_point_generator = initial_point_generator
+        self._initial_samples = None
+        self.model_queue_size = model_queue_size
+        self.device = device
+        self.cand_acq_funcs_ = ["EI", "LCB", "PI"] if acq_func == "gp_hedge" else [acq_func]
+        if acq_func == "gp_hedge":
+            self.gains_ = np.zeros(3)
+        self.Xi, self.yi, self.models = [], [], []
+        self.cache_ = {}
+
+    # ---- ask -------------------------------------------------------------------
+    def copy(self, random_state=None):
+        opt = Optimizer(self.space.dimensions, base_estimator=self.base_estimator_,
+                        n_initial_points=self.n_initial_points_,
+                        initial_point_generator=self._initial_point_generator, acq_func=self.acq_func,
+                        acq_optimizer=self.acq_optimizer, acq_func_kwargs=self.acq_func_kwargs,
+                        acq_optimizer_kwargs=self.acq_optimizer_kwargs, random_state=random_state,
+                        device=self.device)
+        opt._initial_samples = self._initial_samples
+        if hasattr(self, "gains_"):
+            opt.gains_ = np.copy(self.gains_)
+        if self.Xi:
+            opt._tell(self.Xi, self.yi)
+        return opt
+
+    def ask(self, n_points=None, strategy="cl_min"):
+        if n_points is None:
+            return self._ask()
+        if strategy not in ("cl_min", "cl_mean", "cl_max"):
+            raise ValueError(f"strategy {strategy!r}")
+        if (n_points, strategy) in self.cache_:
+            return self.cache_[(n_points, strategy)]
+        opt = self.copy(random_state=self.rng.randint(0, np.iinfo(np.int32).max))
+        X = []
+        for _ in range(n_points):
+            x = opt.ask()
+            X.append(x)
+            if strategy == "cl_min":
+                lie = np.min(opt.yi) if opt.yi else 0.0
+            elif strategy == "cl_mean":
+                lie = np.mean(opt.yi) if opt.yi else 0.0
+            else:
+                lie = np.max(opt.yi) if opt.yi else 0.0
+            opt._tell(x, lie)
+        self.cache_ = {(n_points, strategy): X}
+        return X
+
+    def _ask(self):
+        if self._n_initial_points > 0 or self.base_estimator_ == "dummy":
+            if self._initial_samples is None:
+                return self.space.rvs(random_state=self.rng)[0]
+            return self._initial_samples[len(self._initial_samples) - self._n_initial_points]
+        if not self.models:
+            raise RuntimeError("Random evaluations exhausted and no model has been fit.")
+        return self._next_x
+
+    # ---- tell ------------------------------------------------------------------
+    def tell(self, x, y, fit=True):
+        if len(x) and isinstance(x[0], (list, tuple, np.ndarray)):
+            if not np.ndim(y) == 1 or len(y) != len(x):
+                raise ValueError("tell: X and y must have matching lengths")
+        return self._tell(x, y, fit=fit)
+
+    def _tell(self, x, y, fit=True):
+        if len(x) and isinstance(x[0], (list, tuple, np.ndarray)):
+            self.Xi.extend([list(v) for v in x])
+            self.yi.extend([float(v) for v in y])
+            self._n_initial_points -= len(y)
+        else:
+            self.Xi.append(list(x))
+            self.yi.append(float(y))
+            self._n_initial_points -= 1
+        self.cache_ = {}
+        if fit and self._n_initial_points <= 0 and self.base_estimator_ == "gp":
+            self._fit_and_propose()
+        return self._result()
+
+    def _fit_and_propose(self):
+        Xt = self.space.transform(self.Xi)
+        y = np.asarray(self.yi, dtype=float)
+        seed = self.rng.randint(0, np.iinfo(np.int32).max)
+        amp, ls, noise = fit_gp_hyperparameters(Xt, y, random_state=seed)
+        est = GPModel(Xt, y, amp, ls, noise, device=self.device)
+        if hasattr(self, "next_xs_") and self.acq_func == "gp_hedge":
+            self.gains_ -= est.predict_mean(np.vstack(self.next_xs_))
+        if self.model_queue_size is None or self.model_queue_size > 0:
+            self.models.append(est)
+            if self.model_queue_size is not None and len(self.models) > self.model_queue_size:
+                self.models.pop(0)
+
+        X = self.space.transform(self.space.rvs(n_samples=self.n_points, random_state=self.rng))
+        y_opt = float(np.min(self.yi))
+        xi = self.acq_func_kwargs.get("xi", 0.01)
+        kappa = self.acq_func_kwargs.get("kappa", 1.96)
+        k = 1 if self.acq_optimizer == "sampling" else min(self.n_restarts_optimizer, X.shape[0])
+        scored = est.dev.score(X, y_opt, acqs=tuple(self.cand_acq_funcs_), xi=xi, kappa=kappa, k=k,
+                               want_mu_sd=False, want_values=False)
+        self.next_xs_ = []
+        for acq in self.cand_acq_funcs_:
+            idx = scored["topk"][acq][0].cpu().numpy()
+            if self.acq_optimizer == "sampling":
+                next_x = X[idx[0]]
+            else:
+                results = []
+                for i in idx:
+                    xr, fr, _ = fmin_l_bfgs_b(lambda v, a=acq: _acq_and_grad(est, v, y_opt, a, xi, kappa),
+                                              X[i], bounds=self.space.transformed_bounds, approx_grad=False,
+                                              maxiter=20)
+                    results.append((xr, fr))
+                cand_xs = np.array([r[0] for r in results])
+                cand_acqs = np.array([r[1] for r in results])
+                next_x = cand_xs[np.argmin(cand_acqs)]
+            self.next_xs_.append(np.clip(next_x, 0.0, 1.0))
+        if self.acq_func == "gp_hedge":
+            logits = np.array(self.gains_) - np.max(self.gains_)
+            probs = np.exp(self.eta * logits)
+            probs /= probs.sum()
+            next_x = self.next_xs_[int(np.argmax(self.rng.multinomial(1, probs)))]
+        else:
+            next_x = self.next_xs_[0]
+        self._next_x = self.space.inverse_transform(next_x.reshape(1, -1))[0]
+
+    def _result(self):
+        if not self.yi:
+            return OptimizeResult(x=None, fun=None, x_iters=[], func_vals=np.array([]), models=self.models,
+                                  space=self.space)
+        best = int(np.argmin(self.yi))
+        return OptimizeResult(x=list(self.Xi[best]), fun=float(self.yi[best]), x_iters=list(self.Xi),
+                              func_vals=np.asarray(self.yi), models=self.models, space=self.space,
+                              random_state=self.rng)
+
+    def run(self, func, n_iter=1):
+        for _ in range(n_iter):
+            x = self.ask()
+            self.tell(x, func(x))
+        return self._result()
+
+    def __getstate__(self):
+        return _copy.copy(self.__dict__)

@@ -1,0 +1,51 @@
+import json
+
+import pytest
+
+from mpi_opt_amd import models as M
+
+
+def test_test_mnist_json_ingests_to_spec():
+    js = M.test_mnist(nb_filters=33, pool_size=4, kernel_size=5, dense=77, dropout=0.9)
+    d = json.loads(js)
+    assert d["class_name"] == "Sequential" and len(d["config"]["layers"]) == 12
+    s = M.spec_from_json(js)
+    assert (s.nb_filters, s.pool_size, s.kernel_size, s.dense) == (33, 4, 5, 77)
+    # the space's `dropout` never reaches the model (mpiLAPI.py:151 reads `drop_out`)
+    assert s.dropout == 0.25
+    assert M.spec_from_json(M.test_mnist(drop_out=0.5)).dropout == 0.5
+
+
+def test_builder_from_function_maps_names():
+    space = M.mnist_space()
+    b = M.BuilderFromFunction(M.test_mnist, space)
+    mb = b.builder(20, 3, 4, 100, 0.3)
+    mb.comm = "c"
+    mb.device = mb.get_device_name("gpu0")
+    s = mb.spec()
+    assert (s.nb_filters, s.pool_size, s.kernel_size, s.dense) == (20, 3, 4, 100)
+    assert mb.device == "gpu0"
+
+
+def test_unsupported_topologies_raise():
+    with pytest.raises(ValueError):
+        M.spec_from_json(M.test_cnn(kernel_size=3))
+    with pytest.raises(ValueError):
+        M.spec_from_json(M.test_densenet())
+
+
+def test_base_models_interface():
+    c = M.CNNModel()
+    assert c.get_name() == "CNN_model" and c.get_parameter_grid() == [(3, 9), (.0, .5), (-5, 1)]
+    assert json.loads(c.build([3, 0.2, -3]))["class_name"] == "Sequential"
+    d = M.DenseNetModel()
+    assert d.get_name() == "DenseNet" and len(d.get_parameter_grid()) == 6
+    assert json.loads(d.build([10, 3, 12, 0.0, 16, -3]))["config"]["depth"] == 10
+    with pytest.raises(NotImplementedError):
+        M.BaseModel().build([])
+
+
+def test_reference_spaces():
+    assert [d.name for d in M.mnist_space()] == ["nb_filters", "pool_size", "kernel_size", "dense", "dropout"]
+    assert [d.name for d in M.topclass_space()] == ["dropout", "kernel_size", "llr"]
+    assert len(M.gan_space()) == 5 and len(M.threaded_skopt_space(2)) == 2
