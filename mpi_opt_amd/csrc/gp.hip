@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 namespace {
 
@@ -502,8 +503,14 @@ size_t score_lds_bytes(int bm, int dp, int np16) {
     return ((size_t)np16 * bm + (size_t)bm * dp + red) * sizeof(double);
 }
 
+// Candidates per workgroup.  MPO_GP_BM (16/32/64) overrides the default for
+// experiments; the default prefers the variant that fits several workgroups per
+// CU (VALU Matern phase of one overlapping the MFMA phase of another).
 int choose_bm(int dp, int np16) {
-    for (int bm : {64, 32, 16})
+    const char* env = getenv("MPO_GP_BM");
+    const int forced = env ? atoi(env) : 0;
+    if ((forced == 16 || forced == 32 || forced == 64) && score_lds_bytes(forced, dp, np16) <= kMaxLds) return forced;
+    for (int bm : {32, 16, 64})
         if (score_lds_bytes(bm, dp, np16) <= kMaxLds) return bm;
     return -1;
 }

@@ -119,9 +119,20 @@ def test_ties_resolve_to_lowest_index():
         assert idx[0] < 300 and idx[1] == idx[0] + 300 and idx[2] == idx[0] + 600
 
 
+@pytest.mark.parametrize("bm", ["64", "32", "16"])
+def test_block_variants_agree(bm, monkeypatch):
+    """MPO_GP_BM forces each candidates-per-workgroup variant; all are exact."""
+    monkeypatch.setenv("MPO_GP_BM", bm)
+    f = load(os.path.join(GOLDEN, "gp_ei_n200_d10.npz"))
+    g = device_gp(f)
+    out = g.score(f["C"], float(f["y_opt"]), acqs=("EI",), k=5)
+    assert np.max(np.abs(out["sd"].cpu().numpy() - f["sd_exact"]) / f["sd_exact"]) < 1e-9
+    np.testing.assert_array_equal(out["topk"]["EI"][0].cpu().numpy(), f["top5_EI"])
+
+
 @pytest.mark.parametrize("n,d", [(1, 1), (5, 2), (33, 7), (300, 16), (600, 10), (1100, 32)])
 def test_shapes_and_lds_variants(n, d):
-    """n=300 / 600 / 1100 select the 64 / 32 / 16-candidate block variants."""
+    """Large n falls back to the 16-candidate variant (LDS-resident K* rows)."""
     X, y = O.synthetic_problem(n, d, seed=n + d)
     st = O.gp_from_theta(X, y, 2.0, np.linspace(0.5, 2.0, d), 0.05)
     from mpi_opt_amd.gp import DeviceGP
