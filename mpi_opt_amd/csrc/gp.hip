@@ -37,7 +37,8 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 constexpr double kSqrt5 = 2.236067977499789696409173668731276235;
 constexpr double kSqrt1_2 = 0.707106781186547524400844362104849039;
 constexpr double kSqrt2Pi = 2.506628274631000502415765284811045253;
-constexpr double kJitter = 1e-10;  // sklearn GPR alpha default (_gpr.py:207)
+constexpr double kJitter = 1e-10;
+  // sklearn GPR alpha default (_gpr.py:207)
 
 // sklearn kernels.py:1715-1724 (nu = 2.5) times ConstantKernel.
 __device__ __forceinline__ double matern52(double r, double amp) {
@@ -191,7 +192,7 @@ __global__ void copy_kernel(const double* __restrict__ src, double* __restrict__
 // the k-steps ks < 4(jt+1) (rows i <= 16 jt + 15); lane l of k-step ks holds
 // W^T[4 ks + (l>>4)][16 jt + (l&15)] = W[16 jt + (l&15)][4 ks + (l>>4)].
 __host__ __device__ inline size_t wfrag_tile_base(int jt) { return (size_t)128 * jt * (jt + 1); }
-inline size_t wfrag_elems(int np16) { return wfrag_tile_base(np16 / 16); }
+inline size_t wfrag_elems(int np16) { return wfrag_tile_base(np16 / 16) + 16 * 64; }  // + prefetch slack
 
 __global__ void pack_wfrag_kernel(const double* __restrict__ W, int n, int ldw, int T,
                                   double* __restrict__ wfrag) {
@@ -227,8 +228,8 @@ struct ScoreArgs {
     double* part_val;
 };
 
-template <int BM, int DP>
-__global__ __launch_bounds__(256) void gp_score_kernel(ScoreArgs a) {
+template <int BM, int DP, int OCC>
+__global__ __launch_bounds__(256, OCC) void gp_score_kernel(ScoreArgs a) {
     constexpr int MT = BM / 16;      // 16-row m-tiles per block
     constexpr int G = 64 / BM;       // lanes groups per wave in phase 1
     constexpr int S = 4 * G;         // i-slots per block in phase 1
@@ -298,42 +299,48 @@ __global__ __launch_bounds__(256) void gp_score_kernel(ScoreArgs a) {
             const int jt = T - 1 - p;
             const double* bp = a.wfrag + wfrag_tile_base(jt) + lane;
             const int nks = 4 * (jt + 1);
-            f64x4 acc[MT][2];
+            // CH independent accumulation chains per m-tile (k-step mod CH) hide
+            // the f64 MFMA dependency latency: 4 chains at one m-tile per wave.
+            constexpr int CH = 2;   // 4 chains at MT = 1 measured slower (1.94 vs 1.68 ms / 1M)
+            f64x4 acc[MT][CH];
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt) {
-                acc[mt][0] = f64x4{0.0, 0.0, 0.0, 0.0};
-                acc[mt][1] = f64x4{0.0, 0.0, 0.0, 0.0};
-            }
-            // nks is a multiple of 4: two independent accumulation chains per
-            // m-tile (even / odd k-steps) hide the MFMA dependency latency.
-            double b0 = bp[0], b1 = bp[64], b2 = bp[128], b3 = bp[192];
-            for (int ks = 0; ks < nks; ks += 4) {
-                const bool more = ks + 4 < nks;
-                double n0 = 0.0, n1 = 0.0, n2 = 0.0, n3 = 0.0;
-                if (more) {
-                    n0 = bp[(ks + 4) * 64];
-                    n1 = bp[(ks + 5) * 64];
-                    n2 = bp[(ks + 6) * 64];
-                    n3 = bp[(ks + 7) * 64];
-                }
-                const double* ap = kc + (size_t)ks * MT * 64 + lane;
+            for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-                for (int mt = 0; mt < MT; ++mt) {
-                    acc[mt][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(ap[(0 * MT + mt) * 64], b0, acc[mt][0], 0, 0, 0);
-                    acc[mt][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(ap[(1 * MT + mt) * 64], b1, acc[mt][1], 0, 0, 0);
-                }
+                for (int c = 0; c < CH; ++c) acc[mt][c] = f64x4{0.0, 0.0, 0.0, 0.0};
+            // nks is a multiple of 4.  B fragments stream from L2 two 4-k-step groups
+            // ahead (8 MFMAs ~ the L2 latency); slots past the tile read the next
+            // tile's fragments (wfrag has 8 k-steps of slack at its end), unused.
+            double bq[2][4];
 #pragma unroll
-                for (int mt = 0; mt < MT; ++mt) {
-                    acc[mt][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(ap[(2 * MT + mt) * 64], b2, acc[mt][0], 0, 0, 0);
-                    acc[mt][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(ap[(3 * MT + mt) * 64], b3, acc[mt][1], 0, 0, 0);
+            for (int g = 0; g < 2; ++g)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) bq[g][u] = bp[(4 * g + u) * 64];
+            for (int ks = 0; ks < nks; ks += 8) {
+#pragma unroll
+                for (int g = 0; g < 2; ++g) {
+                    if (ks + 4 * g >= nks) break;
+                    const double* ap = kc + (size_t)(ks + 4 * g) * MT * 64 + lane;
+                    double cur[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        cur[u] = bq[g][u];
+                        bq[g][u] = bp[(ks + 8 + 4 * g + u) * 64];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+#pragma unroll
+                        for (int mt = 0; mt < MT; ++mt)
+                            acc[mt][u % CH] = __builtin_amdgcn_mfma_f64_16x16x4f64(ap[(u * MT + mt) * 64], cur[u],
+                                                                                 acc[mt][u % CH], 0, 0, 0);
                 }
-                b0 = n0; b1 = n1; b2 = n2; b3 = n3;
             }
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const double v = acc[mt][0][r] + acc[mt][1][r];
+                    double v = acc[mt][0][r];
+#pragma unroll
+                    for (int c = 1; c < CH; ++c) v += acc[mt][c][r];
                     sq[mt][r] += v * v;
                 }
         }
@@ -510,26 +517,40 @@ int choose_bm(int dp, int np16) {
     const char* env = getenv("MPO_GP_BM");
     const int forced = env ? atoi(env) : 0;
     if ((forced == 16 || forced == 32 || forced == 64) && score_lds_bytes(forced, dp, np16) <= kMaxLds) return forced;
-    for (int bm : {32, 16, 64})
+    for (int bm : {16, 32, 64})
         if (score_lds_bytes(bm, dp, np16) <= kMaxLds) return bm;
     return -1;
 }
 
-template <int BM, int DP>
+template <int BM, int DP, int OCC>
 hipError_t launch_score(const ScoreArgs& a, int nblocks, size_t lds, hipStream_t s) {
-    auto kern = gp_score_kernel<BM, DP>;
+    auto kern = gp_score_kernel<BM, DP, OCC>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)lds);
     hipLaunchKernelGGL(kern, dim3(nblocks), dim3(256), lds, s, a);
     return hipGetLastError();
 }
 
+// occupancy hint for the 16-candidate variant (min waves per SIMD -> VGPR cap);
+// MPO_GP_OCC overrides for experiments
+inline int gp_occ16() {
+    const char* e = getenv("MPO_GP_OCC");
+    const int v = e ? atoi(e) : 5;
+    return (v == 1 || v == 5 || v == 6) ? v : 5;
+}
+
 template <int DP>
 hipError_t launch_score_bm(int bm, const ScoreArgs& a, int nblocks, size_t lds, hipStream_t s) {
     switch (bm) {
-        case 64: return launch_score<64, DP>(a, nblocks, lds, s);
-        case 32: return launch_score<32, DP>(a, nblocks, lds, s);
-        case 16: return launch_score<16, DP>(a, nblocks, lds, s);
+        case 64: return launch_score<64, DP, 1>(a, nblocks, lds, s);
+        case 32: return launch_score<32, DP, 1>(a, nblocks, lds, s);
+        case 16:
+            switch (gp_occ16()) {
+                case 1: return launch_score<16, DP, 1>(a, nblocks, lds, s);
+                case 5: return launch_score<16, DP, 5>(a, nblocks, lds, s);
+                case 6: return launch_score<16, DP, 6>(a, nblocks, lds, s);
+                default: return launch_score<16, DP, 5>(a, nblocks, lds, s);
+            }
     }
     return hipErrorInvalidValue;
 }

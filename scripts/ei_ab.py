@@ -13,10 +13,10 @@ X, y = synthetic.gp_problem(200, 10, 0)
 ls = np.array([16.2, 1.91, 1.65, 9.84, 1.84, 2.94, 2.45, 9.09, 8.13, 1.94])
 g = DeviceGP(X, y, 17.4955, ls, 0.0465)
 cand = torch.from_numpy(synthetic.gp_candidates(1_000_000, 10, seed=1)).cuda()
-res = {b: [] for b in ("64", "32", "16")}
+res = {b: [] for b in ("32/1", "16/5", "16/6")}
 for rnd in range(4):
     for b in res:
-        os.environ["MPO_GP_BM"] = b
+        os.environ["MPO_GP_BM"], os.environ["MPO_GP_OCC"] = b.split("/")
         g.score(cand, float(y.min()), k=0)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -27,4 +27,4 @@ for rnd in range(4):
         torch.cuda.synchronize()
         res[b].append(e0.elapsed_time(e1) / 5)
 for b, v in res.items():
-    print("BM=%s  median %.3f ms  min %.3f ms" % (b, np.median(v), np.min(v)))
+    print("BM/occ=%s  median %.3f ms  min %.3f ms" % (b, np.median(v), np.min(v)))
