@@ -104,9 +104,16 @@ def bench_ei(args, torch, dist, ws, rank, dev):
             dist.all_gather_into_tensor(gathered, local)
         return out
 
+    # W warmup steps, then the same step until >= 0.3 s of warmup has run: the GPU
+    # clock ramps over the first ~30 ms of back-to-back launches (profiles/r01:
+    # 2.0 -> 1.57 ms per launch), which a 3-step warmup does not cover.
+    tw = time.perf_counter()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    while time.perf_counter() - tw < 0.3:
+        step()
+        torch.cuda.synchronize(dev)
     if ws > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
