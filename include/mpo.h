@@ -179,6 +179,13 @@ int mpo_pop_train_step(void* handle, const float* x, const int32_t* labels, cons
 int mpo_pop_eval_step(void* handle, const float* x, const int32_t* labels, const int32_t* order,
                       int64_t order_stride, int64_t row0, float* loss_sum, int32_t* correct, void* stream);
 
+/* Diagnostics: per-phase device milliseconds accumulated over the steps run
+ * since the last reset, as "phase ms\n" lines into buf (cap bytes).  Only
+ * populated when the plan was created with MPO_POP_PROFILE=1 in the
+ * environment (then every step ends in an event sync); returns MPO_ENOTSUP
+ * otherwise.  reset != 0 clears the accumulators after the read. */
+int mpo_pop_profile(void* handle, char* buf, size_t cap, int reset);
+
 /* k-fold index gather: out[r][:] = X[idx[r]][:] (the fold split
  * that mpi_learn does with per-fold communicators becomes an index gather). */
 int mpo_kfold_gather(const float* X, const int32_t* idx, int64_t rows, int row_elems, float* out,

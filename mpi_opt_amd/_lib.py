@@ -74,6 +74,7 @@ SIGNATURES = {
     "mpo_pop_bind": (_I, [_P, _P, _P, _P, _P, _P, _P, _P]),
     "mpo_pop_train_step": (_I, [_P, _P, _P, _P, _I64, _I64, ctypes.c_int32, _P, _P]),
     "mpo_pop_eval_step": (_I, [_P, _P, _P, _P, _I64, _I64, _P, _P, _P]),
+    "mpo_pop_profile": (_I, [_P, _P, _SZ, _I]),
     "mpo_kfold_gather": (_I, [_P, _P, _I64, _I, _P, _P]),
 }
 

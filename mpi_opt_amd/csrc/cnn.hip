@@ -34,7 +34,9 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <memory>
+#include <string>
 #include <vector>
 
 namespace {
@@ -58,7 +60,7 @@ struct Member {
     long long w1, b1, w2, b2, w3, b3, w4, b4, pend;
     // activation arena offsets (floats)
     long long a1, a2, pd, am, h, hd, z3, dz3, dh, dp, dz2, dz1, w2t, wp1, wp2;
-    long long w1p, w2p;  // zero-padded forward weights [K16][16*NT] (+16 rows slack)
+    long long w1p, w2p;  // zero-padded forward weights [K16 + kWSlack][16*NT]
 };
 
 struct ConvItem { int member, b, y0, R; };
@@ -86,6 +88,8 @@ struct StepArgs {
     float* loss_out;         // [n_members] mean batch loss (train)
     float* loss_sum;         // [n_members] running loss sum (eval)
     int* correct;            // [n_members] running correct count (eval)
+    long long zero_off;      // 64 zero floats in the activation arena (DMA source past row ends)
+    int debug;               // diagnostics only (env MPO_POP_DEBUG): 1 skip conv MMA loops, 2 skip conv staging
 };
 
 // ---- dropout counter hash (identical in oracle/cnn.py) ---------------------
@@ -111,10 +115,7 @@ __device__ __forceinline__ bool drop_keep(unsigned base, unsigned elem, unsigned
 // = dword index mod 32 per 32-lane half):
 //  * forward conv: lanes 0-15 read 16 pixels at stride fp, lanes 16-31 the next
 //    channel (+1): fp = 2 (mod 4) puts the two halves on the even / odd banks;
-//  * weight gradient: lanes 0-15 read 16 channels (+1 each), lanes 16-31 the next
-//    pixel (+fp): fp = 16 (mod 32) puts them on banks 0-15 / 16-31.
 __host__ __device__ constexpr inline int fwd_fp(int c) { return c == 1 ? 1 : c + ((6 - (c & 3)) & 3); }
-__host__ __device__ constexpr inline int wg_fp(int c) { return c == 1 ? 1 : c + ((48 - (c & 31)) & 31); }
 
 // ============================================================================
 // Image-stationary implicit-GEMM convolution (forward and input-gradient).
@@ -122,9 +123,7 @@ __host__ __device__ constexpr inline int wg_fp(int c) { return c == 1 ? 1 : c + 
 // One workgroup = (member, sample b, output rows [y0, y0+R)); M = R*Ho <= 128
 // output pixels = 8 m-tiles of 16 spread over 4 waves; N = F in NT tiles of 16.
 // ============================================================================
-constexpr int kConvBK = 32;  // B rows per LDS chunk (8 k-steps), double-buffered
 
-__host__ __device__ constexpr inline int bn_stride(int nt) { return nt * 16 + ((nt & 1) ? 0 : 16); }
 __host__ __device__ constexpr inline int align4(int x) { return (x + 3) & ~3; }
 
 // dgrad image pixel stride: >= F rounded to 4 (zero channels for the 16-channel
@@ -142,6 +141,72 @@ __device__ __forceinline__ void stage_row(const float* __restrict__ src, float* 
         c += r;
         gx += q;
         if (c >= cin) { c -= cin; ++gx; }
+    }
+}
+
+// Slack past the K16 rows: the pipelined loops below run an even number of
+// 16-k groups and read up to two groups (weights) and three groups (tap
+// offsets) past that; the slack is zero.
+constexpr int kWSlack = 48;
+constexpr int kKoffSlack = 64;
+
+// Main loop of the forward conv for MT (1 or 2) m-tiles per wave: one 16-k group
+// per half-iteration; the weights of group g+1 (L2 -> VGPR) and the A gathers of
+// group g+1 (LDS) are issued before the MFMAs of group g, and the tap offsets
+// one group further ahead, so no MFMA waits on a load issued in its own group.
+template <int MT, int NT>
+__device__ __forceinline__ void conv_fwd_loop(const float* __restrict__ img, const int* __restrict__ koff,
+                                              const float* __restrict__ W, int ngroups, const int (&pb)[2],
+                                              f32x4 (&acc)[2][NT], int krow, int kcol) {
+    constexpr int N16 = NT * 16;
+    const float* wsrc = W + krow * N16 + kcol;
+    const int* kp = koff + krow * 4;
+    float b0[4][NT], b1[4][NT], a0[4][MT], a1[4][MT];
+    auto loadB = [&](int g, float (&dst)[4][NT]) {
+        const float* src = wsrc + (long long)g * 16 * N16;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) dst[u][j] = src[u * 4 * N16 + j * 16];
+    };
+    auto kof = [&](int g) { return *reinterpret_cast<const int4*>(kp + g * 16); };
+    auto readA = [&](const int4 ko, float (&dst)[4][MT]) {
+        const int kov[4] = {ko.x, ko.y, ko.z, ko.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int i = 0; i < MT; ++i) dst[u][i] = img[pb[i] + kov[u]];
+    };
+    auto mma = [&](const float (&av)[4][MT], const float (&bw)[4][NT]) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][i], bw[u][j], acc[i][j], 0, 0, 0);
+    };
+    loadB(0, b0);
+    int4 ko = kof(0);
+    readA(ko, a0);
+    ko = kof(1);
+    // Two groups per iteration with no exit in between (an odd group count runs
+    // one zero group from the slack): a mid-loop exit makes the compiler shuffle
+    // the accumulators between AGPRs at every iteration.  sched_barrier(0) pins
+    // the issue order -- otherwise each load sinks next to its first use.
+    for (int g = 0; g < ngroups; g += 2) {
+        loadB(g + 1, b1);
+        readA(ko, a1);
+        ko = kof(g + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        loadB(g + 2, b0);
+        readA(ko, a0);
+        ko = kof(g + 3);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(a1, b1);
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -169,7 +234,6 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
         out = a.act + mb.a2 + (long long)it.b * Ho * Ho * F;
     }
     const int N = F;
-    constexpr int N16 = NT * 16;
     const int K = k * k * Cin;
     const int K16 = (K + 15) & ~15;
     const int Wp = Hin;
@@ -179,13 +243,13 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
 
     float* img = smem;                                               // [rows][Wp][Fp]
     const int img_elems = rows * Wp * Fp;
-    int* koff = reinterpret_cast<int*>(smem + align4(img_elems));   // [K16], groups of 16 as [krow][4]
+    int* koff = reinterpret_cast<int*>(smem + align4(img_elems));   // [K16 + slack], groups of 16 as [krow][4]
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int krow = lane >> 4, kcol = lane & 15;
 
     // ---- stage the input rows + the tap-offset table (the only barrier)
-    for (int r = 0; r < rows; ++r) {
+    for (int r = 0; r < rows && a.debug != 2; ++r) {
         const float* src = in + (long long)(it.y0 + r) * Hin * Cin;
         float* dst = img + r * Wp * Fp;
         if (Cin == 1) {
@@ -194,7 +258,7 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
             stage_row(src, dst, Hin * Cin, Cin, Fp, tid);
         }
     }
-    for (int kk = tid; kk < K16; kk += 256) {
+    for (int kk = tid; kk < K16 + kKoffSlack; kk += 256) {
         int off = 0;
         if (kk < K) {
             const int kc = k * Cin;
@@ -207,13 +271,11 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
     }
 
     const int mtiles = (M + 15) >> 4;
+    const int mine = __builtin_amdgcn_readfirstlane(mtiles > wave + 4 ? 2 : (mtiles > wave ? 1 : 0));
     int pb[2];
-    bool has[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-        const int mt = wave + 4 * i;
-        has[i] = mt < mtiles;
-        const int m = mt * 16 + (lane & 15);
+        const int m = (wave + 4 * i) * 16 + (lane & 15);
         int base = 0;
         if (m < M) {
             const int y = m / Ho, xx = m - y * Ho;
@@ -227,55 +289,16 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     __syncthreads();
-    if (!has[0]) return;   // wave-uniform; no barriers below
-
-    // ---- K loop: groups of 16 k (4 k-steps); weights stream from L2 into
-    // ping-pong registers (padded [K16+16][N16] copy: no bounds selects)
-    const int ngroups = K16 >> 4;
-    auto load_group = [&](int g, float (&dst)[4][NT]) {
-        const float* src = W + (long long)(g * 16 + krow) * N16 + kcol;
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int j = 0; j < NT; ++j) dst[u][j] = src[u * 4 * N16 + j * 16];
-    };
-    auto compute = [&](int g, const float (&bw)[4][NT]) {
-        const int4 ko4 = *reinterpret_cast<const int4*>(koff + g * 16 + krow * 4);
-        const int kov[4] = {ko4.x, ko4.y, ko4.z, ko4.w};
-        float av[4][2];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            av[u][0] = img[pb[0] + kov[u]];
-            av[u][1] = img[pb[1] + kov[u]];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-#pragma unroll
-            for (int j = 0; j < NT; ++j)
-                acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][0], bw[u][j], acc[0][j], 0, 0, 0);
-            if (has[1]) {
-#pragma unroll
-                for (int j = 0; j < NT; ++j)
-                    acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][1], bw[u][j], acc[1][j], 0, 0, 0);
-            }
-        }
-    };
-    float b0[4][NT], b1[4][NT];
-    load_group(0, b0);
-    for (int g = 0; g < ngroups; g += 2) {
-        // the +16-row slack keeps the one-past-the-end prefetch in bounds
-        load_group(g + 1, b1);
-        compute(g, b0);
-        if (g + 1 >= ngroups) break;
-        load_group(g + 2, b0);
-        compute(g + 1, b1);
-    }
+    const int ngroups = a.debug == 1 ? 0 : K16 >> 4;
+    if (mine == 2) conv_fwd_loop<2, NT>(img, koff, W, ngroups, pb, acc, krow, kcol);
+    else if (mine == 1) conv_fwd_loop<1, NT>(img, koff, W, ngroups, pb, acc, krow, kcol);
+    else return;
 
     // ---- epilogue: C/D map col = lane & 15, row = (lane >> 4) * 4 + r
     const long long pix0 = (long long)it.y0 * Ho;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-        if (!has[i]) continue;
+        if (i >= mine) break;
         const int mt = wave + 4 * i;
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
@@ -329,7 +352,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
 
     for (int e = tid; e < img_elems; e += 256) img[e] = 0.f;
     __syncthreads();
-    for (int r = 0; r < rows; ++r) {
+    for (int r = 0; r < rows && a.debug != 2; ++r) {
         const int gy = y0 + r - pad;
         if (gy < 0 || gy >= H2) continue;
         stage_row(in + (long long)gy * H2 * F, img + (r * Wp + pad) * Fp, H2 * F, F, Fp, tid);
@@ -372,7 +395,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
     // ping-pong register buffers (loop unrolled by two), loads unconditional.
     const int CB = (F4 + 15) >> 4;
     const int nx = ux1 - ux0;
-    const int ngroups = (uy1 > uy0 && nx > 0) ? (uy1 - uy0) * nx * CB : 0;
+    const int ngroups = (uy1 > uy0 && nx > 0 && a.debug != 1) ? (uy1 - uy0) * nx * CB : 0;
     constexpr int N16 = NT * 16;
     auto load_group = [&](int ky, int kx, int cb, float (&dst)[4][NT]) {
         // w2t is [k*k][F4][N16], zero padded (+16 rows of slack): no bounds select,
@@ -455,14 +478,68 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
 
 // ============================================================================
 // Weight gradient: dW[(ky,kx,c)][n] = sum_{b,y,x} in[b][y+ky][x+kx][c] * dout[b][y][x][n]
-// One workgroup = (member, 128 rows of (ky,kx,c), a group of samples); loops
-// over its samples and output row chunks, staging input rows + dout rows in LDS.
-// Writes one partial slab per sample group (reduced deterministically later).
+// (plus the bias gradient as row Kw = k*k*Cin: an all-ones A row).
+// GEMM view M = Kw + 1 rows of (ky,kx,c), N = F, K = pixels.  One workgroup =
+// (member, 512-row m-group, a group of samples), 8 waves x up to 4 m-tiles.
+// The workgroup streams its samples one OUTPUT ROW at a time.  Output row y
+// needs input rows y .. y+k-1: they live in an LDS ring of k+2 row slots, each
+// input row staged exactly once per m-group; the dout rows in 3 buffers.  Rows
+// arrive by LDS-DMA (global_load_lds_dword) two output rows ahead: at row y the
+// workgroup issues input row y+k+1 and dout row y+2, waits (counted vmcnt) for
+// what it issued at row y-1 and meets one raw s_barrier -- the DMA stays in
+// flight across the barrier, so its latency hides behind two rows of MFMAs.
+// Every wave issues exactly kWgDma DMA instructions per row (lanes past a row's
+// end read a zero block), so the counted wait is a constant.
+// Writes one partial slab per sample group (reduced in fixed order later).
 // ============================================================================
-__host__ __device__ constexpr inline int dout_stride(int nt) { return bn_stride(nt); }
+constexpr int kWgWaves = 8;
+constexpr int kWgThreads = kWgWaves * 64;
+constexpr int kWgMaxMT = 4;                        // m-tiles per wave
+constexpr int kWgRows = kWgWaves * kWgMaxMT * 16;  // 512 rows per m-group
+constexpr int kWgChunks = 4;                       // 64-float DMA chunks per wave per row: rows <= 8*4*64 floats
+// DMA instructions per wave per output row: 2 * kWgChunks = 8 (the vmcnt(8) below)
+static_assert(kWgChunks == 4, "the counted s_waitcnt vmcnt(8) assumes 2 * 4 DMA instructions per row");
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__host__ __device__ constexpr inline int round64(int x) { return (x + 63) & ~63; }
+
+// One output row's MFMAs for MT m-tiles: nk4 k-steps of 4 pixels; the LDS reads
+// of k-step s+1 are issued before the MFMAs of k-step s.
+template <int MT, int NT>
+__device__ __forceinline__ void wgrad_row(const float* __restrict__ img, const float* __restrict__ dl,
+                                          const int (&abase)[kWgMaxMT], const int (&astep)[kWgMaxMT], int dstride,
+                                          int nk4, int krow, int kcol, f32x4 (&acc)[kWgMaxMT][NT]) {
+    float a0[MT], a1[MT], b0[NT], b1[NT];
+    auto rd = [&](int s, float (&av)[MT], float (&bv)[NT]) {
+        const int x = 4 * s + krow;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) av[i] = img[abase[i] + x * astep[i]];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) bv[j] = dl[x * dstride + j * 16 + kcol];
+    };
+    auto mma = [&](const float (&av)[MT], const float (&bv)[NT]) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    };
+    rd(0, a0, b0);
+    for (int s = 0; s < nk4; s += 2) {
+        rd(s + 1, a1, b1);   // s + 1 <= nk4: reads zero dout padding / finite LDS
+        __builtin_amdgcn_sched_barrier(0);
+        mma(a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 1 >= nk4) break;
+        rd(s + 2, a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(a1, b1);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
 
 template <int OP, int NT>
-__global__ __launch_bounds__(256) void conv_wgrad_kernel(StepArgs a, const WgItem* __restrict__ items) {
+__global__ __launch_bounds__(kWgThreads) void conv_wgrad_kernel(StepArgs a, const WgItem* __restrict__ items) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const WgItem it = items[blockIdx.x];
     const Member& mb = a.mem[it.member];
@@ -475,127 +552,124 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(StepArgs a, const WgIte
         Hin = mb.H1; Cin = F; Ho = mb.H2; dout_off = mb.dz2; part_off = mb.wp2;
     }
     const int N = F;
-    const int Kw = k * k * Cin;  // weight rows; row Kw is the bias gradient (an all-ones A row)
-    const int Fp = wg_fp(Cin);
-    constexpr int Fq = NT * 16 + ((NT & 1) ? 0 : 16);
-    const int R = it.R;
-    const int P = R * Ho;
-    const int P4 = (P + 15) & ~15;   // pixel rows padded to whole 16-pixel read groups
-    const int rows = R + k - 1;
-    float* img = smem;                                   // [rows][Hin][Fp]
-    const int img_elems = rows * Hin * Fp;
-    float* dl = smem + ((img_elems + 3) & ~3);            // [P4][Fq]
-    int* poff = reinterpret_cast<int*>(dl + P4 * Fq);     // [P4]
+    const int Kw = k * k * Cin;
+    const int RS = k + 2;                       // ring slots
+    const int rowf = Hin * Cin;                 // floats per input row
+    const int rowS = round64(rowf);             // slot stride (a DMA chunk never crosses a slot)
+    const int dcnt = Ho * N;                    // floats per dout row (pixel stride N)
+    const int nk4 = (Ho + 3) >> 2;
+    const int dS = round64((4 * nk4 + 4) * N + 64);   // dout buffer stride: zero padding past Ho*N
+    float* ring = smem;                                              // [RS][rowS] (+ slack)
+    const int ring_elems = RS * rowS + 8 * Cin + 64;                 // k-step padding reads stay in bounds
+    float* dl = smem + round64(ring_elems);                          // [3][dS]
+    const int lds_floats = round64(ring_elems) + 3 * dS;             // + kWgWaves*64 scratch, + {0, 1}
+    const int kZero = lds_floats + kWgWaves * 64, kOne = kZero + 1;  // constant A rows (padding / bias)
+    const float* zero_src = a.act + a.zero_off;                      // 64 zero floats in global memory
+    const float* in_base = OP == WG_CONV1 ? a.x : a.act + mb.a1;
+    const float* dout_base = a.act + dout_off;
+    const int* order = a.order + (long long)it.member * a.order_stride + a.row0;
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int krow = lane >> 4, kcol = lane & 15;
+    const int mtiles = (Kw + 1 + 15) >> 4;
+    const int t0 = it.mg * (kWgRows / 16);
+    const int mine = __builtin_amdgcn_readfirstlane(
+        min(kWgMaxMT, max(0, (mtiles - t0 - wave + kWgWaves - 1) / kWgWaves)));
 
-    int toff[4];
-    bool has[4], ones[4];
+    // per lane, per tile: A row (ky, kx*Cin + c) -> ring address ring_row(y+ky)*rowS + col + x*Cin;
+    // rows past Kw read the constant 0 (padding) or 1 (the bias row) with x stride 0
+    int tky[kWgMaxMT], tcol[kWgMaxMT], astep[kWgMaxMT];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int mt = wave + 4 * i;
-        const int m0 = it.mg * 256 + mt * 16;
-        has[i] = m0 <= Kw;
-        const int m = m0 + (lane & 15);
-        ones[i] = m == Kw;
-        int off = 0;
+    for (int i = 0; i < kWgMaxMT; ++i) {
+        const int m = (t0 + wave + kWgWaves * i) * 16 + (lane & 15);
+        int ky = 0, col = m == Kw ? kOne : kZero, st = 0;
         if (m < Kw) {
             const int kc = k * Cin;
-            const int ky = m / kc, rem = m - ky * kc;
-            const int kx = rem / Cin, c = rem - kx * Cin;
-            off = (ky * Hin + kx) * Fp + c;
+            ky = m / kc;
+            col = m - ky * kc;
+            st = Cin;
         }
-        toff[i] = off;
+        tky[i] = ky;
+        tcol[i] = col;
+        astep[i] = st;
     }
-    f32x4 acc[4][NT];
+    f32x4 acc[kWgMaxMT][NT];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < kWgMaxMT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    for (int b = it.b0; b < it.b1; ++b) {
-        const float* in;
-        if (OP == WG_CONV1) {
-            const int sidx = a.order[(long long)it.member * a.order_stride + a.row0 + b];
-            in = a.x + (long long)sidx * (kImg * kImg);
-        } else {
-            in = a.act + mb.a1 + (long long)b * Hin * Hin * Cin;
+    // zero all LDS once (ring slack, dout padding) before any DMA lands; the bias constant 1
+    for (int e = tid; e <= kOne; e += kWgThreads) smem[e] = e == kOne ? 1.f : 0.f;
+    __syncthreads();
+
+    // kWgChunks DMA instructions: cnt floats of src -> LDS dst (64-float chunks, chunk q*8+wave)
+    auto dma = [&](const float* src, int cnt, float* dst) {
+#pragma unroll
+        for (int q = 0; q < kWgChunks; ++q) {
+            const int c0 = (q * kWgWaves + wave) * 64;
+            const int e = c0 + lane;
+            const float* g = e < cnt ? src + e : zero_src + lane;
+            // chunks wholly past the row land in the scratch tail
+            float* d = c0 < cnt ? dst + c0 : smem + lds_floats + wave * 64;
+            __builtin_amdgcn_global_load_lds(g, (lds_ptr_t)d, 4, 0, 0);
         }
-        const float* dout = a.act + dout_off + (long long)b * Ho * Ho * N;
-        for (int y0 = 0; y0 < Ho; y0 += R) {
-            const int rcnt = min(R, Ho - y0);
-            const int pcnt = rcnt * Ho;
-            __syncthreads();
-            // input rows y0 .. y0 + rcnt + k - 2 (always inside the image)
-            const int irows = rcnt + k - 1;
-            const float* src = in + (long long)y0 * Hin * Cin;
-            if (Cin == Fp) {
-                for (int e = tid; e < irows * Hin * Cin; e += 256) img[e] = src[e];
-            } else {
-                stage_row(src, img, irows * Hin * Cin, Cin, Fp, tid);
+    };
+
+    for (int b = it.b0; b < it.b1; ++b) {
+        const float* inb = OP == WG_CONV1 ? in_base + (long long)order[b] * (kImg * kImg)
+                                          : in_base + (long long)b * Hin * rowf;
+        const float* dob = dout_base + (long long)b * Ho * dcnt;
+        // prologue of the sample: input rows 0..k (slots 0..k), dout rows 0, 1
+        for (int r = 0; r <= k && r < Hin; ++r) dma(inb + r * rowf, rowf, ring + r * rowS);
+        dma(dob, dcnt, dl);
+        if (Ho > 1) dma(dob + dcnt, dcnt, dl + dS);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int slot0 = 0;   // ring slot of input row y
+        for (int y = 0; y < Ho; ++y) {
+            // two rows ahead: input row y+k+1 -> the slot row y-1 used; dout row y+2
+            const bool ahead = y + 2 < Ho;   // then input row y + k + 1 = (y + 2) + k - 1 < Hin too
+            if (ahead) {
+                int sl = slot0 + k + 1;
+                sl = sl >= RS ? sl - RS : sl;
+                dma(inb + (y + k + 1) * rowf, rowf, ring + sl * rowS);
+                dma(dob + (y + 2) * dcnt, dcnt, dl + ((y + 2) % 3) * dS);
             }
-            const float* dsrc = dout + (long long)y0 * Ho * N;
-            stage_row(dsrc, dl, pcnt * N, N, Fq, tid);
-            // zero the channel padding of the staged pixels and the padded pixels
-            for (int e = tid; e < P4 * (Fq - N); e += 256) {
-                const int px = e / (Fq - N), c = N + (e - px * (Fq - N));
-                dl[px * Fq + c] = 0.f;
+            int abase[kWgMaxMT];
+#pragma unroll
+            for (int i = 0; i < kWgMaxMT; ++i) {
+                int sl = slot0 + tky[i];
+                sl = sl >= RS ? sl - RS : sl;
+                abase[i] = astep[i] ? sl * rowS + tcol[i] : tcol[i];
             }
-            for (int e = pcnt * N + tid; e < P4 * N; e += 256) {
-                const int px = e / N, c = e - px * N;
-                dl[px * Fq + c] = 0.f;
+            const float* dcur = dl + (y % 3) * dS;
+            if (a.debug != 1) {
+                if (mine == 4) wgrad_row<4, NT>(ring, dcur, abase, astep, N, nk4, krow, kcol, acc);
+                else if (mine == 3) wgrad_row<3, NT>(ring, dcur, abase, astep, N, nk4, krow, kcol, acc);
+                else if (mine == 2) wgrad_row<2, NT>(ring, dcur, abase, astep, N, nk4, krow, kcol, acc);
+                else if (mine == 1) wgrad_row<1, NT>(ring, dcur, abase, astep, N, nk4, krow, kcol, acc);
             }
-            for (int px = tid; px < P4; px += 256) {
-                int off = 0;
-                if (px < pcnt) {
-                    const int y = px / Ho, xx = px - y * Ho;
-                    off = (y * Hin + xx) * Fp;
-                }
-                poff[px] = off;
-            }
-            __syncthreads();
-            if (!has[0]) continue;
-            const int pc4 = (pcnt + 3) & ~3;
-            const int p16 = (pc4 + 15) & ~15;   // poff/dl are padded to 16 pixels
-            for (int ks0 = 0; ks0 < p16; ks0 += 16) {
-                float bf[4][NT], av[4][4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int ks = ks0 + 4 * u;
-                    const int po = poff[ks + krow];
-#pragma unroll
-                    for (int j = 0; j < NT; ++j) bf[u][j] = dl[(ks + krow) * Fq + j * 16 + kcol];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) av[u][i] = ones[i] ? 1.f : img[toff[i] + po];
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    if (ks0 + 4 * u >= pc4) break;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        if (!has[i]) break;   // tiles are assigned in order: has[] is a prefix
-#pragma unroll
-                        for (int j = 0; j < NT; ++j)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][i], bf[u][j], acc[i][j], 0, 0, 0);
-                    }
-                }
-            }
+            slot0 = slot0 + 1 == RS ? 0 : slot0 + 1;
+            // retire the DMA issued one row ago (row y+1's data); this row's stays in flight
+            if (ahead) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
         }
     }
     float* part = a.act + part_off + (long long)it.group * (Kw + 1) * N;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        if (!has[i]) continue;
-        const int mt = wave + 4 * i;
+    for (int i = 0; i < kWgMaxMT; ++i) {
+        if (i >= mine) break;
+        const int mt = t0 + wave + kWgWaves * i;
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
             const int n = j * 16 + kcol;
             if (n >= N) continue;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int m = it.mg * 256 + mt * 16 + krow * 4 + r;
+                const int m = mt * 16 + krow * 4 + r;
                 if (m <= Kw) part[(long long)m * N + n] = acc[i][j][r];
             }
         }
@@ -639,10 +713,10 @@ __global__ void flip_w2_kernel(StepArgs a, const MItem* __restrict__ items) {
         const int src_tap = (k - 1 - ky) * k + (k - 1 - kx);
         w2t[i] = (f < F && c < F) ? w2[((long long)src_tap * F + c) * F + f] : 0.f;
     }
-    // forward weights, zero-padded to [K16 + 16][N16]
+    // forward weights, zero-padded to [K16 + kWSlack][N16]
     const int K2 = k * k * F, K1 = k * k;
-    const long long S2 = (long long)(((K2 + 15) & ~15) + 16) * N16;
-    const long long S1 = (long long)(((K1 + 15) & ~15) + 16) * N16;
+    const long long S2 = (long long)(((K2 + 15) & ~15) + kWSlack) * N16;
+    const long long S1 = (long long)(((K1 + 15) & ~15) + kWSlack) * N16;
     float* w2p = a.act + mb.w2p;
     float* w1p = a.act + mb.w1p;
     const float* w1 = a.params + mb.w1;
@@ -962,14 +1036,65 @@ __global__ void kfold_gather_kernel(const float* __restrict__ X, const int* __re
 // ============================================================================
 // Host-side plan
 // ============================================================================
-struct Bucketed {
-    // items sorted by NT (1..4); [begin, end) per NT; dynamic LDS per NT bucket
-    int begin[5] = {0, 0, 0, 0, 0}, end[5] = {0, 0, 0, 0, 0};
-    size_t lds[5] = {0, 0, 0, 0, 0};
+// Launch segments of one op: items sorted by (NT, occupancy class), one launch
+// per segment with that segment's own dynamic LDS size.  Bucketing by NT alone
+// would size every block of a bucket for its largest member and cap the whole
+// bucket at that member's occupancy.
+struct Seg {
+    int nt, begin, end;
+    size_t lds;
 };
+struct Bucketed {
+    std::vector<Seg> segs;
+};
+
+// Per-phase device timing for diagnostics (env MPO_POP_PROFILE=1 at plan
+// creation): hipEvents between the launches of a step, accumulated on the host
+// after an event sync.  Off by default (no events, no syncs).
+struct PhaseTimer {
+    bool on = false;
+    std::vector<hipEvent_t> ev;
+    std::vector<std::string> names;
+    int used = 0;
+    std::vector<std::pair<std::string, double>> acc;
+    void mark(const std::string& name, hipStream_t s) {
+        if (!on) return;
+        if (used == (int)ev.size()) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) { on = false; return; }
+            ev.push_back(e);
+            names.emplace_back();
+        }
+        names[used] = name;
+        (void)hipEventRecord(ev[used], s);
+        ++used;
+    }
+    void finish() {
+        if (!on || used < 2) { used = 0; return; }
+        (void)hipEventSynchronize(ev[used - 1]);
+        for (int i = 1; i < used; ++i) {
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, ev[i - 1], ev[i]);
+            auto it = std::find_if(acc.begin(), acc.end(), [&](const auto& p) { return p.first == names[i]; });
+            if (it == acc.end()) acc.emplace_back(names[i], (double)ms); else it->second += ms;
+        }
+        used = 0;
+    }
+    ~PhaseTimer() { for (auto e : ev) (void)hipEventDestroy(e); }
+};
+
+// Integer tuning knob from the environment (read once per plan; A/B only).
+int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return (v && *v) ? atoi(v) : dflt;
+}
 
 struct Plan {
     int n = 0, B = 0;
+    PhaseTimer timer;
+    bool timer_detail = false;
+    long long zero_off = 0;
+    int debug = 0;
     std::vector<Member> mem;
     long long n_params = 0, act_floats = 0;
     std::vector<ConvItem> conv1, conv2, dgrad;
@@ -994,7 +1119,7 @@ struct Plan {
 size_t conv_lds_bytes(int rows, int Wp, int Cin, int K, int nt) {
     (void)nt;
     const int Fp = fwd_fp(Cin);
-    return (size_t)(align4(rows * Wp * Fp) + ((K + 15) & ~15)) * sizeof(float);
+    return (size_t)(align4(rows * Wp * Fp) + ((K + 15) & ~15) + kKoffSlack) * sizeof(float);
 }
 
 size_t dgrad_lds_bytes(int R, int k, int F, int nt) {
@@ -1003,20 +1128,19 @@ size_t dgrad_lds_bytes(int R, int k, int F, int nt) {
     return (size_t)align4((R + k - 1) * Wp * dgrad_fp(F) + 16) * sizeof(float);
 }
 
-size_t wg_lds_bytes(int rows, int Hin, int Cin, int P, int nt) {
-    const int Fp = wg_fp(Cin);
-    const int img = align4(rows * Hin * Fp);
-    const int P4 = (P + 15) & ~15;
-    return (size_t)(img + P4 * dout_stride(nt) + P4) * sizeof(float);
+size_t wg_lds_bytes(int k, int Hin, int Cin, int Ho, int F) {
+    const int ring = round64((k + 2) * round64(Hin * Cin) + 8 * Cin + 64);
+    const int dS = round64((4 * ((Ho + 3) >> 2) + 4) * F + 64);
+    return (size_t)(ring + 3 * dS + kWgWaves * 64 + 4) * sizeof(float);
 }
 
 // Row-chunk height: as many output rows as fit M = R*Ho <= 128 pixels, shrunk
 // (down to half of that) to fit 3 or 2 workgroups per CU when possible.
 template <class Fn>
-int choose_rows(int Ho, Fn lds_of) {
+int choose_rows(int Ho, Fn lds_of, int kb1 = 52, int kb2 = 78) {
     const int rmax = std::max(1, std::min(Ho, 128 / Ho));
     const int rmin = std::max(1, rmax / 2);
-    for (size_t budget : {(size_t)52 << 10, (size_t)78 << 10})
+    for (size_t budget : {(size_t)kb1 << 10, (size_t)kb2 << 10})
         for (int R = rmax; R >= rmin; --R)
             if (lds_of(R) <= budget) return R;
     for (int R = rmax; R >= 1; --R)
@@ -1024,14 +1148,23 @@ int choose_rows(int Ho, Fn lds_of) {
     return 1;
 }
 
+// Workgroups per CU that `lds` bytes allow (LDS 160 KiB; 8 = the 32-wave cap).
+int lds_class(size_t lds) { return (int)std::min<size_t>(8, ((size_t)160 << 10) / std::max<size_t>(lds, 1)); }
+
 template <class T>
-void bucket_by_nt(std::vector<T>& items, Bucketed& bk, const std::vector<Member>& mem) {
-    std::stable_sort(items.begin(), items.end(), [&](const T& x, const T& y) { return mem[x.member].nt < mem[y.member].nt; });
-    for (int nt = 1; nt <= 4; ++nt) {
-        bk.begin[nt] = (int)(std::lower_bound(items.begin(), items.end(), nt,
-                                              [&](const T& x, int v) { return mem[x.member].nt < v; }) - items.begin());
-        bk.end[nt] = (int)(std::upper_bound(items.begin(), items.end(), nt,
-                                            [&](int v, const T& x) { return v < mem[x.member].nt; }) - items.begin());
+void bucket_segs(std::vector<T>& items, Bucketed& bk, const std::vector<Member>& mem, const std::vector<size_t>& lds) {
+    auto key = [&](const T& x) { return mem[x.member].nt * 16 + (8 - lds_class(lds[x.member])); };
+    std::stable_sort(items.begin(), items.end(), [&](const T& x, const T& y) { return key(x) < key(y); });
+    bk.segs.clear();
+    for (int i = 0; i < (int)items.size();) {
+        const int kk = key(items[i]);
+        Seg sg{mem[items[i].member].nt, i, i, 0};
+        while (i < (int)items.size() && key(items[i]) == kk) {
+            sg.lds = std::max(sg.lds, lds[items[i].member]);
+            ++i;
+        }
+        sg.end = i;
+        bk.segs.push_back(sg);
     }
 }
 
@@ -1069,8 +1202,9 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         m.pend = po;
         // wgrad sample groups (partial slabs reduced in a fixed order): ~10
         // samples per conv2 block, ~4 per conv1 block (its GEMM is tiny)
-        m.g2 = std::max(1, std::min(B, (B + 9) / 10));
-        m.g1 = std::max(1, std::min(B, (B + 3) / 4));
+        const int spg2 = std::max(1, env_int("MPO_WG_SPG2", 10)), spg1 = std::max(1, env_int("MPO_WG_SPG1", 4));
+        m.g2 = std::max(1, std::min(B, (B + spg2 - 1) / spg2));
+        m.g1 = std::max(1, std::min(B, (B + spg1 - 1) / spg1));
         m.a1 = aalloc((long long)B * m.H1 * m.H1 * F);
         m.a2 = aalloc((long long)B * m.H2 * m.H2 * F);
         m.pd = aalloc((long long)B * m.K1);
@@ -1084,28 +1218,31 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         m.dz2 = aalloc((long long)B * m.H2 * m.H2 * F);
         m.dz1 = aalloc((long long)B * m.H1 * m.H1 * F);
         m.w2t = aalloc((long long)(k * k * ((F + 3) & ~3) + 16) * (m.nt * 16));
-        m.w1p = aalloc((long long)(((k * k + 15) & ~15) + 16) * (m.nt * 16));
-        m.w2p = aalloc((long long)(((k * k * F + 15) & ~15) + 16) * (m.nt * 16));
+        m.w1p = aalloc((long long)(((k * k + 15) & ~15) + kWSlack) * (m.nt * 16));
+        m.w2p = aalloc((long long)(((k * k * F + 15) & ~15) + kWSlack) * (m.nt * 16));
         m.wp1 = aalloc((long long)m.g1 * (k * k + 1) * F);
         m.wp2 = aalloc((long long)m.g2 * (k * k * F + 1) * F);
     }
+    P.zero_off = aalloc(64);   // never written: the caller zero-initialises the arena
     P.n_params = po;
     P.act_floats = ao;
 
-    // ---- work lists
+    // ---- work lists (LDS budgets per workgroup in KiB: A/B knobs, defaults tuned on MI355X)
+    const int kc1 = env_int("MPO_CONV_KB1", 52), kc2 = env_int("MPO_CONV_KB2", 78);
+    const int kdg = env_int("MPO_DG_KB", 78);
+    std::vector<size_t> L1(n), L2(n), LD(n), LW1(n), LW2(n);   // per-member LDS bytes per op
     for (int i = 0; i < n; ++i) {
         const Member& m = P.mem[i];
         const int k = m.k, F = m.F, nt = m.nt;
-        const int R1 = choose_rows(m.H1, [&](int R) { return conv_lds_bytes(R + k - 1, kImg, 1, k * k, nt); });
-        const int R2 = choose_rows(m.H2, [&](int R) { return conv_lds_bytes(R + k - 1, m.H1, F, k * k * F, nt); });
+        const int R1 = choose_rows(m.H1, [&](int R) { return conv_lds_bytes(R + k - 1, kImg, 1, k * k, nt); }, kc1, kc2);
+        const int R2 = choose_rows(m.H2, [&](int R) { return conv_lds_bytes(R + k - 1, m.H1, F, k * k * F, nt); }, kc1, kc2);
         // dgrad: 4x4-pixel tiles in bands of 4 rows; 8-row chunks unless only 4 fit 2 blocks/CU
-        const int Rd = (dgrad_lds_bytes(8, k, F, nt) <= ((size_t)78 << 10) || dgrad_lds_bytes(4, k, F, nt) > ((size_t)78 << 10)) ? 8 : 4;
+        const size_t dgb = (size_t)kdg << 10;
+        const int Rd = (dgrad_lds_bytes(8, k, F, nt) <= dgb || dgrad_lds_bytes(4, k, F, nt) > dgb) ? 8 : 4;
         const size_t l1 = conv_lds_bytes(R1 + k - 1, kImg, 1, k * k, nt);
         const size_t l2 = conv_lds_bytes(R2 + k - 1, m.H1, F, k * k * F, nt);
         const size_t ld = dgrad_lds_bytes(Rd, k, F, nt);
-        P.bc1.lds[nt] = std::max(P.bc1.lds[nt], l1);
-        P.bc2.lds[nt] = std::max(P.bc2.lds[nt], l2);
-        P.bdg.lds[nt] = std::max(P.bdg.lds[nt], ld);
+        L1[i] = l1; L2[i] = l2; LD[i] = ld;
         for (int b = 0; b < B; ++b) {
             for (int y = 0; y < m.H1; y += R1) P.conv1.push_back({i, b, y, std::min(R1, m.H1 - y)});
             for (int y = 0; y < m.H2; y += R2) P.conv2.push_back({i, b, y, std::min(R2, m.H2 - y)});
@@ -1113,21 +1250,18 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
             P.per_sample.push_back({i, b});
         }
         P.lds_conv_max = std::max({P.lds_conv_max, l1, l2, ld});
-        // wgrad items
-        const int Rw2 = choose_rows(m.H2, [&](int R) { return wg_lds_bytes(R + k - 1, m.H1, F, R * m.H2, nt); });
-        const int Rw1 = choose_rows(m.H1, [&](int R) { return wg_lds_bytes(R + k - 1, kImg, 1, R * m.H1, nt); });
-        const size_t lw2 = wg_lds_bytes(Rw2 + k - 1, m.H1, F, Rw2 * m.H2, nt);
-        const size_t lw1 = wg_lds_bytes(Rw1 + k - 1, kImg, 1, Rw1 * m.H1, nt);
-        P.bw2.lds[nt] = std::max(P.bw2.lds[nt], lw2);
-        P.bw1.lds[nt] = std::max(P.bw1.lds[nt], lw1);
+        // wgrad items: (member, 512-row m-group, sample group)
+        const size_t lw2 = wg_lds_bytes(k, m.H1, F, m.H2, F);
+        const size_t lw1 = wg_lds_bytes(k, kImg, 1, m.H1, F);
+        LW2[i] = lw2; LW1[i] = lw1;
         const int K2 = k * k * F, K1w = k * k;
         for (int g = 0; g < m.g2; ++g) {
             const int b0 = (int)((long long)B * g / m.g2), b1 = (int)((long long)B * (g + 1) / m.g2);
-            for (int mg = 0; mg * 256 <= K2; ++mg) P.wg2.push_back({i, mg, b0, b1, g, Rw2});
+            for (int mg = 0; mg * kWgRows <= K2; ++mg) P.wg2.push_back({i, mg, b0, b1, g, 0});
         }
         for (int g = 0; g < m.g1; ++g) {
             const int b0 = (int)((long long)B * g / m.g1), b1 = (int)((long long)B * (g + 1) / m.g1);
-            for (int mg = 0; mg * 256 <= K1w; ++mg) P.wg1.push_back({i, mg, b0, b1, g, Rw1});
+            for (int mg = 0; mg * kWgRows <= K1w; ++mg) P.wg1.push_back({i, mg, b0, b1, g, 0});
         }
         P.lds_wg_max = std::max({P.lds_wg_max, lw2, lw1});
         auto tiles = [&](std::vector<GemmItem>& v, int M, int N) {
@@ -1154,11 +1288,11 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
     long long wmax = 0;
     for (auto& m : P.mem) wmax = std::max(wmax, (long long)m.k * m.k * m.F * m.F + m.F);
     P.wred_blocks = (int)((wmax + P.wred_per_block - 1) / P.wred_per_block);
-    bucket_by_nt(P.conv1, P.bc1, P.mem);
-    bucket_by_nt(P.conv2, P.bc2, P.mem);
-    bucket_by_nt(P.dgrad, P.bdg, P.mem);
-    bucket_by_nt(P.wg1, P.bw1, P.mem);
-    bucket_by_nt(P.wg2, P.bw2, P.mem);
+    bucket_segs(P.conv1, P.bc1, P.mem, L1);
+    bucket_segs(P.conv2, P.bc2, P.mem, L2);
+    bucket_segs(P.dgrad, P.bdg, P.mem, LD);
+    bucket_segs(P.wg1, P.bw1, P.mem, LW1);
+    bucket_segs(P.wg2, P.bw2, P.mem, LW2);
 
     // ---- serialise tables (one device upload)
     size_t off = 0;
@@ -1206,16 +1340,6 @@ hipError_t launch_conv_nt(const StepArgs& a, const ConvItem* items, int count, s
     return hipGetLastError();
 }
 
-template <int OP>
-hipError_t launch_conv(const Plan& P, const StepArgs& a, size_t table_off, const Bucketed& bk, hipStream_t s) {
-    const ConvItem* base = dev_table<ConvItem>(P, table_off);
-    hipError_t e;
-    if ((e = launch_conv_nt<OP, 1>(a, base + bk.begin[1], bk.end[1] - bk.begin[1], bk.lds[1], s))) return e;
-    if ((e = launch_conv_nt<OP, 2>(a, base + bk.begin[2], bk.end[2] - bk.begin[2], bk.lds[2], s))) return e;
-    if ((e = launch_conv_nt<OP, 3>(a, base + bk.begin[3], bk.end[3] - bk.begin[3], bk.lds[3], s))) return e;
-    return launch_conv_nt<OP, 4>(a, base + bk.begin[4], bk.end[4] - bk.begin[4], bk.lds[4], s);
-}
-
 template <int NT>
 hipError_t launch_dgrad_nt(const StepArgs& a, const ConvItem* items, int count, size_t lds, hipStream_t s) {
     if (count <= 0) return hipSuccess;
@@ -1225,33 +1349,68 @@ hipError_t launch_dgrad_nt(const StepArgs& a, const ConvItem* items, int count, 
     return hipGetLastError();
 }
 
-hipError_t launch_dgrad(const Plan& P, const StepArgs& a, hipStream_t s) {
-    const ConvItem* base = dev_table<ConvItem>(P, P.off_dgrad);
-    const Bucketed& bk = P.bdg;
-    hipError_t e;
-    if ((e = launch_dgrad_nt<1>(a, base + bk.begin[1], bk.end[1] - bk.begin[1], bk.lds[1], s))) return e;
-    if ((e = launch_dgrad_nt<2>(a, base + bk.begin[2], bk.end[2] - bk.begin[2], bk.lds[2], s))) return e;
-    if ((e = launch_dgrad_nt<3>(a, base + bk.begin[3], bk.end[3] - bk.begin[3], bk.lds[3], s))) return e;
-    return launch_dgrad_nt<4>(a, base + bk.begin[4], bk.end[4] - bk.begin[4], bk.lds[4], s);
-}
-
 template <int OP, int NT>
 hipError_t launch_wg_nt(const StepArgs& a, const WgItem* items, int count, size_t lds, hipStream_t s) {
     if (count <= 0) return hipSuccess;
     auto kern = conv_wgrad_kernel<OP, NT>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3(count), dim3(256), lds, s, a, items);
+    hipLaunchKernelGGL(kern, dim3(count), dim3(kWgThreads), lds, s, a, items);
     return hipGetLastError();
 }
 
+template <class Fn>
+hipError_t launch_segs(Plan& P, const Bucketed& bk, const char* name, hipStream_t s, Fn launch_nt) {
+    for (const Seg& sg : bk.segs) {
+        if (hipError_t e = launch_nt(sg)) return e;
+        P.timer.mark(std::string(name) + "/nt" + std::to_string(sg.nt) +
+                         (P.timer_detail ? "/occ" + std::to_string(lds_class(sg.lds)) + "/n" + std::to_string(sg.end - sg.begin) : ""),
+                     s);
+    }
+    return hipSuccess;
+}
+
+#define MPO_NT_SWITCH(FN, sg, ...)                                     \
+    ((sg).nt == 1 ? FN<1>(__VA_ARGS__)                                 \
+     : (sg).nt == 2 ? FN<2>(__VA_ARGS__)                               \
+     : (sg).nt == 3 ? FN<3>(__VA_ARGS__) : FN<4>(__VA_ARGS__))
+
 template <int OP>
-hipError_t launch_wg(const Plan& P, const StepArgs& a, size_t table_off, const Bucketed& bk, hipStream_t s) {
+struct ConvLaunch {
+    template <int NT>
+    static hipError_t go(const StepArgs& a, const ConvItem* items, int count, size_t lds, hipStream_t s) {
+        return launch_conv_nt<OP, NT>(a, items, count, lds, s);
+    }
+};
+
+template <int OP>
+hipError_t launch_conv(Plan& P, const StepArgs& a, size_t table_off, const Bucketed& bk, hipStream_t s) {
+    const ConvItem* base = dev_table<ConvItem>(P, table_off);
+    return launch_segs(P, bk, OP == CONV1_FWD ? "conv1_fwd" : "conv2_fwd", s, [&](const Seg& sg) {
+        return MPO_NT_SWITCH(ConvLaunch<OP>::template go, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, s);
+    });
+}
+
+hipError_t launch_dgrad(Plan& P, const StepArgs& a, hipStream_t s) {
+    const ConvItem* base = dev_table<ConvItem>(P, P.off_dgrad);
+    return launch_segs(P, P.bdg, "conv2_dgrad", s, [&](const Seg& sg) {
+        return MPO_NT_SWITCH(launch_dgrad_nt, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, s);
+    });
+}
+
+template <int OP>
+struct WgLaunch {
+    template <int NT>
+    static hipError_t go(const StepArgs& a, const WgItem* items, int count, size_t lds, hipStream_t s) {
+        return launch_wg_nt<OP, NT>(a, items, count, lds, s);
+    }
+};
+
+template <int OP>
+hipError_t launch_wg(Plan& P, const StepArgs& a, size_t table_off, const Bucketed& bk, hipStream_t s) {
     const WgItem* base = dev_table<WgItem>(P, table_off);
-    hipError_t e;
-    if ((e = launch_wg_nt<OP, 1>(a, base + bk.begin[1], bk.end[1] - bk.begin[1], bk.lds[1], s))) return e;
-    if ((e = launch_wg_nt<OP, 2>(a, base + bk.begin[2], bk.end[2] - bk.begin[2], bk.lds[2], s))) return e;
-    if ((e = launch_wg_nt<OP, 3>(a, base + bk.begin[3], bk.end[3] - bk.begin[3], bk.lds[3], s))) return e;
-    return launch_wg_nt<OP, 4>(a, base + bk.begin[4], bk.end[4] - bk.begin[4], bk.lds[4], s);
+    return launch_segs(P, bk, OP == WG_CONV1 ? "conv1_wgrad" : "conv2_wgrad", s, [&](const Seg& sg) {
+        return MPO_NT_SWITCH(WgLaunch<OP>::template go, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, s);
+    });
 }
 
 template <int OP>
@@ -1279,22 +1438,29 @@ StepArgs make_args(const Plan& P, const float* x, const int* labels, const int* 
     a.loss_out = nullptr;
     a.loss_sum = nullptr;
     a.correct = nullptr;
+    a.debug = P.debug;
+    a.zero_off = P.zero_off;
     return a;
 }
 
-int forward(const Plan& P, const StepArgs& a, hipStream_t s) {
+int forward(Plan& P, const StepArgs& a, hipStream_t s) {
+    P.timer.mark("start", s);
     // padded / rotated weight copies for this step's convolutions
     hipLaunchKernelGGL(flip_w2_kernel, dim3(64, (unsigned)P.n), dim3(256), 0, s, a, dev_table<MItem>(P, P.off_pm));
     MPO_LAUNCH_CHECK();
+    P.timer.mark("flip_w2", s);
     MPO_HIP(launch_conv<CONV1_FWD>(P, a, P.off_conv1, P.bc1, s));
     MPO_HIP(launch_conv<CONV2_FWD>(P, a, P.off_conv2, P.bc2, s));
     hipLaunchKernelGGL(pool_fwd_kernel, dim3((unsigned)P.per_sample.size()), dim3(256), 0, s, a,
                        dev_table<MItem>(P, P.off_ps));
     MPO_LAUNCH_CHECK();
+    P.timer.mark("pool_fwd", s);
     MPO_HIP(launch_dense<D1_FWD>(P, a, P.off_d1f, P.d1f.size(), s));
     MPO_HIP(launch_dense<D2_FWD>(P, a, P.off_d2f, P.d2f.size(), s));
+    P.timer.mark("dense_fwd", s);
     hipLaunchKernelGGL(softmax_bce_kernel, dim3((unsigned)P.n), dim3(256), 0, s, a, dev_table<MItem>(P, P.off_pm));
     MPO_LAUNCH_CHECK();
+    P.timer.mark("softmax_bce", s);
     return MPO_OK;
 }
 
@@ -1309,6 +1475,9 @@ int mpo_pop_create(const MpoCnnSpec* specs, int n_members, int batch, void** han
     MPO_CHECK_ARG(n_members > 0 && batch > 0 && batch <= 256, "mpo_pop_create: n_members=%d batch=%d (1..256)",
                   n_members, batch);
     auto P = std::make_unique<Plan>();
+    P->timer.on = env_int("MPO_POP_PROFILE", 0) != 0;
+    P->debug = env_int("MPO_POP_DEBUG", 0);
+    P->timer_detail = env_int("MPO_POP_PROFILE", 0) > 1;
     int rc = build_plan(*P, specs, n_members, batch);
     if (rc) return rc;
     *handle = P.release();
@@ -1387,9 +1556,11 @@ int mpo_pop_train_step(void* handle, const float* x, const int32_t* labels, cons
     MPO_HIP(launch_dense<D2_DGRAD>(P, a, P.off_d2d, P.d2d.size(), s));
     MPO_HIP(launch_dense<D1_WGRAD>(P, a, P.off_d1w, P.d1w.size(), s));
     MPO_HIP(launch_dense<D1_DGRAD>(P, a, P.off_d1d, P.d1d.size(), s));
+    P.timer.mark("dense_bwd", s);
     hipLaunchKernelGGL(pool_bwd_kernel, dim3((unsigned)P.per_sample.size()), dim3(256), 0, s, a,
                        dev_table<MItem>(P, P.off_ps));
     MPO_LAUNCH_CHECK();
+    P.timer.mark("pool_bwd", s);
     MPO_HIP(launch_dgrad(P, a, s));
     MPO_HIP(launch_wg<WG_CONV2>(P, a, P.off_wg2, P.bw2, s));
     MPO_HIP(launch_wg<WG_CONV1>(P, a, P.off_wg1, P.bw1, s));
@@ -1398,9 +1569,12 @@ int mpo_pop_train_step(void* handle, const float* x, const int32_t* labels, cons
     MPO_LAUNCH_CHECK();
     hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)P.colsum.size()), dim3(256), 0, s, a, dev_table<MItem>(P, P.off_cs));
     MPO_LAUNCH_CHECK();
+    P.timer.mark("wgrad_reduce", s);
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)P.adam.size()), dim3(256), 0, s, a, dev_table<MItem>(P, P.off_adam),
                        P.params, P.m, P.v, step + 1, 0.9f, 0.999f, 1e-8f, P.adam_chunk);
     MPO_LAUNCH_CHECK();
+    P.timer.mark("adam", s);
+    P.timer.finish();
     return MPO_OK;
     MPO_GUARD_END
 }
@@ -1414,8 +1588,28 @@ int mpo_pop_eval_step(void* handle, const float* x, const int32_t* labels, const
     StepArgs a = make_args(P, x, labels, order, order_stride, row0, 0, 0);
     a.loss_sum = loss_sum;
     a.correct = correct;
-    return forward(P, a, static_cast<hipStream_t>(stream));
+    const int rc = forward(P, a, static_cast<hipStream_t>(stream));
+    P.timer.finish();
+    return rc;
     MPO_GUARD_END
+}
+
+int mpo_pop_profile(void* handle, char* buf, size_t cap, int reset) {
+    MPO_CHECK_ARG(handle && (buf || !cap), "mpo_pop_profile: null pointer");
+    Plan& P = *static_cast<Plan*>(handle);
+    std::string out;
+    for (const auto& pr : P.timer.acc) {
+        char line[128];
+        snprintf(line, sizeof(line), "%s %.6f\n", pr.first.c_str(), pr.second);
+        out += line;
+    }
+    if (cap) {
+        const size_t n = std::min(cap - 1, out.size());
+        std::copy_n(out.data(), n, buf);
+        buf[n] = 0;
+    }
+    if (reset) P.timer.acc.clear();
+    return P.timer.on ? MPO_OK : MPO_ENOTSUP;
 }
 
 int mpo_kfold_gather(const float* X, const int32_t* idx, int64_t rows, int row_elems, float* out, void* stream) {

@@ -214,6 +214,19 @@ class PopulationEngine:
         self.step_count = step + 1
         return self.loss
 
+    def profile(self, reset=True):
+        """Per-phase device ms since the last reset ({phase: ms}); empty unless the
+        engine was created with MPO_POP_PROFILE=1 in the environment."""
+        buf = ctypes.create_string_buffer(8192)
+        rc = lib().mpo_pop_profile(self._h, buf, len(buf), int(reset))
+        if rc != _lib.MPO_OK:
+            return {}
+        out = {}
+        for line in buf.value.decode().splitlines():
+            name, ms = line.split()
+            out[name] = float(ms)
+        return out
+
     def eval_reset(self):
         self.val_loss_sum.zero_()
         self.val_correct.zero_()
