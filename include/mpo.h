@@ -186,6 +186,61 @@ int mpo_pop_eval_step(void* handle, const float* x, const int32_t* labels, const
  * otherwise.  reset != 0 clears the accumulators after the read. */
 int mpo_pop_profile(void* handle, char* buf, size_t cap, int reset);
 
+/* ------------------------------------------------------------------------
+ * DenseNet population (BASELINE config 5).
+ * Replaces the per-block Keras training of DenseNet (densenet.py:135-196, built
+ * by base_model.py:61-72 / mpiLAPI.py:197-201, trained by process_block.py:71-96).
+ * All members share one architecture (the reference grid searches lr only,
+ * base_model.py:84-92); each member has its own lr, weights and sample order.
+ * ---------------------------------------------------------------------- */
+typedef struct MpoDnArch {
+    int32_t H, W, C;          /* img_dim (channels last)                 */
+    int32_t classes;          /* nb_classes                              */
+    int32_t depth;            /* 3 N + 4                                 */
+    int32_t nb_dense_block;
+    int32_t growth;           /* growth_rate                             */
+    int32_t nb_filter;
+} MpoDnArch;
+
+typedef struct MpoDnSizes {
+    int64_t n_params;     /* floats per member in the parameter arena (also grads, adam m, v) */
+    int64_t n_state;      /* floats per member of BN moving statistics                         */
+    int64_t act_floats;   /* floats in the activation arena (all members)                      */
+    int32_t n_members;
+    int32_t batch;
+    int32_t n_layers;
+    int32_t reserved;
+} MpoDnSizes;
+
+int mpo_dn_create(const MpoDnArch* arch, int n_members, int batch, void** handle);
+int mpo_dn_destroy(void* handle);
+int mpo_dn_sizes(const void* handle, MpoDnSizes* out);
+/* Layer i: geom[8] = kind (0 initial conv, 1 dense-block conv, 2 transition, 3 head),
+ * stage, H, W, cin, cout, kernel size, concat channel offset; offs[6] = float
+ * offsets within a member's parameter block of the conv kernel (head: dense kernel),
+ * gamma, beta, and within its state block of moving mean, moving variance, and
+ * (head only) the dense bias; -1 where absent.  Keras shapes: conv (ks,ks,cin,cout),
+ * gamma/beta/moving stats [H] (BatchNormalization axis=1 of NHWC). */
+int mpo_dn_layer(const void* handle, int i, int32_t* geom, int64_t* offs);
+/* Bind caller-owned, zero-initialised device arenas: params/grads/adam_m/adam_v
+ * [n_members][n_params], state [n_members][n_state], act [act_floats]; lr is a
+ * HOST array of n_members learning rates (copied, stream-synchronised). */
+int mpo_dn_bind(void* handle, float* params, float* grads, float* adam_m, float* adam_v, float* state, float* act,
+                const float* lr, void* stream);
+/* One Adam step of every member on rows [row0, row0+batch) of its order table:
+ * sample = order[member*order_stride + row0 + b] into x [n][H][W][C] f32, labels
+ * [n] i32.  BN uses batch statistics and updates the moving averages.
+ * loss_out[member] = mean categorical CE + l2 penalty (before the update);
+ * Adam t = step + 1. */
+int mpo_dn_train_step(void* handle, const float* x, const int32_t* labels, const int32_t* order,
+                      int64_t order_stride, int64_t row0, int32_t step, float* loss_out, void* stream);
+/* Inference-mode forward (BN moving averages) of one batch: loss_sum[member] +=
+ * sum of per-sample CE, correct[member] += argmax hits. */
+int mpo_dn_eval_step(void* handle, const float* x, const int32_t* labels, const int32_t* order,
+                     int64_t order_stride, int64_t row0, float* loss_sum, int32_t* correct, void* stream);
+/* out[member] = 1e-4 * sum of squared parameters (Keras adds it to val_loss). */
+int mpo_dn_penalty(void* handle, float* out, void* stream);
+
 /* k-fold index gather: out[r][:] = X[idx[r]][:] (the fold split
  * that mpi_learn does with per-fold communicators becomes an index gather). */
 int mpo_kfold_gather(const float* X, const int32_t* idx, int64_t rows, int row_elems, float* out,

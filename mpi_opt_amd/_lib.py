@@ -46,6 +46,18 @@ class MpoPopSizes(ctypes.Structure):
                 ("n_members", ctypes.c_int32), ("batch", ctypes.c_int32)]
 
 
+class MpoDnArch(ctypes.Structure):
+    _fields_ = [("H", ctypes.c_int32), ("W", ctypes.c_int32), ("C", ctypes.c_int32), ("classes", ctypes.c_int32),
+                ("depth", ctypes.c_int32), ("nb_dense_block", ctypes.c_int32), ("growth", ctypes.c_int32),
+                ("nb_filter", ctypes.c_int32)]
+
+
+class MpoDnSizes(ctypes.Structure):
+    _fields_ = [("n_params", ctypes.c_int64), ("n_state", ctypes.c_int64), ("act_floats", ctypes.c_int64),
+                ("n_members", ctypes.c_int32), ("batch", ctypes.c_int32), ("n_layers", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _I64 = ctypes.c_int64
@@ -75,6 +87,14 @@ SIGNATURES = {
     "mpo_pop_train_step": (_I, [_P, _P, _P, _P, _I64, _I64, ctypes.c_int32, _P, _P]),
     "mpo_pop_eval_step": (_I, [_P, _P, _P, _P, _I64, _I64, _P, _P, _P]),
     "mpo_pop_profile": (_I, [_P, _P, _SZ, _I]),
+    "mpo_dn_create": (_I, [ctypes.POINTER(MpoDnArch), _I, _I, ctypes.POINTER(ctypes.c_void_p)]),
+    "mpo_dn_destroy": (_I, [_P]),
+    "mpo_dn_sizes": (_I, [_P, ctypes.POINTER(MpoDnSizes)]),
+    "mpo_dn_layer": (_I, [_P, _I, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64)]),
+    "mpo_dn_bind": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "mpo_dn_train_step": (_I, [_P, _P, _P, _P, _I64, _I64, ctypes.c_int32, _P, _P]),
+    "mpo_dn_eval_step": (_I, [_P, _P, _P, _P, _I64, _I64, _P, _P, _P]),
+    "mpo_dn_penalty": (_I, [_P, _P, _P]),
     "mpo_kfold_gather": (_I, [_P, _P, _I64, _I, _P, _P]),
 }
 

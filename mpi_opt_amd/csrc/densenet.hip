@@ -1,0 +1,1215 @@
+// densenet.hip -- the DenseNet population engine for gfx950.
+//
+// Replaces the per-trial Keras training of DenseNet (/root/reference/densenet.py:135-196,
+// compiled by base_model.py:61-72 / mpiLAPI.py:197-201 and trained per MPI block by
+// process_block.py:71-96) with one device-resident population: every member is a
+// (trial, fold) with the SAME architecture (the reference grid fixes depth 10,
+// 3 blocks, growth 12, nb_filter 16, dropout 0 and searches lr only,
+// base_model.py:84-92), so every tensor of every member has one shape and the
+// member index is just the outermost grid dimension of each launch.
+//
+// Layout (fp32, NHWC, member-major per buffer):
+//   cat[s]  [B][H_s][W_s][C_s]  the dense-block concat of stage s: the initial conv /
+//           pooled transition writes channels [0, f0), dense layer l writes its growth
+//           slice [coff_l, coff_l + g) -- concatenation costs nothing;
+//   dcat[s] gradient of cat[s]; the transition / head BN-backward STORES [0, C_s)
+//           first, the dense layers then ACCUMULATE into [0, cin_l) last-to-first;
+//   z[i]    [B][H][W][cin_i] = ELU(BN(cat[..., :cin_i])) of BN site i (the conv input,
+//           kept for the weight gradient and the ELU derivative);
+//   t[i]    transition conv output before AvgPool2.
+//
+// Kernels (all member-batched; MFMA = v_mfma_f32_16x16x4_f32, exact f32):
+//   dn_conv<KS, NT>   implicit-GEMM 'same' conv, M = row-chunk pixels (<=128), N = cout,
+//                     K = KS^2 * cin4: input rows + halo staged once in LDS, weights
+//                     streamed from L2 one 16-k group ahead.  Also the input gradient
+//                     (a 'same' conv of dOut with the rotated/transposed kernel).
+//   dn_wgrad<KS, NT>  M = KS^2 * cin weight rows, N = cout, K = pixels of a sample
+//                     group; partial slabs per group, reduced in fixed order.
+//   dn_bn_fwd / dn_bn_bwd  BatchNormalization(axis=1) of NHWC = per image ROW h:
+//                     one workgroup per (member, h) reduces (B, W, cin) in fp64, then
+//                     applies BN + ELU (fwd) or the BN/ELU backward (bwd).
+//   dn_pool_fwd/bwd, dn_head_fwd/reduce (GAP + dense + softmax + categorical CE),
+//   dn_adam (Keras Adam + l2 1e-4 gradient), dn_prep (padded weight copies).
+#include "mpo_internal.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <memory>
+#include <vector>
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr float kBnEps = 1e-3f;
+constexpr float kBnMomentum = 0.99f;
+constexpr float kL2 = 1e-4f;
+constexpr float kCeEps = 1e-7f;
+constexpr int kWRowsSlack = 48;   // zero weight rows past K16 (the loop reads 2 groups ahead)
+constexpr int kKoffSlack = 64;    // zero tap offsets past K16 (3 groups ahead)
+constexpr int kMaxPix = 128;      // pixels per conv / wgrad workgroup chunk
+
+__host__ __device__ constexpr inline int r4(int x) { return (x + 3) & ~3; }
+__host__ __device__ constexpr inline int r16(int x) { return (x + 15) & ~15; }
+// conv LDS pixel stride = cin4 + 2 == 2 (mod 4): lanes 0-15 (16 pixels, one channel)
+// and lanes 16-31 (the next channel) land on the even / odd banks.
+__host__ __device__ constexpr inline int conv_cp(int cin) { return r4(cin) + 2; }
+// wgrad LDS pixel stride == 16 (mod 32): lanes 0-15 read 16 channels, lanes 16-31
+// the next pixel -> banks 0-15 / 16-31.
+__host__ __device__ constexpr inline int wg_cp(int c) { return c + ((48 - (c & 31)) & 31); }
+// wgrad dOut pixel stride == 16 (mod 32)
+__host__ __device__ constexpr inline int wg_ns(int nt) { return nt * 16 + ((nt & 1) ? 0 : 16); }
+
+// ---- argument blocks ----------------------------------------------------------
+struct ConvArgs {
+    const float* in; long long in_ms; int in_ps;          // input (+ channel offset), member / pixel strides
+    const int* order; long long ord_ms; long long row0;   // sample gather (initial conv only)
+    long long img_floats;
+    const float* w; long long w_ms;                       // padded weights [K16 + slack][N16]
+    float* out; long long out_ms; int out_ps;
+    int H, W, Cin, N, R;
+};
+
+struct WgArgs {
+    const float* in; long long in_ms; int in_ps;
+    const int* order; long long ord_ms; long long row0;
+    long long img_floats;
+    const float* dout; long long dout_ms; int dout_ps;
+    float* part; long long part_ms;                       // [G][Kw][N]
+    int H, W, Cin, N, R, spg, B;
+};
+
+struct BnArgs {
+    const float* x; long long x_ms; int x_ps;             // cat (channels [0, Cin))
+    float* z; long long z_ms;                             // [B][H][W][Cin]
+    float* coef; long long coef_ms;                       // [4][H]: mean, inv, scale, shift
+    const float* params; long long p_ms; long long g_off, b_off;
+    float* state; long long s_ms; long long mm_off, mv_off;
+    float* grads;                                         // member stride p_ms
+    const float* dz; long long dz_ms;                     // [B][H][W][Cin] (bcast == 0)
+    const float* dg; long long dg_ms; float inv_hw;       // [B][Cin] / (H W)  (bcast == 1)
+    float* dx; long long dx_ms; int dx_ps;
+    int B, H, W, Cin, train, bcast, accumulate;
+};
+
+// ---- shared reductions -----------------------------------------------------------
+__device__ __forceinline__ double block_sum(double v, double* red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    double s = 0.0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += red[i];
+    return s;
+}
+
+// ============================================================================
+// Implicit-GEMM 'same' convolution, stride 1 (forward and input gradient).
+// One workgroup = (member, sample b, output rows [y0, y0 + R)); M = R*W <= 128
+// pixels in up to 8 m-tiles of 16 (2 per wave), N = NT tiles of 16.
+// ============================================================================
+template <int MT, int NT>
+__device__ __forceinline__ void dn_conv_loop(const float* __restrict__ img, const int* __restrict__ koff,
+                                             const float* __restrict__ Wt, int N16, int ngroups, const int (&pb)[2],
+                                             f32x4 (&acc)[2][NT], int krow, int kcol) {
+    const float* wsrc = Wt + krow * N16 + kcol;
+    const int* kp = koff + krow * 4;
+    float b0[4][NT], b1[4][NT], a0[4][MT], a1[4][MT];
+    auto loadB = [&](int g, float (&dst)[4][NT]) {
+        const float* src = wsrc + (long long)g * 16 * N16;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) dst[u][j] = src[u * 4 * N16 + j * 16];
+    };
+    auto kof = [&](int g) { return *reinterpret_cast<const int4*>(kp + g * 16); };
+    auto readA = [&](const int4 ko, float (&dst)[4][MT]) {
+        const int kov[4] = {ko.x, ko.y, ko.z, ko.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int i = 0; i < MT; ++i) dst[u][i] = img[pb[i] + kov[u]];
+    };
+    auto mma = [&](const float (&av)[4][MT], const float (&bw)[4][NT]) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][i], bw[u][j], acc[i][j], 0, 0, 0);
+    };
+    loadB(0, b0);
+    int4 ko = kof(0);
+    readA(ko, a0);
+    ko = kof(1);
+    // two 16-k groups per iteration (an odd count runs one zero group from the slack)
+    for (int g = 0; g < ngroups; g += 2) {
+        loadB(g + 1, b1);
+        readA(ko, a1);
+        ko = kof(g + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        loadB(g + 2, b0);
+        readA(ko, a0);
+        ko = kof(g + 3);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(a1, b1);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int KS, int NT>
+__global__ __launch_bounds__(256) void dn_conv_kernel(ConvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int P = (KS - 1) / 2;
+    const int m = blockIdx.z, b = blockIdx.y, y0 = blockIdx.x * a.R;
+    const int H = a.H, W = a.W, Cin = a.Cin;
+    const int rows_out = min(a.R, H - y0);
+    const int Wp = W + KS - 1;
+    const int Cin4 = r4(Cin), Cp = conv_cp(Cin);
+    const int rows = a.R + KS - 1;
+    const float* src = a.order ? a.in + (long long)a.order[m * a.ord_ms + a.row0 + b] * a.img_floats
+                               : a.in + m * a.in_ms + (long long)b * H * W * a.in_ps;
+    float* img = smem;
+    const int row_elems = Wp * Cp;
+    const int img_elems = rows * row_elems;
+    int* koff = reinterpret_cast<int*>(smem + r4(img_elems));
+    const int K = KS * KS * Cin4, K16 = r16(K);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int krow = lane >> 4, kcol = lane & 15;
+
+    for (int e = tid; e < img_elems; e += 256) {
+        const int r = e / row_elems, rem = e - r * row_elems;
+        const int col = rem / Cp, c = rem - col * Cp;
+        const int gy = y0 + r - P, gx = col - P;
+        float v = 0.f;
+        if (gy >= 0 && gy < H && gx >= 0 && gx < W && c < Cin) v = src[((long long)gy * W + gx) * a.in_ps + c];
+        img[e] = v;
+    }
+    // tap offsets, each 16-k group stored as [krow][u] so a lane reads its four
+    // k-steps (k = g*16 + u*4 + krow) as one b128
+    for (int kq = tid; kq < K16 + kKoffSlack; kq += 256) {
+        const int kk = (kq & ~15) + ((kq & 3) << 2) + ((kq >> 2) & 3);
+        int off = 0;
+        if (kk < K) {
+            const int tap = kk / Cin4, c = kk - tap * Cin4;
+            const int ky = tap / KS, kx = tap - ky * KS;
+            off = (ky * Wp + kx) * Cp + c;
+        }
+        koff[kq] = off;
+    }
+    const int Mc = rows_out * W;
+    const int mtiles = (Mc + 15) >> 4;
+    const int mine = __builtin_amdgcn_readfirstlane(mtiles > wave + 4 ? 2 : (mtiles > wave ? 1 : 0));
+    int pb[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int mm = (wave + 4 * i) * 16 + (lane & 15);
+        pb[i] = mm < Mc ? ((mm / W) * Wp + (mm % W)) * Cp : 0;
+    }
+    f32x4 acc[2][NT];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+    const int ngroups = K16 >> 4;
+    const float* Wt = a.w + m * a.w_ms;
+    const int N16 = NT * 16;
+    if (mine == 2) dn_conv_loop<2, NT>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
+    else if (mine == 1) dn_conv_loop<1, NT>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
+    else return;
+
+    float* dst = a.out + m * a.out_ms + ((long long)b * H + y0) * W * a.out_ps;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        if (i >= mine) break;
+        const int mt = wave + 4 * i;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int n = j * 16 + kcol;
+            if (n >= a.N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int mm = mt * 16 + krow * 4 + r;
+                if (mm < Mc) dst[(long long)mm * a.out_ps + n] = acc[i][j][r];
+            }
+        }
+    }
+}
+
+// ============================================================================
+// Weight gradient: dW[(ky,kx,c)][n] = sum_{b,y,x} in[b][y+ky-P][x+kx-P][c] * dout[b][y][x][n]
+// One workgroup = (member, 256-row m-group, group of spg samples); loops over its
+// samples' row chunks (<= 128 pixels), staging the input rows (+ halo) and the
+// dOut rows in LDS; 4 waves x up to 4 m-tiles.  One partial slab per group.
+// ============================================================================
+template <int MT, int NT>
+__device__ __forceinline__ void dn_wgrad_chunk(const float* __restrict__ img, const float* __restrict__ dl,
+                                               const int* __restrict__ ptab, const int (&aoff)[4], int ns, int nk4,
+                                               int krow, int kcol, f32x4 (&acc)[4][NT]) {
+    float a0[MT], a1[MT], b0[NT], b1[NT];
+    auto rd = [&](int s, float (&av)[MT], float (&bv)[NT]) {
+        const int p = 4 * s + krow;
+        const int po = ptab[p];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) av[i] = img[aoff[i] + po];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) bv[j] = dl[p * ns + j * 16 + kcol];
+    };
+    auto mma = [&](const float (&av)[MT], const float (&bv)[NT]) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    };
+    rd(0, a0, b0);
+    for (int s = 0; s < nk4; s += 2) {
+        rd(s + 1, a1, b1);   // s + 1 <= nk4: the tables hold one zero k-step of slack
+        __builtin_amdgcn_sched_barrier(0);
+        mma(a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 1 >= nk4) break;
+        rd(s + 2, a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(a1, b1);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int KS, int NT>
+__global__ __launch_bounds__(256) void dn_wgrad_kernel(WgArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int P = (KS - 1) / 2;
+    const int m = blockIdx.z, grp = blockIdx.y, mg = blockIdx.x;
+    const int H = a.H, W = a.W, Cin = a.Cin, N = a.N;
+    const int Kw = KS * KS * Cin;
+    const int Wp = W + KS - 1;
+    const int Cp = wg_cp(Cin);
+    const int ns = wg_ns(NT);
+    const int R = a.R;
+    const int rows = R + KS - 1;
+    const int row_elems = Wp * Cp;
+    const int img_elems = rows * row_elems;
+    const int np = 4 * (((R * W + 3) >> 2) + 1);   // pixel slots incl. one zero k-step of slack
+    float* img = smem;
+    float* dl = smem + r4(img_elems);
+    int* ptab = reinterpret_cast<int*>(dl + np * ns);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int krow = lane >> 4, kcol = lane & 15;
+    const int mtiles = (Kw + 15) >> 4;
+    const int t0 = mg * 16;
+    const int mine = __builtin_amdgcn_readfirstlane(min(4, max(0, (mtiles - t0 - wave + 3) / 4)));
+    if (mine == 0 && mtiles - t0 <= 0) return;   // whole workgroup idle (never happens for a sized grid)
+
+    int aoff[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = (t0 + wave + 4 * i) * 16 + (lane & 15);
+        int off = 0;   // rows past Kw read finite LDS; their partials are never stored
+        if (r < Kw) {
+            const int tap = r / Cin, c = r - tap * Cin;
+            const int ky = tap / KS, kx = tap - ky * KS;
+            off = (ky * Wp + kx) * Cp + c;
+        }
+        aoff[i] = off;
+    }
+    for (int p = tid; p < np; p += 256) ptab[p] = p < R * W ? ((p / W) * Wp + (p % W)) * Cp : 0;
+    f32x4 acc[4][NT];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int b0 = grp * a.spg, b1 = min(a.B, b0 + a.spg);
+    const float* inm = a.in + m * a.in_ms;
+    const float* dom = a.dout + m * a.dout_ms;
+    for (int b = b0; b < b1; ++b) {
+        const float* src = a.order ? a.in + (long long)a.order[m * a.ord_ms + a.row0 + b] * a.img_floats
+                                   : inm + (long long)b * H * W * a.in_ps;
+        for (int y0 = 0; y0 < H; y0 += R) {
+            const int Mc = min(R, H - y0) * W;
+            __syncthreads();   // the previous chunk's MFMAs are done with the LDS
+            for (int e = tid; e < img_elems; e += 256) {
+                const int r = e / row_elems, rem = e - r * row_elems;
+                const int col = rem / Cp, c = rem - col * Cp;
+                const int gy = y0 + r - P, gx = col - P;
+                float v = 0.f;
+                if (gy >= 0 && gy < H && gx >= 0 && gx < W && c < Cin) v = src[((long long)gy * W + gx) * a.in_ps + c];
+                img[e] = v;
+            }
+            const float* dsrc = dom + ((long long)b * H + y0) * W * a.dout_ps;
+            for (int e = tid; e < np * ns; e += 256) {
+                const int p = e / ns, n = e - p * ns;
+                dl[e] = (p < Mc && n < N) ? dsrc[(long long)p * a.dout_ps + n] : 0.f;
+            }
+            __syncthreads();
+            const int nk4 = (Mc + 3) >> 2;
+            if (mine == 4) dn_wgrad_chunk<4, NT>(img, dl, ptab, aoff, ns, nk4, krow, kcol, acc);
+            else if (mine == 3) dn_wgrad_chunk<3, NT>(img, dl, ptab, aoff, ns, nk4, krow, kcol, acc);
+            else if (mine == 2) dn_wgrad_chunk<2, NT>(img, dl, ptab, aoff, ns, nk4, krow, kcol, acc);
+            else if (mine == 1) dn_wgrad_chunk<1, NT>(img, dl, ptab, aoff, ns, nk4, krow, kcol, acc);
+        }
+    }
+    float* part = a.part + m * a.part_ms + (long long)grp * Kw * N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (i >= mine) break;
+        const int mt = t0 + wave + 4 * i;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int n = j * 16 + kcol;
+            if (n >= N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = mt * 16 + krow * 4 + r;
+                if (row < Kw) part[(long long)row * N + n] = acc[i][j][r];
+            }
+        }
+    }
+}
+
+// grads[w_off + e] = sum_g part[g][e]  (fixed order: deterministic)
+__global__ void dn_wgrad_reduce_kernel(const float* __restrict__ part, long long part_ms, int G, long long cnt,
+                                       float* __restrict__ grads, long long g_ms, long long w_off) {
+    const int m = blockIdx.y;
+    const float* pm = part + m * part_ms;
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < cnt; e += (long long)gridDim.x * blockDim.x) {
+        float s = 0.f;
+        for (int g = 0; g < G; ++g) s += pm[g * cnt + e];
+        grads[m * g_ms + w_off + e] = s;
+    }
+}
+
+// Padded weight copies.  Forward: dst[(tap*cin4 + c)][n] = w[tap][c][n].
+// Input gradient (transpose = 1): dst[(tap'*cout4 + f)][c] = w[KS^2-1-tap'][c][f].
+__global__ void dn_prep_kernel(const float* __restrict__ params, long long p_ms, long long w_off, float* __restrict__ dst,
+                               long long d_ms, int taps, int cin, int cout, int rows, int n16, int transpose) {
+    const int m = blockIdx.y;
+    const float* w = params + m * p_ms + w_off;
+    float* d = dst + m * d_ms;
+    const int total = rows * n16;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+        const int k = e / n16, n = e - k * n16;
+        float v = 0.f;
+        if (!transpose) {
+            const int c4 = r4(cin), tap = k / c4, c = k - tap * c4;
+            if (tap < taps && c < cin && n < cout) v = w[((long long)tap * cin + c) * cout + n];
+        } else {
+            const int f4 = r4(cout), tp = k / f4, f = k - tp * f4;
+            if (tp < taps && f < cout && n < cin) v = w[((long long)(taps - 1 - tp) * cin + n) * cout + f];
+        }
+        d[e] = v;
+    }
+}
+
+// ============================================================================
+// BatchNormalization(mode=0, axis=1) of an NHWC tensor: statistics per image row h
+// over (batch, W, channels) -- densenet.py:24-27 -- then ELU.  One workgroup per
+// (h, member).  Element order: (w, c) pairs of the row, each over all samples b.
+// ============================================================================
+__global__ __launch_bounds__(256) void dn_bn_fwd_kernel(BnArgs a) {
+    __shared__ double red[4];
+    __shared__ float sc[2];
+    const int h = blockIdx.x, m = blockIdx.y, tid = threadIdx.x;
+    const int H = a.H, W = a.W, Cin = a.Cin, B = a.B;
+    const int rowe = W * Cin;
+    const long long bstride = (long long)H * W * a.x_ps;
+    const float* xm = a.x + m * a.x_ms + (long long)h * W * a.x_ps;
+    const float* pm = a.params + m * a.p_ms;
+    float* coef = a.coef + m * a.coef_ms;
+    float mean, var;
+    if (a.train) {
+        double s = 0.0;
+        for (int e = tid; e < rowe; e += 256) {
+            const int w = e / Cin, c = e - w * Cin;
+            const float* p = xm + (long long)w * a.x_ps + c;
+            for (int b = 0; b < B; ++b) s += p[b * bstride];
+        }
+        const double n = (double)B * rowe;
+        const double mu = block_sum(s, red) / n;
+        double q = 0.0;
+        for (int e = tid; e < rowe; e += 256) {
+            const int w = e / Cin, c = e - w * Cin;
+            const float* p = xm + (long long)w * a.x_ps + c;
+            for (int b = 0; b < B; ++b) {
+                const double d = p[b * bstride] - mu;
+                q += d * d;
+            }
+        }
+        const double vr = block_sum(q, red) / n;
+        mean = (float)mu;
+        var = (float)vr;
+        if (tid == 0) {
+            float* st = a.state + m * a.s_ms;
+            st[a.mm_off + h] = kBnMomentum * st[a.mm_off + h] + (1.f - kBnMomentum) * mean;
+            st[a.mv_off + h] = kBnMomentum * st[a.mv_off + h] + (1.f - kBnMomentum) * var;
+        }
+    } else {
+        const float* st = a.state + m * a.s_ms;
+        mean = st[a.mm_off + h];
+        var = st[a.mv_off + h];
+    }
+    const float inv = (float)(1.0 / sqrt((double)var + (double)kBnEps));
+    const float gam = pm[a.g_off + h], bet = pm[a.b_off + h];
+    if (tid == 0) {
+        coef[h] = mean;
+        coef[H + h] = inv;
+        sc[0] = gam * inv;
+        sc[1] = bet - mean * gam * inv;
+    }
+    __syncthreads();
+    const float s = sc[0], t = sc[1];
+    float* zm = a.z + m * a.z_ms + (long long)h * rowe;
+    const long long zb = (long long)H * rowe;
+    for (int e = tid; e < rowe; e += 256) {
+        const int w = e / Cin, c = e - w * Cin;
+        const float* p = xm + (long long)w * a.x_ps + c;
+        for (int b = 0; b < B; ++b) {
+            const float y = p[b * bstride] * s + t;
+            zm[b * zb + e] = y > 0.f ? y : expm1f(y);
+        }
+    }
+}
+
+// BN + ELU backward for one (h, member): dy = dz * ELU'(z); dgamma = sum dy xhat,
+// dbeta = sum dy; dx = gamma inv / n (n dy - dbeta - xhat dgamma) into dcat (store or add).
+__global__ __launch_bounds__(256) void dn_bn_bwd_kernel(BnArgs a) {
+    __shared__ double red[4];
+    const int h = blockIdx.x, m = blockIdx.y, tid = threadIdx.x;
+    const int H = a.H, W = a.W, Cin = a.Cin, B = a.B;
+    const int rowe = W * Cin;
+    const long long xb = (long long)H * W * a.x_ps, zb = (long long)H * rowe;
+    const float* xm = a.x + m * a.x_ms + (long long)h * W * a.x_ps;
+    const float* zm = a.z + m * a.z_ms + (long long)h * rowe;
+    const float* dzm = a.bcast ? nullptr : a.dz + m * a.dz_ms + (long long)h * rowe;
+    const float* dgm = a.bcast ? a.dg + m * a.dg_ms : nullptr;
+    const float* coef = a.coef + m * a.coef_ms;
+    const float mean = coef[h], inv = coef[H + h];
+    const float gam = a.params[m * a.p_ms + a.g_off + h];
+    auto dy_at = [&](int b, int e, int c) {
+        const float zz = zm[b * zb + e];
+        const float d = a.bcast ? dgm[b * Cin + c] * a.inv_hw : dzm[b * zb + e];
+        return d * (zz > 0.f ? 1.f : zz + 1.f);
+    };
+    double sdy = 0.0, sdyx = 0.0;
+    for (int e = tid; e < rowe; e += 256) {
+        const int w = e / Cin, c = e - w * Cin;
+        const float* p = xm + (long long)w * a.x_ps + c;
+        for (int b = 0; b < B; ++b) {
+            const float dy = dy_at(b, e, c);
+            const float xh = (p[b * xb] - mean) * inv;
+            sdy += dy;
+            sdyx += (double)dy * xh;
+        }
+    }
+    const double dbeta = block_sum(sdy, red);
+    const double dgamma = block_sum(sdyx, red);
+    if (tid == 0) {
+        float* gm = a.grads + m * a.p_ms;
+        gm[a.g_off + h] = (float)dgamma;
+        gm[a.b_off + h] = (float)dbeta;
+    }
+    const float n = (float)B * rowe;
+    const float ca = gam * inv / n, fb = (float)dbeta, fg = (float)dgamma;
+    float* dxm = a.dx + m * a.dx_ms + (long long)h * W * a.dx_ps;
+    const long long db = (long long)H * W * a.dx_ps;
+    for (int e = tid; e < rowe; e += 256) {
+        const int w = e / Cin, c = e - w * Cin;
+        const float* p = xm + (long long)w * a.x_ps + c;
+        float* q = dxm + (long long)w * a.dx_ps + c;
+        for (int b = 0; b < B; ++b) {
+            const float dy = dy_at(b, e, c);
+            const float xh = (p[b * xb] - mean) * inv;
+            const float v = ca * (n * dy - fb - xh * fg);
+            if (a.accumulate) q[b * db] += v; else q[b * db] = v;
+        }
+    }
+}
+
+// AvgPool2D((2,2), strides 2, valid): t [B][H][W][C] -> cat' [B][H/2][W/2][.] channels [0, C)
+__global__ void dn_pool_fwd_kernel(const float* __restrict__ t, long long t_ms, float* __restrict__ out, long long o_ms,
+                                   int o_ps, int B, int H, int W, int C) {
+    const int m = blockIdx.y, H2 = H / 2, W2 = W / 2;
+    const long long total = (long long)B * H2 * W2 * C;
+    const float* tm = t + m * t_ms;
+    float* om = out + m * o_ms;
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+        const int c = (int)(e % C);
+        const long long pix = e / C;
+        const int x = (int)(pix % W2);
+        const long long r = pix / W2;
+        const int y = (int)(r % H2), b = (int)(r / H2);
+        const float* s = tm + (((long long)b * H + 2 * y) * W + 2 * x) * C + c;
+        om[pix * o_ps + c] = 0.25f * (s[0] + s[C] + s[(long long)W * C] + s[(long long)W * C + C]);
+    }
+}
+
+__global__ void dn_pool_bwd_kernel(const float* __restrict__ dcat, long long d_ms, int d_ps, float* __restrict__ dt,
+                                   long long t_ms, int B, int H, int W, int C) {
+    const int m = blockIdx.y, H2 = H / 2, W2 = W / 2;
+    const long long total = (long long)B * H * W * C;
+    const float* dm = dcat + m * d_ms;
+    float* tm = dt + m * t_ms;
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+        const int c = (int)(e % C);
+        const long long pix = e / C;
+        const int x = (int)(pix % W);
+        const long long r = pix / W;
+        const int y = (int)(r % H), b = (int)(r / H);
+        float v = 0.f;
+        if ((y >> 1) < H2 && (x >> 1) < W2) v = 0.25f * dm[(((long long)b * H2 + (y >> 1)) * W2 + (x >> 1)) * d_ps + c];
+        tm[e] = v;
+    }
+}
+
+// ============================================================================
+// Head: GlobalAveragePooling -> Dense(classes) -> softmax -> categorical CE.
+// dn_head_fwd: one workgroup per (sample, member).  Writes g [B][C], per-sample CE,
+// correct flag and dlogits = live * (p - onehot) / B (Keras: p /= sum p, clip to
+// [1e-7, 1 - 1e-7]: a clipped target has zero gradient).
+// ============================================================================
+struct HeadArgs {
+    const float* z; long long z_ms;
+    const float* params; long long p_ms; long long wd_off, bd_off;
+    float* grads;
+    float* g; float* dl; float* ce; float* dg; long long h_ms;   // head scratch, member stride h_ms
+    const int* labels; const int* order; long long ord_ms; long long row0;
+    float* loss_out; float* loss_sum; int* correct;
+    int B, HW, C, classes, train;
+};
+
+__global__ __launch_bounds__(256) void dn_head_fwd_kernel(HeadArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float hs[];
+    const int b = blockIdx.x, m = blockIdx.y, tid = threadIdx.x;
+    const int C = a.C, K = a.classes, HW = a.HW, B = a.B;
+    float* g = hs;          // [C]
+    float* lg = hs + C;     // [K]
+    const float* zb = a.z + m * a.z_ms + (long long)b * HW * C;
+    const float inv_hw = 1.f / HW;
+    for (int c = tid; c < C; c += 256) {
+        float s = 0.f;
+        for (int p = 0; p < HW; ++p) s += zb[(long long)p * C + c];
+        s *= inv_hw;
+        g[c] = s;
+        a.g[m * a.h_ms + (long long)b * C + c] = s;
+    }
+    __syncthreads();
+    const float* pm = a.params + m * a.p_ms;
+    for (int j = tid; j < K; j += 256) {
+        float s = pm[a.bd_off + j];
+        for (int c = 0; c < C; ++c) s += g[c] * pm[a.wd_off + (long long)c * K + j];
+        lg[j] = s;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const int y = a.labels[a.order[m * a.ord_ms + a.row0 + b]];
+        float mx = lg[0];
+        int arg = 0;
+        for (int j = 1; j < K; ++j)
+            if (lg[j] > mx) { mx = lg[j]; arg = j; }
+        float S = 0.f;
+        for (int j = 0; j < K; ++j) { lg[j] = expf(lg[j] - mx); S += lg[j]; }
+        float S2 = 0.f;
+        for (int j = 0; j < K; ++j) { lg[j] /= S; S2 += lg[j]; }
+        for (int j = 0; j < K; ++j) lg[j] /= S2;
+        const float pt = lg[y];
+        const float pc = fminf(fmaxf(pt, kCeEps), 1.f - kCeEps);
+        float* hm = a.ce + m * a.h_ms;
+        hm[b] = -logf(pc);
+        hm[B + b] = arg == y ? 1.f : 0.f;
+        const float live = (pt >= kCeEps && pt <= 1.f - kCeEps) ? 1.f : 0.f;
+        float* dl = a.dl + m * a.h_ms + (long long)b * K;
+        for (int j = 0; j < K; ++j) dl[j] = live * (lg[j] - (j == y ? 1.f : 0.f)) / B;
+    }
+}
+
+// One workgroup per member.  Train: loss_out = mean CE + l2 penalty; dense grads;
+// dg = dlogits . wd^T.  Eval: loss_sum += sum CE, correct += sum correct.
+__global__ __launch_bounds__(256) void dn_head_reduce_kernel(HeadArgs a, long long n_params) {
+    __shared__ double red[4];
+    const int m = blockIdx.x, tid = threadIdx.x;
+    const int C = a.C, K = a.classes, B = a.B;
+    const float* hm = a.ce + m * a.h_ms;
+    double s = 0.0, cor = 0.0;
+    for (int b = tid; b < B; b += 256) { s += hm[b]; cor += hm[B + b]; }
+    const double ce_sum = block_sum(s, red);
+    const double cor_sum = block_sum(cor, red);
+    if (!a.train) {
+        if (tid == 0) {
+            a.loss_sum[m] += (float)ce_sum;
+            a.correct[m] += (int)(cor_sum + 0.5);
+        }
+        return;
+    }
+    const float* pm = a.params + m * a.p_ms;
+    double pen = 0.0;
+    for (long long i = tid; i < n_params; i += 256) pen += (double)pm[i] * pm[i];
+    pen = block_sum(pen, red);
+    if (tid == 0) a.loss_out[m] = (float)(ce_sum / B + (double)kL2 * pen);
+    const float* g = a.g + m * a.h_ms;
+    const float* dl = a.dl + m * a.h_ms;
+    float* gm = a.grads + m * a.p_ms;
+    for (int e = tid; e < C * K; e += 256) {
+        const int c = e / K, j = e - c * K;
+        float v = 0.f;
+        for (int b = 0; b < B; ++b) v += g[(long long)b * C + c] * dl[(long long)b * K + j];
+        gm[a.wd_off + e] = v;
+    }
+    for (int j = tid; j < K; j += 256) {
+        float v = 0.f;
+        for (int b = 0; b < B; ++b) v += dl[(long long)b * K + j];
+        gm[a.bd_off + j] = v;
+    }
+    float* dg = a.dg + m * a.h_ms;
+    for (int e = tid; e < B * C; e += 256) {
+        const int b = e / C, c = e - b * C;
+        float v = 0.f;
+        for (int j = 0; j < K; ++j) v += dl[(long long)b * K + j] * pm[a.wd_off + (long long)c * K + j];
+        dg[e] = v;
+    }
+}
+
+// Per-member l2 penalty 1e-4 * sum w^2 (Keras adds it to loss and val_loss).
+__global__ __launch_bounds__(256) void dn_penalty_kernel(const float* __restrict__ params, long long p_ms, long long n,
+                                                         float* __restrict__ out) {
+    __shared__ double red[4];
+    const float* pm = params + blockIdx.x * p_ms;
+    double s = 0.0;
+    for (long long i = threadIdx.x; i < n; i += 256) s += (double)pm[i] * pm[i];
+    s = block_sum(s, red);
+    if (threadIdx.x == 0) out[blockIdx.x] = (float)((double)kL2 * s);
+}
+
+// Keras Adam with the l2(1e-4) gradient 2e-4 w folded in (every DenseNet tensor is
+// regularised: conv kernels, gamma/beta, dense kernel + bias -- densenet.py:24-33, 188-191).
+__global__ void dn_adam_kernel(float* __restrict__ params, float* __restrict__ grads, float* __restrict__ mo,
+                               float* __restrict__ vo, long long p_ms, long long n, const float* __restrict__ lr, int t) {
+    const int m = blockIdx.y;
+    const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
+    const double corr = sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t));
+    const float lr_t = (float)(lr[m] * corr);
+    const long long base = m * p_ms;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const float w = params[base + i];
+        const float g = grads[base + i] + 2.f * kL2 * w;
+        const float mm = b1 * mo[base + i] + (1.f - b1) * g;
+        const float vv = b2 * vo[base + i] + (1.f - b2) * g * g;
+        mo[base + i] = mm;
+        vo[base + i] = vv;
+        params[base + i] = w - lr_t * mm / (sqrtf(vv) + eps);
+    }
+}
+
+// ============================================================================
+// Host plan
+// ============================================================================
+enum Kind { K_CONV0 = 0, K_DENSE = 1, K_TRANS = 2, K_HEAD = 3 };
+
+struct Layer {
+    int kind, stage, H, W, cin, cout, ks, coff;
+    long long w_off = -1, g_off = -1, b_off = -1, mm_off = -1, mv_off = -1;   // params / state
+    long long wf_off = -1, wd_off_act = -1;    // padded fwd / dgrad weights (act arena)
+    int wf_rows = 0, wf_n16 = 0, wd_rows = 0, wd_n16 = 0;
+    long long z_off = -1, t_off = -1, coef_off = -1;
+    int G = 1, spg = 1, R = 1, Rw = 1;
+};
+
+struct DnPlan {
+    MpoDnArch arch{};
+    int n = 0, B = 0;
+    std::vector<Layer> layers;
+    std::vector<int> sH, sW, sC;
+    std::vector<long long> cat_off, dcat_off, cat_sz;
+    long long n_params = 0, n_state = 0, act_floats = 0;
+    long long wd_off = 0, bd_off = 0;
+    // member strides of the activation buffers (floats)
+    std::vector<long long> cat_ms;
+    long long z_ms_max = 0;
+    long long dz_off = 0, dz_ms = 0, dt_off = 0, dt_ms = 0, part_off = 0, part_ms = 0;
+    long long head_off = 0, head_ms = 0, lr_off = 0;
+    float *params = nullptr, *grads = nullptr, *m = nullptr, *v = nullptr, *state = nullptr, *act = nullptr;
+    bool bound = false;
+};
+
+// (member stride, offset) allocator over the member-major activation arena
+struct Arena {
+    long long used = 0;
+    int n;
+    explicit Arena(int n_) : n(n_) {}
+    // returns the offset; the per-member stride is the aligned size
+    long long take(long long per_member, long long* ms) {
+        const long long s = (per_member + 63) & ~63LL;
+        const long long off = used;
+        used += s * n;
+        *ms = s;
+        return off;
+    }
+};
+
+// Choose rows per chunk so that R * W <= kMaxPix pixels.
+int rows_per_chunk(int H, int W) { return std::max(1, std::min(H, kMaxPix / std::max(1, W))); }
+
+size_t conv_lds(int R, int W, int ks, int cin) {
+    const int img = (R + ks - 1) * (W + ks - 1) * conv_cp(cin);
+    return (size_t)(r4(img) + r16(ks * ks * r4(cin)) + kKoffSlack) * sizeof(float);
+}
+
+size_t wg_lds(int R, int W, int ks, int cin, int nt) {
+    const int img = (R + ks - 1) * (W + ks - 1) * wg_cp(cin);
+    const int np = 4 * (((R * W + 3) >> 2) + 1);
+    return (size_t)(r4(img) + np * wg_ns(nt) + np) * sizeof(float);
+}
+
+int build_plan(DnPlan& p) {
+    const MpoDnArch& A = p.arch;
+    const int L = (A.depth - 4) / 3;
+    int H = A.H, W = A.W, f = A.nb_filter, stage = 0;
+    auto& ls = p.layers;
+    ls.push_back(Layer{K_CONV0, 0, H, W, A.C, f, 3, 0});
+    for (int blk = 0; blk < A.nb_dense_block; ++blk) {
+        for (int l = 0; l < L; ++l) {
+            ls.push_back(Layer{K_DENSE, stage, H, W, f, A.growth, 3, f});
+            f += A.growth;
+        }
+        if (blk < A.nb_dense_block - 1) {
+            ls.push_back(Layer{K_TRANS, stage, H, W, f, f, 1, 0});
+            p.sH.push_back(H); p.sW.push_back(W); p.sC.push_back(f);
+            H /= 2; W /= 2;
+            ++stage;
+        }
+    }
+    ls.push_back(Layer{K_HEAD, stage, H, W, f, A.classes, 0, 0});
+    p.sH.push_back(H); p.sW.push_back(W); p.sC.push_back(f);
+    for (auto& ly : ls)
+        if (ly.H < 1 || ly.W < 1 || ly.W > kMaxPix) return MPO_ENOTSUP;
+    if (f > 1024 || A.classes > 1024) return MPO_ENOTSUP;
+
+    // parameters (Keras creation order), 16-float aligned; moving stats
+    long long po = 0, so = 0;
+    auto take = [](long long& o, long long cnt) { const long long r = o; o += (cnt + 15) & ~15LL; return r; };
+    for (auto& ly : ls) {
+        if (ly.kind == K_CONV0) {
+            ly.w_off = take(po, 9LL * ly.cin * ly.cout);
+        } else if (ly.kind == K_HEAD) {
+            ly.g_off = take(po, ly.H);
+            ly.b_off = take(po, ly.H);
+            p.wd_off = take(po, (long long)ly.cin * ly.cout);
+            p.bd_off = take(po, ly.cout);
+            ly.mm_off = take(so, ly.H);
+            ly.mv_off = take(so, ly.H);
+        } else {
+            ly.g_off = take(po, ly.H);
+            ly.b_off = take(po, ly.H);
+            ly.w_off = take(po, (long long)ly.ks * ly.ks * ly.cin * ly.cout);
+            ly.mm_off = take(so, ly.H);
+            ly.mv_off = take(so, ly.H);
+        }
+    }
+    p.n_params = (po + 63) & ~63LL;
+    p.n_state = (so + 63) & ~63LL;
+
+    // activation arena
+    Arena ar(p.n);
+    const int B = p.B;
+    const int S = (int)p.sH.size();
+    p.cat_off.resize(S); p.dcat_off.resize(S); p.cat_ms.resize(S);
+    for (int s = 0; s < S; ++s) {
+        const long long sz = (long long)B * p.sH[s] * p.sW[s] * p.sC[s];
+        long long ms;
+        p.cat_off[s] = ar.take(sz, &ms);
+        p.dcat_off[s] = ar.take(sz, &ms);
+        p.cat_ms[s] = ms;
+    }
+    long long dz_max = 0, dt_max = 0, part_max = 0;
+    const int target = 2048;
+    for (auto& ly : ls) {
+        long long ms;
+        if (ly.kind != K_CONV0) {
+            ly.z_off = ar.take((long long)B * ly.H * ly.W * ly.cin, &ms);
+            ly.coef_off = ar.take(4LL * ly.H, &ms);
+            dz_max = std::max(dz_max, (long long)B * ly.H * ly.W * ly.cin);
+        }
+        if (ly.kind == K_TRANS) {
+            ly.t_off = ar.take((long long)B * ly.H * ly.W * ly.cout, &ms);
+            dt_max = std::max(dt_max, (long long)B * ly.H * ly.W * ly.cout);
+        }
+        if (ly.kind != K_HEAD) {
+            const int taps = ly.ks * ly.ks;
+            ly.wf_n16 = r16(ly.cout);
+            ly.wf_rows = r16(taps * r4(ly.cin)) + kWRowsSlack;
+            ly.wf_off = ar.take((long long)ly.wf_rows * ly.wf_n16, &ms);
+            if (ly.kind != K_CONV0) {
+                ly.wd_n16 = r16(ly.cin);
+                ly.wd_rows = r16(taps * r4(ly.cout)) + kWRowsSlack;
+                ly.wd_off_act = ar.take((long long)ly.wd_rows * ly.wd_n16, &ms);
+            }
+            ly.R = rows_per_chunk(ly.H, ly.W);
+            ly.Rw = ly.R;
+            const long long Kw = (long long)taps * ly.cin;
+            const int mgroups = (int)((Kw + 255) / 256);
+            const int gt = std::max(1, (target + mgroups * p.n - 1) / (mgroups * p.n));
+            const int G0 = std::min(B, gt);
+            ly.spg = (B + G0 - 1) / G0;
+            ly.G = (B + ly.spg - 1) / ly.spg;
+            part_max = std::max(part_max, (long long)ly.G * Kw * ly.cout);
+        }
+    }
+    p.dz_off = ar.take(dz_max, &p.dz_ms);
+    p.dt_off = ar.take(std::max(dt_max, 1LL), &p.dt_ms);
+    p.part_off = ar.take(part_max, &p.part_ms);
+    const Layer& hd = ls.back();
+    // head scratch: g [B][C] | dl [B][K] | ce [2B] | dg [B][C]
+    p.head_off = ar.take((long long)B * hd.cin * 2 + (long long)B * hd.cout + 2LL * B, &p.head_ms);
+    p.lr_off = ar.used;   // per-member learning rates
+    ar.used += (p.n + 63) & ~63LL;
+    p.act_floats = ar.used;
+    return MPO_OK;
+}
+
+template <int KS, int NT>
+void launch_conv_t(const ConvArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+    auto kern = dn_conv_kernel<KS, NT>;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a);
+}
+
+template <int KS, int NT>
+void launch_wg_t(const WgArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+    auto kern = dn_wgrad_kernel<KS, NT>;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a);
+}
+
+template <int KS>
+int launch_conv(const ConvArgs& a, int n_members, int B, hipStream_t s) {
+    const int nt = (a.N + 15) / 16;
+    const dim3 grid((a.H + a.R - 1) / a.R, B, n_members);
+    const size_t lds = conv_lds(a.R, a.W, KS, a.Cin);
+    if (lds > ((size_t)160 << 10)) { mpo::set_error("dn_conv: LDS %zu B exceeds 160 KiB", lds); return MPO_ENOTSUP; }
+    switch (nt) {
+        case 1: launch_conv_t<KS, 1>(a, grid, lds, s); break;
+        case 2: launch_conv_t<KS, 2>(a, grid, lds, s); break;
+        case 3: launch_conv_t<KS, 3>(a, grid, lds, s); break;
+        case 4: launch_conv_t<KS, 4>(a, grid, lds, s); break;
+        case 5: launch_conv_t<KS, 5>(a, grid, lds, s); break;
+        case 6: launch_conv_t<KS, 6>(a, grid, lds, s); break;
+        default: mpo::set_error("dn_conv: %d output channels unsupported (max 96)", a.N); return MPO_ENOTSUP;
+    }
+    return MPO_OK;
+}
+
+template <int KS>
+int launch_wgrad(const WgArgs& a, int n_members, int G, hipStream_t s) {
+    const int nt = (a.N + 15) / 16;
+    const int Kw = KS * KS * a.Cin;
+    const dim3 grid((Kw + 255) / 256, G, n_members);
+    const size_t lds = wg_lds(a.R, a.W, KS, a.Cin, nt);
+    if (lds > ((size_t)160 << 10)) { mpo::set_error("dn_wgrad: LDS %zu B exceeds 160 KiB", lds); return MPO_ENOTSUP; }
+    switch (nt) {
+        case 1: launch_wg_t<KS, 1>(a, grid, lds, s); break;
+        case 2: launch_wg_t<KS, 2>(a, grid, lds, s); break;
+        case 3: launch_wg_t<KS, 3>(a, grid, lds, s); break;
+        case 4: launch_wg_t<KS, 4>(a, grid, lds, s); break;
+        case 5: launch_wg_t<KS, 5>(a, grid, lds, s); break;
+        case 6: launch_wg_t<KS, 6>(a, grid, lds, s); break;
+        default: mpo::set_error("dn_wgrad: %d output channels unsupported (max 96)", a.N); return MPO_ENOTSUP;
+    }
+    return MPO_OK;
+}
+
+inline dim3 flat_grid(long long total, int n_members) {
+    long long bx = (total + 255) / 256;
+    bx = std::max(1LL, std::min(bx, 1024LL));
+    return dim3((unsigned)bx, n_members);
+}
+
+#define DN_TRY(x)                     \
+    do {                              \
+        const int rc_ = (x);          \
+        if (rc_ != MPO_OK) return rc_; \
+    } while (0)
+
+int enqueue_prep(DnPlan& p, bool with_dgrad, hipStream_t s) {
+    for (auto& ly : p.layers) {
+        if (ly.kind == K_HEAD) continue;
+        const int taps = ly.ks * ly.ks;
+        const long long wms = (long long)ly.wf_rows * ly.wf_n16;
+        hipLaunchKernelGGL(dn_prep_kernel, flat_grid(wms, p.n), dim3(256), 0, s, p.params, p.n_params, ly.w_off,
+                           p.act + ly.wf_off, ((wms + 63) & ~63LL), taps, ly.cin, ly.cout, ly.wf_rows, ly.wf_n16, 0);
+        if (with_dgrad && ly.kind != K_CONV0) {
+            const long long dms = (long long)ly.wd_rows * ly.wd_n16;
+            hipLaunchKernelGGL(dn_prep_kernel, flat_grid(dms, p.n), dim3(256), 0, s, p.params, p.n_params, ly.w_off,
+                               p.act + ly.wd_off_act, ((dms + 63) & ~63LL), taps, ly.cin, ly.cout, ly.wd_rows,
+                               ly.wd_n16, 1);
+        }
+    }
+    MPO_LAUNCH_CHECK();
+    return MPO_OK;
+}
+
+BnArgs bn_args(DnPlan& p, const Layer& ly, bool train) {
+    BnArgs a{};
+    const int s = ly.stage;
+    a.x = p.act + p.cat_off[s]; a.x_ms = p.cat_ms[s]; a.x_ps = p.sC[s];
+    a.z = p.act + ly.z_off; a.z_ms = ((long long)p.B * ly.H * ly.W * ly.cin + 63) & ~63LL;
+    a.coef = p.act + ly.coef_off; a.coef_ms = (4LL * ly.H + 63) & ~63LL;
+    a.params = p.params; a.p_ms = p.n_params; a.g_off = ly.g_off; a.b_off = ly.b_off;
+    a.state = p.state; a.s_ms = p.n_state; a.mm_off = ly.mm_off; a.mv_off = ly.mv_off;
+    a.grads = p.grads;
+    a.B = p.B; a.H = ly.H; a.W = ly.W; a.Cin = ly.cin; a.train = train ? 1 : 0;
+    return a;
+}
+
+HeadArgs head_args(DnPlan& p, const int* labels, const int* order, long long ord_ms, long long row0, bool train) {
+    const Layer& hd = p.layers.back();
+    HeadArgs h{};
+    h.z = p.act + hd.z_off; h.z_ms = ((long long)p.B * hd.H * hd.W * hd.cin + 63) & ~63LL;
+    h.params = p.params; h.p_ms = p.n_params; h.wd_off = p.wd_off; h.bd_off = p.bd_off;
+    h.grads = p.grads;
+    float* base = p.act + p.head_off;
+    const long long BC = (long long)p.B * hd.cin, BK = (long long)p.B * hd.cout;
+    h.g = base; h.dl = base + BC; h.ce = base + BC + BK; h.dg = base + BC + BK + 2LL * p.B; h.h_ms = p.head_ms;
+    h.labels = labels; h.order = order; h.ord_ms = ord_ms; h.row0 = row0;
+    h.B = p.B; h.HW = hd.H * hd.W; h.C = hd.cin; h.classes = hd.cout; h.train = train ? 1 : 0;
+    return h;
+}
+
+int enqueue_forward(DnPlan& p, const float* x, const int* labels, const int* order, long long ord_ms, long long row0,
+                    bool train, float* loss_out, float* loss_sum, int* correct, hipStream_t s) {
+    const int B = p.B, n = p.n;
+    for (auto& ly : p.layers) {
+        const int st = ly.stage;
+        if (ly.kind == K_CONV0) {
+            ConvArgs c{};
+            c.in = x; c.in_ps = ly.cin; c.order = order; c.ord_ms = ord_ms; c.row0 = row0;
+            c.img_floats = (long long)ly.H * ly.W * ly.cin;
+            c.w = p.act + ly.wf_off; c.w_ms = ((long long)ly.wf_rows * ly.wf_n16 + 63) & ~63LL;
+            c.out = p.act + p.cat_off[0]; c.out_ms = p.cat_ms[0]; c.out_ps = p.sC[0];
+            c.H = ly.H; c.W = ly.W; c.Cin = ly.cin; c.N = ly.cout; c.R = ly.R;
+            DN_TRY(launch_conv<3>(c, n, B, s));
+            continue;
+        }
+        BnArgs bn = bn_args(p, ly, train);
+        hipLaunchKernelGGL(dn_bn_fwd_kernel, dim3(ly.H, n), dim3(256), 0, s, bn);
+        if (ly.kind == K_HEAD) {
+            HeadArgs h = head_args(p, labels, order, ord_ms, row0, train);
+            h.loss_out = loss_out; h.loss_sum = loss_sum; h.correct = correct;
+            const size_t lds = (size_t)(h.C + h.classes) * sizeof(float);
+            hipLaunchKernelGGL(dn_head_fwd_kernel, dim3(B, n), dim3(256), lds, s, h);
+            hipLaunchKernelGGL(dn_head_reduce_kernel, dim3(n), dim3(256), 0, s, h, p.n_params);
+            continue;
+        }
+        ConvArgs c{};
+        c.in = bn.z; c.in_ms = bn.z_ms; c.in_ps = ly.cin;
+        c.w = p.act + ly.wf_off; c.w_ms = ((long long)ly.wf_rows * ly.wf_n16 + 63) & ~63LL;
+        c.H = ly.H; c.W = ly.W; c.Cin = ly.cin; c.N = ly.cout; c.R = ly.R;
+        if (ly.kind == K_DENSE) {
+            c.out = p.act + p.cat_off[st] + ly.coff; c.out_ms = p.cat_ms[st]; c.out_ps = p.sC[st];
+            DN_TRY(launch_conv<3>(c, n, B, s));
+        } else {
+            const long long tms = ((long long)B * ly.H * ly.W * ly.cout + 63) & ~63LL;
+            c.out = p.act + ly.t_off; c.out_ms = tms; c.out_ps = ly.cout;
+            DN_TRY(launch_conv<1>(c, n, B, s));
+            const long long tot = (long long)B * (ly.H / 2) * (ly.W / 2) * ly.cout;
+            hipLaunchKernelGGL(dn_pool_fwd_kernel, flat_grid(tot, n), dim3(256), 0, s, p.act + ly.t_off, tms,
+                               p.act + p.cat_off[st + 1], p.cat_ms[st + 1], p.sC[st + 1], B, ly.H, ly.W, ly.cout);
+        }
+    }
+    MPO_LAUNCH_CHECK();
+    return MPO_OK;
+}
+
+int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_ms, long long row0, hipStream_t s) {
+    const int B = p.B, n = p.n;
+    for (int i = (int)p.layers.size() - 1; i >= 0; --i) {
+        Layer& ly = p.layers[i];
+        const int st = ly.stage;
+        if (ly.kind == K_HEAD) {
+            BnArgs bn = bn_args(p, ly, true);
+            HeadArgs h = head_args(p, nullptr, nullptr, 0, 0, true);
+            bn.bcast = 1; bn.dg = h.dg; bn.dg_ms = h.h_ms; bn.inv_hw = 1.f / (ly.H * ly.W);
+            bn.dx = p.act + p.dcat_off[st]; bn.dx_ms = p.cat_ms[st]; bn.dx_ps = p.sC[st]; bn.accumulate = 0;
+            hipLaunchKernelGGL(dn_bn_bwd_kernel, dim3(ly.H, n), dim3(256), 0, s, bn);
+            continue;
+        }
+        // dOut of this layer's conv and the input it saw
+        WgArgs w{};
+        w.H = ly.H; w.W = ly.W; w.Cin = ly.cin; w.N = ly.cout; w.R = ly.Rw; w.spg = ly.spg; w.B = B;
+        w.part = p.act + p.part_off; w.part_ms = p.part_ms;
+        const float* dout;
+        long long dout_ms;
+        int dout_ps;
+        if (ly.kind == K_TRANS) {
+            const long long tot = (long long)B * ly.H * ly.W * ly.cout;
+            hipLaunchKernelGGL(dn_pool_bwd_kernel, flat_grid(tot, n), dim3(256), 0, s, p.act + p.dcat_off[st + 1],
+                               p.cat_ms[st + 1], p.sC[st + 1], p.act + p.dt_off, p.dt_ms, B, ly.H, ly.W, ly.cout);
+            dout = p.act + p.dt_off; dout_ms = p.dt_ms; dout_ps = ly.cout;
+        } else {
+            dout = p.act + p.dcat_off[st] + ly.coff; dout_ms = p.cat_ms[st]; dout_ps = p.sC[st];
+        }
+        w.dout = dout; w.dout_ms = dout_ms; w.dout_ps = dout_ps;
+        if (ly.kind == K_CONV0) {
+            w.in = x; w.in_ps = ly.cin; w.order = order; w.ord_ms = ord_ms; w.row0 = row0;
+            w.img_floats = (long long)ly.H * ly.W * ly.cin;
+        } else {
+            w.in = p.act + ly.z_off; w.in_ms = ((long long)B * ly.H * ly.W * ly.cin + 63) & ~63LL; w.in_ps = ly.cin;
+        }
+        if (ly.ks == 3) DN_TRY(launch_wgrad<3>(w, n, ly.G, s));
+        else DN_TRY(launch_wgrad<1>(w, n, ly.G, s));
+        const long long cnt = (long long)ly.ks * ly.ks * ly.cin * ly.cout;
+        hipLaunchKernelGGL(dn_wgrad_reduce_kernel, flat_grid(cnt, n), dim3(256), 0, s, (const float*)(p.act + p.part_off),
+                           p.part_ms, ly.G, cnt, p.grads, p.n_params, ly.w_off);
+        if (ly.kind == K_CONV0) continue;
+        // input gradient: 'same' conv of dOut with the rotated, transposed kernel -> dz
+        ConvArgs c{};
+        c.in = dout; c.in_ms = dout_ms; c.in_ps = dout_ps;
+        c.w = p.act + ly.wd_off_act; c.w_ms = ((long long)ly.wd_rows * ly.wd_n16 + 63) & ~63LL;
+        c.out = p.act + p.dz_off; c.out_ms = p.dz_ms; c.out_ps = ly.cin;
+        c.H = ly.H; c.W = ly.W; c.Cin = ly.cout; c.N = ly.cin; c.R = ly.R;
+        if (ly.ks == 3) DN_TRY(launch_conv<3>(c, n, B, s));
+        else DN_TRY(launch_conv<1>(c, n, B, s));
+        BnArgs bn = bn_args(p, ly, true);
+        bn.dz = p.act + p.dz_off; bn.dz_ms = p.dz_ms;
+        bn.dx = p.act + p.dcat_off[st]; bn.dx_ms = p.cat_ms[st]; bn.dx_ps = p.sC[st];
+        bn.accumulate = ly.kind == K_DENSE ? 1 : 0;
+        hipLaunchKernelGGL(dn_bn_bwd_kernel, dim3(ly.H, n), dim3(256), 0, s, bn);
+    }
+    MPO_LAUNCH_CHECK();
+    return MPO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mpo_dn_create(const MpoDnArch* arch, int n_members, int batch, void** handle) {
+    MPO_GUARD_BEGIN
+    MPO_CHECK_ARG(arch && handle, "mpo_dn_create: null pointer");
+    MPO_CHECK_ARG(n_members > 0 && n_members <= 65535 && batch > 0 && batch <= 65535,
+                  "mpo_dn_create: n_members %d / batch %d out of range", n_members, batch);
+    MPO_CHECK_ARG(arch->depth >= 4 && (arch->depth - 4) % 3 == 0, "mpo_dn_create: Depth must be 3 N + 4 (got %d)",
+                  arch->depth);
+    MPO_CHECK_ARG(arch->nb_dense_block >= 1 && arch->growth > 0 && arch->nb_filter > 0 && arch->classes > 1 &&
+                      arch->H > 0 && arch->W > 0 && arch->C > 0,
+                  "mpo_dn_create: bad architecture");
+    auto p = std::make_unique<DnPlan>();
+    p->arch = *arch;
+    p->n = n_members;
+    p->B = batch;
+    const int rc = build_plan(*p);
+    if (rc != MPO_OK) {
+        mpo::set_error("mpo_dn_create: architecture outside the kernels' range (W <= %d, C <= 1024)", kMaxPix);
+        return rc;
+    }
+    for (auto& ly : p->layers) {
+        if (ly.kind == K_HEAD) continue;
+        if (conv_lds(ly.R, ly.W, ly.ks, ly.cin) > ((size_t)160 << 10) ||
+            conv_lds(ly.R, ly.W, ly.ks, ly.cout) > ((size_t)160 << 10) ||
+            wg_lds(ly.Rw, ly.W, ly.ks, ly.cin, (ly.cout + 15) / 16) > ((size_t)160 << 10) || ly.cout > 96 ||
+            (ly.kind != K_CONV0 && ly.cin > 96)) {
+            mpo::set_error("mpo_dn_create: layer (cin %d, cout %d, %dx%d) exceeds the kernels' LDS / channel range",
+                           ly.cin, ly.cout, ly.H, ly.W);
+            return MPO_ENOTSUP;
+        }
+    }
+    *handle = p.release();
+    return MPO_OK;
+    MPO_GUARD_END
+}
+
+int mpo_dn_destroy(void* handle) {
+    delete static_cast<DnPlan*>(handle);
+    return MPO_OK;
+}
+
+int mpo_dn_sizes(const void* handle, MpoDnSizes* out) {
+    MPO_CHECK_ARG(handle && out, "mpo_dn_sizes: null pointer");
+    const DnPlan& p = *static_cast<const DnPlan*>(handle);
+    out->n_params = p.n_params;
+    out->n_state = p.n_state;
+    out->act_floats = p.act_floats;
+    out->n_members = p.n;
+    out->batch = p.B;
+    out->n_layers = (int32_t)p.layers.size();
+    return MPO_OK;
+}
+
+int mpo_dn_layer(const void* handle, int i, int32_t* geom, int64_t* offs) {
+    MPO_CHECK_ARG(handle && geom && offs, "mpo_dn_layer: null pointer");
+    const DnPlan& p = *static_cast<const DnPlan*>(handle);
+    MPO_CHECK_ARG(i >= 0 && i < (int)p.layers.size(), "mpo_dn_layer: layer %d out of range", i);
+    const Layer& ly = p.layers[i];
+    const int32_t g[8] = {ly.kind, ly.stage, ly.H, ly.W, ly.cin, ly.cout, ly.ks, ly.coff};
+    for (int k = 0; k < 8; ++k) geom[k] = g[k];
+    const bool head = ly.kind == K_HEAD;
+    const int64_t o[6] = {head ? p.wd_off : ly.w_off, ly.g_off, ly.b_off, ly.mm_off, ly.mv_off, head ? p.bd_off : -1};
+    for (int k = 0; k < 6; ++k) offs[k] = o[k];
+    return MPO_OK;
+}
+
+int mpo_dn_bind(void* handle, float* params, float* grads, float* adam_m, float* adam_v, float* state, float* act,
+                const float* lr, void* stream) {
+    MPO_GUARD_BEGIN
+    MPO_CHECK_ARG(handle && params && grads && adam_m && adam_v && state && act && lr, "mpo_dn_bind: null pointer");
+    DnPlan& p = *static_cast<DnPlan*>(handle);
+    p.params = params; p.grads = grads; p.m = adam_m; p.v = adam_v; p.state = state; p.act = act;
+    MPO_HIP(hipMemcpyAsync(act + p.lr_off, lr, sizeof(float) * p.n, hipMemcpyHostToDevice,
+                           static_cast<hipStream_t>(stream)));
+    MPO_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    p.bound = true;
+    return MPO_OK;
+    MPO_GUARD_END
+}
+
+int mpo_dn_train_step(void* handle, const float* x, const int32_t* labels, const int32_t* order, int64_t order_stride,
+                      int64_t row0, int32_t step, float* loss_out, void* stream) {
+    MPO_GUARD_BEGIN
+    MPO_CHECK_ARG(handle && x && labels && order && loss_out, "mpo_dn_train_step: null pointer");
+    DnPlan& p = *static_cast<DnPlan*>(handle);
+    MPO_CHECK_ARG(p.bound, "mpo_dn_train_step: plan not bound");
+    MPO_CHECK_ARG(step >= 0 && row0 >= 0 && row0 + p.B <= order_stride, "mpo_dn_train_step: batch outside the order table");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    DN_TRY(enqueue_prep(p, true, s));
+    DN_TRY(enqueue_forward(p, x, labels, order, order_stride, row0, true, loss_out, nullptr, nullptr, s));
+    DN_TRY(enqueue_backward(p, x, order, order_stride, row0, s));
+    hipLaunchKernelGGL(dn_adam_kernel, flat_grid(p.n_params, p.n), dim3(256), 0, s, p.params, p.grads, p.m, p.v,
+                       p.n_params, p.n_params, (const float*)(p.act + p.lr_off), (int)step + 1);
+    MPO_LAUNCH_CHECK();
+    return MPO_OK;
+    MPO_GUARD_END
+}
+
+int mpo_dn_eval_step(void* handle, const float* x, const int32_t* labels, const int32_t* order, int64_t order_stride,
+                     int64_t row0, float* loss_sum, int32_t* correct, void* stream) {
+    MPO_GUARD_BEGIN
+    MPO_CHECK_ARG(handle && x && labels && order && loss_sum && correct, "mpo_dn_eval_step: null pointer");
+    DnPlan& p = *static_cast<DnPlan*>(handle);
+    MPO_CHECK_ARG(p.bound, "mpo_dn_eval_step: plan not bound");
+    MPO_CHECK_ARG(row0 >= 0 && row0 + p.B <= order_stride, "mpo_dn_eval_step: batch outside the order table");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    DN_TRY(enqueue_prep(p, false, s));
+    DN_TRY(enqueue_forward(p, x, labels, order, order_stride, row0, false, nullptr, loss_sum, correct, s));
+    return MPO_OK;
+    MPO_GUARD_END
+}
+
+int mpo_dn_penalty(void* handle, float* out, void* stream) {
+    MPO_GUARD_BEGIN
+    MPO_CHECK_ARG(handle && out, "mpo_dn_penalty: null pointer");
+    DnPlan& p = *static_cast<DnPlan*>(handle);
+    MPO_CHECK_ARG(p.bound, "mpo_dn_penalty: plan not bound");
+    hipLaunchKernelGGL(dn_penalty_kernel, dim3(p.n), dim3(256), 0, static_cast<hipStream_t>(stream), p.params,
+                       p.n_params, p.n_params, out);
+    MPO_LAUNCH_CHECK();
+    return MPO_OK;
+    MPO_GUARD_END
+}
+
+}  // extern "C"

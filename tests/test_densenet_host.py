@@ -1,0 +1,86 @@
+"""Host-side DenseNet plan (no GPU): layer geometry and parameter layout from
+the C ABI agree with the oracle's reading of densenet.py:135-196."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import densenet as od
+
+
+def _plan(arch, n=4, batch=16):
+    from mpi_opt_amd import _lib
+
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    rc = L.mpo_dn_create(ctypes.byref(arch.c_struct()), n, batch, ctypes.byref(h))
+    return L, rc, h
+
+
+@pytest.mark.parametrize("img,depth,blocks,growth,nbf", [((32, 32, 3), 10, 3, 12, 16), ((9, 11, 2), 7, 2, 5, 7),
+                                                        ((150, 94, 5), 10, 3, 12, 16)])
+def test_plan_geometry_matches_oracle(img, depth, blocks, growth, nbf):
+    from mpi_opt_amd import _lib
+    from mpi_opt_amd.densenet import KIND_NAMES, DenseNetArch, param_shapes
+
+    arch = DenseNetArch(img_dim=img, nb_classes=3, depth=depth, nb_dense_block=blocks, growth_rate=growth,
+                        nb_filter=nbf)
+    L, rc, h = _plan(arch)
+    assert rc == 0, L.mpo_last_error()
+    try:
+        sz = _lib.MpoDnSizes()
+        assert L.mpo_dn_sizes(h, ctypes.byref(sz)) == 0
+        ref = od.arch_layers(img_dim=img, nb_classes=3, depth=depth, nb_dense_block=blocks, growth_rate=growth,
+                             nb_filter=nbf)
+        assert sz.n_layers == len(ref)
+        geom = (ctypes.c_int32 * 8)()
+        offs = (ctypes.c_int64 * 6)()
+        layers = []
+        spans = []
+        for i, r in enumerate(ref):
+            assert L.mpo_dn_layer(h, i, geom, offs) == 0
+            g = list(geom)
+            ly = dict(kind=KIND_NAMES[g[0]], stage=g[1], H=g[2], W=g[3], cin=g[4], cout=g[5], ks=g[6], coff=g[7])
+            layers.append(ly)
+            for k in ("kind", "H", "W", "cin", "cout"):
+                assert ly[k] == r[k], (i, k)
+            if r["kind"] in ("dense", "trans"):
+                assert ly["ks"] == r["ks"] and ly["coff"] == r["coff"]
+            o = list(offs)
+            if ly["kind"] == "conv0":
+                spans.append((o[0], 9 * ly["cin"] * ly["cout"]))
+            else:
+                spans += [(o[1], ly["H"]), (o[2], ly["H"])]
+                if ly["kind"] == "head":
+                    spans += [(o[0], ly["cin"] * ly["cout"]), (o[5], ly["cout"])]
+                else:
+                    spans.append((o[0], ly["ks"] ** 2 * ly["cin"] * ly["cout"]))
+        # parameter tensors are disjoint and inside the per-member block
+        spans.sort()
+        for (a0, n0), (a1, _) in zip(spans, spans[1:]):
+            assert a0 + n0 <= a1
+        assert spans[-1][0] + spans[-1][1] <= sz.n_params
+        P, _ = param_shapes(layers)
+        Po, _ = od.param_shapes(ref)
+        assert P == Po
+        assert sz.act_floats > 0
+    finally:
+        L.mpo_dn_destroy(h)
+
+
+def test_plan_rejects_bad_depth_and_wide_images():
+    from mpi_opt_amd.densenet import DenseNetArch
+
+    L, rc, h = _plan(DenseNetArch(depth=11))
+    assert rc == 1 and b"3 N + 4" in L.mpo_last_error()
+    L, rc, h = _plan(DenseNetArch(img_dim=(8, 300, 3)))
+    assert rc == 3
+
+
+def test_flops_reference_config():
+    from mpi_opt_amd.densenet import flops_per_sample_fwd, flops_per_sample_train
+
+    layers = od.arch_layers()
+    assert flops_per_sample_fwd(layers) == od.flops_per_sample_fwd(layers)
+    assert flops_per_sample_train(layers) == od.flops_per_sample_train(layers)
+    assert np.isclose(flops_per_sample_fwd(layers) / 1e6, 22.8, atol=0.5)
