@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py -- measures BASELINE.json's metric on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload ei|train|all]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload ei|train|densenet|all]
 
 N=1 workload = BASELINE configs[1]: the GP/EI "ask" step, 200 observations,
 10-dim space, 1M candidates, fp64.  One *step* = one full acquisition pass of the
@@ -294,16 +294,125 @@ def bench_train(args, torch, dist, ws, rank, dev):
     }
 
 
+def cpu_baseline_densenet(budget_s=10.0, B=20):
+    """fp64 numpy restatement (oracle/densenet.py) of one DenseNet trial on the
+    host: one train step + one validation batch at batch B, scaled linearly to
+    batch 100 and extrapolated to a whole trial (10 epochs x (350 train + 150
+    validation batches))."""
+    from oracle import densenet as od
+
+    layers = od.arch_layers()
+    rng = np.random.RandomState(0)
+    x = rng.uniform(size=(B, 32, 32, 3))
+    y = rng.randint(0, 10, size=B)
+    t_start = time.perf_counter()
+    t_tr = t_ev = 0.0
+    n = 0
+    while True:
+        p, s = od.he_uniform_init(layers, n)
+        o = od.DenseNetOracle(layers, p, s)
+        t0 = time.perf_counter()
+        o.train_step(x, y)
+        t1 = time.perf_counter()
+        o.eval_batch(x, y)
+        t2 = time.perf_counter()
+        t_tr += t1 - t0
+        t_ev += t2 - t1
+        n += 1
+        if time.perf_counter() - t_start > budget_s:
+            break
+    scale = 100.0 / B
+    sec_per_trial = 10 * (350 * t_tr * scale + 150 * t_ev * scale) / n
+    cores = int(os.environ.get("OMP_NUM_THREADS", len(os.sched_getaffinity(0))))
+    return {"value": 3600.0 / sec_per_trial, "unit": "trials/hour", "cores": cores, "kind": "port",
+            "sample": f"{n} x (1 train step + 1 validation batch) at batch {B}, fp64 numpy restatement "
+                      f"(oracle/densenet.py, BLAS threads = {cores}), scaled to batch 100 and extrapolated to "
+                      f"3500 train steps + 1500 validation batches per trial ({time.perf_counter() - t_start:.1f} s)"}
+
+
+def bench_densenet(args, torch, dist, ws, rank, dev):
+    """BASELINE config 5: a population of DenseNets (densenet.py, base_model.py grid:
+    depth 10, 3 blocks, growth 12, nb_filter 16; lr = 10**U(-5, 1)) on synthetic
+    CIFAR-10-shape data; each trial trains 10 epochs on the option3 70/30 split of
+    50 000 samples (350 train + 150 validation batches of 100 per epoch)."""
+    from mpi_opt_amd.densenet import DenseNetArch, DenseNetPopulation, flops_per_sample_fwd, \
+        flops_per_sample_train, synthetic_cifar
+    from mpi_opt_amd.population import kfold_split
+
+    n_trials, B = args.dn_trials, 100
+    rng = np.random.RandomState(2024 + rank)
+    lrs = 10.0 ** rng.uniform(-5, 1, size=n_trials)
+    pop = DenseNetPopulation(DenseNetArch(), lrs, batch=B, device=dev, init_seed=rank * 1000)
+    x, yl = synthetic_cifar(50000, seed=rank, device=dev)
+    tr, va = kfold_split(50000, 1, 0)
+    otr = torch.from_numpy(np.stack([tr] * n_trials)).to(dev)
+    ova = torch.from_numpy(np.stack([va] * n_trials)).to(dev)
+    n_tr, n_va = len(tr) // B, len(va) // B        # 350, 150
+    state = {"st": 0, "vb": 0}
+
+    def macro_step():                               # 7 train + 3 validation batches = 1/50 epoch
+        for _ in range(7):
+            pop.train_step(x, yl, otr, (state["st"] % n_tr) * B)
+            state["st"] += 1
+        for _ in range(3):
+            pop.eval_step(x, yl, ova, (state["vb"] % n_va) * B)
+            state["vb"] += 1
+
+    for _ in range(args.train_warmup):
+        macro_step()
+    torch.cuda.synchronize(dev)
+    if ws > 1:
+        dist.barrier()
+    stream = torch.cuda.current_stream(dev)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.train_steps):
+        macro_step()
+    e1.record(stream)
+    if ws > 1:
+        g = torch.empty(ws * n_trials, dtype=torch.float32, device=dev)
+        dist.all_gather_into_tensor(g, pop.val_loss_sum)
+    torch.cuda.synchronize(dev)
+    if ws > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    t_gpu = e0.elapsed_time(e1) / 1e3
+    if ws > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    t_macro = dt / args.train_steps
+    trials_per_hour = ws * n_trials * 3600.0 / (t_macro * 50 * 10)
+    flops = n_trials * B * (7 * flops_per_sample_train(pop.layers) + 3 * flops_per_sample_fwd(pop.layers))
+    achieved = flops / (t_gpu / args.train_steps) / 1e12
+    return {
+        "metric": "DenseNet trials/hour (CIFAR-10 shape, 10 epochs, 70/30 split of 50k samples)",
+        "value": trials_per_hour, "unit": "trials/hour", "n_gpus": ws, "steps": args.train_steps,
+        "warmup": args.train_warmup, "ms_per_step": t_macro * 1e3, "scaling": "weak", "dtype": "f32",
+        "data": "synthetic CIFAR-10-shape x~U[0,1] (50000x32x32x3 f32), uniform labels; he_uniform init",
+        "config": {"workload": f"BASELINE configs[4]: {n_trials} DenseNet trials (depth 10, 3 blocks, growth 12, "
+                               f"nb_filter 16, lr 10**U(-5,1)) per GPU; step = 7 train + 3 validation batches "
+                               f"(1/50 epoch)", "trials_per_gpu": n_trials, "batch": B, "epochs": 10,
+                   "parallelism": f"trials sharded, {ws} GPU(s), all-gather of validation losses"},
+        "roofline": {"kernel": "population step (all DenseNet kernels)", "bound": "mfma",
+                     "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None, "algorithmic_flops_per_step": flops},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="all", choices=["ei", "train", "all"])
+    ap.add_argument("--workload", default="all", choices=["ei", "train", "densenet", "all"])
     ap.add_argument("--candidates", type=int, default=1_000_000)
     ap.add_argument("--train-trials", type=int, default=64)
     ap.add_argument("--train-steps", type=int, default=5)
     ap.add_argument("--train-warmup", type=int, default=1)
+    ap.add_argument("--dn-trials", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -322,17 +431,22 @@ def main():
 
     res = bench_ei(args, torch, dist, ws, rank, dev) if args.workload in ("ei", "all") else None
     train = bench_train(args, torch, dist, ws, rank, dev) if args.workload in ("train", "all") else None
+    dn = bench_densenet(args, torch, dist, ws, rank, dev) if args.workload in ("densenet", "all") else None
     if rank == 0:
         cpu = ws == 1 and not args.no_cpu_baseline
         if train is not None:
             trials = train.pop("_trials")
             train["cpu_baseline"] = cpu_baseline_train(trials) if cpu else None
-        if res is None:
-            res, train = train, None
-        else:
+        if dn is not None:
+            dn["cpu_baseline"] = cpu_baseline_densenet() if cpu else None
+        if res is not None:
             res["cpu_baseline"] = cpu_baseline_ei() if cpu else None
             if train is not None:
                 res["train"] = train
+            if dn is not None:
+                res["densenet"] = dn
+        else:
+            res = train if train is not None else dn
         print(json.dumps(res), flush=True)
     if ws > 1:
         dist.barrier()

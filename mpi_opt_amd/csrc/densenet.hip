@@ -25,9 +25,11 @@
 //                     (a 'same' conv of dOut with the rotated/transposed kernel).
 //   dn_wgrad<KS, NT>  M = KS^2 * cin weight rows, N = cout, K = pixels of a sample
 //                     group; partial slabs per group, reduced in fixed order.
-//   dn_bn_fwd / dn_bn_bwd  BatchNormalization(axis=1) of NHWC = per image ROW h:
-//                     one workgroup per (member, h) reduces (B, W, cin) in fp64, then
-//                     applies BN + ELU (fwd) or the BN/ELU backward (bwd).
+//   dn_bn_stats / dn_bn_apply, dn_bn_bwd_reduce / dn_bn_bwd_apply
+//                     BatchNormalization(axis=1) of NHWC = statistics per image ROW h:
+//                     fp64 partial sums per (member, h, batch slice), folded in fixed
+//                     order by the per-(sample, row) apply kernels (BN + ELU forward,
+//                     BN/ELU backward into dcat).
 //   dn_pool_fwd/bwd, dn_head_fwd/reduce (GAP + dense + softmax + categorical CE),
 //   dn_adam (Keras Adam + l2 1e-4 gradient), dn_prep (padded weight copies).
 #include "mpo_internal.h"
@@ -411,125 +413,176 @@ __global__ void dn_prep_kernel(const float* __restrict__ params, long long p_ms,
 
 // ============================================================================
 // BatchNormalization(mode=0, axis=1) of an NHWC tensor: statistics per image row h
-// over (batch, W, channels) -- densenet.py:24-27 -- then ELU.  One workgroup per
-// (h, member).  Element order: (w, c) pairs of the row, each over all samples b.
+// over (batch, W, channels) -- densenet.py:24-27 -- then ELU.
+//   dn_bn_stats  grid (h, batch slice, member): fp64 (sum, sum of squares) of the
+//                slice's (b, w, c) elements of row h -> part[member][slice][h][2];
+//   dn_bn_apply  grid (b*H + h, member): folds the S slice partials in fixed order
+//                (deterministic), z = ELU(x * gamma inv + (beta - mean gamma inv)).
+//                Training: block (b = 0) stores mean / inv and updates the moving
+//                averages; evaluation: the moving averages.
 // ============================================================================
-__global__ __launch_bounds__(256) void dn_bn_fwd_kernel(BnArgs a) {
+__global__ __launch_bounds__(256) void dn_bn_stats_kernel(BnArgs a, double* __restrict__ part, int S, int bs) {
     __shared__ double red[4];
-    __shared__ float sc[2];
-    const int h = blockIdx.x, m = blockIdx.y, tid = threadIdx.x;
-    const int H = a.H, W = a.W, Cin = a.Cin, B = a.B;
+    const int h = blockIdx.x, sl = blockIdx.y, m = blockIdx.z, tid = threadIdx.x;
+    const int H = a.H, W = a.W, Cin = a.Cin;
     const int rowe = W * Cin;
     const long long bstride = (long long)H * W * a.x_ps;
     const float* xm = a.x + m * a.x_ms + (long long)h * W * a.x_ps;
-    const float* pm = a.params + m * a.p_ms;
-    float* coef = a.coef + m * a.coef_ms;
-    float mean, var;
-    if (a.train) {
-        double s = 0.0;
-        for (int e = tid; e < rowe; e += 256) {
-            const int w = e / Cin, c = e - w * Cin;
-            const float* p = xm + (long long)w * a.x_ps + c;
-            for (int b = 0; b < B; ++b) s += p[b * bstride];
+    const int b0 = sl * bs, b1 = min(a.B, b0 + bs);
+    double s = 0.0, q = 0.0;
+    for (int e = tid; e < rowe; e += 256) {
+        const int w = e / Cin, c = e - w * Cin;
+        const float* p = xm + (long long)w * a.x_ps + c;
+        for (int b = b0; b < b1; ++b) {
+            const double v = p[b * bstride];
+            s += v;
+            q += v * v;
         }
-        const double n = (double)B * rowe;
-        const double mu = block_sum(s, red) / n;
-        double q = 0.0;
-        for (int e = tid; e < rowe; e += 256) {
-            const int w = e / Cin, c = e - w * Cin;
-            const float* p = xm + (long long)w * a.x_ps + c;
-            for (int b = 0; b < B; ++b) {
-                const double d = p[b * bstride] - mu;
-                q += d * d;
-            }
-        }
-        const double vr = block_sum(q, red) / n;
-        mean = (float)mu;
-        var = (float)vr;
-        if (tid == 0) {
-            float* st = a.state + m * a.s_ms;
-            st[a.mm_off + h] = kBnMomentum * st[a.mm_off + h] + (1.f - kBnMomentum) * mean;
-            st[a.mv_off + h] = kBnMomentum * st[a.mv_off + h] + (1.f - kBnMomentum) * var;
-        }
-    } else {
-        const float* st = a.state + m * a.s_ms;
-        mean = st[a.mm_off + h];
-        var = st[a.mv_off + h];
     }
-    const float inv = (float)(1.0 / sqrt((double)var + (double)kBnEps));
-    const float gam = pm[a.g_off + h], bet = pm[a.b_off + h];
+    s = block_sum(s, red);
+    q = block_sum(q, red);
     if (tid == 0) {
-        coef[h] = mean;
-        coef[H + h] = inv;
+        double* o = part + (((long long)m * S + sl) * H + h) * 2;
+        o[0] = s;
+        o[1] = q;
+    }
+}
+
+__global__ __launch_bounds__(256) void dn_bn_apply_kernel(BnArgs a, const double* __restrict__ part, int S) {
+    __shared__ float sc[2];
+    const int row = blockIdx.x, m = blockIdx.y, tid = threadIdx.x;
+    const int H = a.H, W = a.W, Cin = a.Cin;
+    const int b = row / H, h = row - b * H;
+    const int rowe = W * Cin;
+    if (tid == 0) {
+        float mean, var;
+        if (a.train) {
+            double s = 0.0, q = 0.0;
+            for (int sl = 0; sl < S; ++sl) {
+                const double* o = part + (((long long)m * S + sl) * H + h) * 2;
+                s += o[0];
+                q += o[1];
+            }
+            const double n = (double)a.B * rowe;
+            const double mu = s / n;
+            mean = (float)mu;
+            var = (float)fmax(q / n - mu * mu, 0.0);
+            if (b == 0) {
+                float* st = a.state + m * a.s_ms;
+                st[a.mm_off + h] = kBnMomentum * st[a.mm_off + h] + (1.f - kBnMomentum) * mean;
+                st[a.mv_off + h] = kBnMomentum * st[a.mv_off + h] + (1.f - kBnMomentum) * var;
+            }
+        } else {
+            const float* st = a.state + m * a.s_ms;
+            mean = st[a.mm_off + h];
+            var = st[a.mv_off + h];
+        }
+        const float inv = (float)(1.0 / sqrt((double)var + (double)kBnEps));
+        const float* pm = a.params + m * a.p_ms;
+        const float gam = pm[a.g_off + h], bet = pm[a.b_off + h];
+        if (b == 0) {
+            float* coef = a.coef + m * a.coef_ms;
+            coef[h] = mean;
+            coef[H + h] = inv;
+        }
         sc[0] = gam * inv;
         sc[1] = bet - mean * gam * inv;
     }
     __syncthreads();
     const float s = sc[0], t = sc[1];
-    float* zm = a.z + m * a.z_ms + (long long)h * rowe;
-    const long long zb = (long long)H * rowe;
+    const float* xr = a.x + m * a.x_ms + ((long long)b * H + h) * W * a.x_ps;
+    float* zr = a.z + m * a.z_ms + ((long long)b * H + h) * rowe;
     for (int e = tid; e < rowe; e += 256) {
         const int w = e / Cin, c = e - w * Cin;
-        const float* p = xm + (long long)w * a.x_ps + c;
-        for (int b = 0; b < B; ++b) {
-            const float y = p[b * bstride] * s + t;
-            zm[b * zb + e] = y > 0.f ? y : expm1f(y);
-        }
+        const float y = xr[(long long)w * a.x_ps + c] * s + t;
+        zr[e] = y > 0.f ? y : expm1f(y);
     }
 }
 
-// BN + ELU backward for one (h, member): dy = dz * ELU'(z); dgamma = sum dy xhat,
-// dbeta = sum dy; dx = gamma inv / n (n dy - dbeta - xhat dgamma) into dcat (store or add).
-__global__ __launch_bounds__(256) void dn_bn_bwd_kernel(BnArgs a) {
+// BN + ELU backward.  dy = dz * ELU'(z) (ELU' = 1 for z > 0, else z + 1);
+// dbeta[h] = sum dy, dgamma[h] = sum dy xhat (dn_bn_bwd_reduce, slice partials);
+// dx = gamma inv / n (n dy - dbeta - xhat dgamma) stored or added into dcat
+// (dn_bn_bwd_apply, one block per (b, h) row).
+__device__ __forceinline__ float bn_dy(const BnArgs& a, const float* zr, const float* dzr, const float* dgr, int e,
+                                       int c) {
+    const float zz = zr[e];
+    const float d = a.bcast ? dgr[c] * a.inv_hw : dzr[e];
+    return d * (zz > 0.f ? 1.f : zz + 1.f);
+}
+
+__global__ __launch_bounds__(256) void dn_bn_bwd_reduce_kernel(BnArgs a, double* __restrict__ part, int S, int bs) {
     __shared__ double red[4];
-    const int h = blockIdx.x, m = blockIdx.y, tid = threadIdx.x;
-    const int H = a.H, W = a.W, Cin = a.Cin, B = a.B;
+    const int h = blockIdx.x, sl = blockIdx.y, m = blockIdx.z, tid = threadIdx.x;
+    const int H = a.H, W = a.W, Cin = a.Cin;
     const int rowe = W * Cin;
-    const long long xb = (long long)H * W * a.x_ps, zb = (long long)H * rowe;
-    const float* xm = a.x + m * a.x_ms + (long long)h * W * a.x_ps;
-    const float* zm = a.z + m * a.z_ms + (long long)h * rowe;
-    const float* dzm = a.bcast ? nullptr : a.dz + m * a.dz_ms + (long long)h * rowe;
-    const float* dgm = a.bcast ? a.dg + m * a.dg_ms : nullptr;
     const float* coef = a.coef + m * a.coef_ms;
     const float mean = coef[h], inv = coef[H + h];
-    const float gam = a.params[m * a.p_ms + a.g_off + h];
-    auto dy_at = [&](int b, int e, int c) {
-        const float zz = zm[b * zb + e];
-        const float d = a.bcast ? dgm[b * Cin + c] * a.inv_hw : dzm[b * zb + e];
-        return d * (zz > 0.f ? 1.f : zz + 1.f);
-    };
+    const int b0 = sl * bs, b1 = min(a.B, b0 + bs);
     double sdy = 0.0, sdyx = 0.0;
-    for (int e = tid; e < rowe; e += 256) {
-        const int w = e / Cin, c = e - w * Cin;
-        const float* p = xm + (long long)w * a.x_ps + c;
-        for (int b = 0; b < B; ++b) {
-            const float dy = dy_at(b, e, c);
-            const float xh = (p[b * xb] - mean) * inv;
+    for (int b = b0; b < b1; ++b) {
+        const float* xr = a.x + m * a.x_ms + ((long long)b * H + h) * W * a.x_ps;
+        const long long zo = ((long long)b * H + h) * rowe;
+        const float* zr = a.z + m * a.z_ms + zo;
+        const float* dzr = a.bcast ? nullptr : a.dz + m * a.dz_ms + zo;
+        const float* dgr = a.bcast ? a.dg + m * a.dg_ms + (long long)b * Cin : nullptr;
+        for (int e = tid; e < rowe; e += 256) {
+            const int w = e / Cin, c = e - w * Cin;
+            const float dy = bn_dy(a, zr, dzr, dgr, e, c);
+            const float xh = (xr[(long long)w * a.x_ps + c] - mean) * inv;
             sdy += dy;
             sdyx += (double)dy * xh;
         }
     }
-    const double dbeta = block_sum(sdy, red);
-    const double dgamma = block_sum(sdyx, red);
+    sdy = block_sum(sdy, red);
+    sdyx = block_sum(sdyx, red);
     if (tid == 0) {
-        float* gm = a.grads + m * a.p_ms;
-        gm[a.g_off + h] = (float)dgamma;
-        gm[a.b_off + h] = (float)dbeta;
+        double* o = part + (((long long)m * S + sl) * H + h) * 2;
+        o[0] = sdy;
+        o[1] = sdyx;
     }
-    const float n = (float)B * rowe;
-    const float ca = gam * inv / n, fb = (float)dbeta, fg = (float)dgamma;
-    float* dxm = a.dx + m * a.dx_ms + (long long)h * W * a.dx_ps;
-    const long long db = (long long)H * W * a.dx_ps;
+}
+
+__global__ __launch_bounds__(256) void dn_bn_bwd_apply_kernel(BnArgs a, const double* __restrict__ part, int S) {
+    __shared__ float sc[3];
+    const int row = blockIdx.x, m = blockIdx.y, tid = threadIdx.x;
+    const int H = a.H, W = a.W, Cin = a.Cin;
+    const int b = row / H, h = row - b * H;
+    const int rowe = W * Cin;
+    const float* coef = a.coef + m * a.coef_ms;
+    const float mean = coef[h], inv = coef[H + h];
+    if (tid == 0) {
+        double sdy = 0.0, sdyx = 0.0;
+        for (int sl = 0; sl < S; ++sl) {
+            const double* o = part + (((long long)m * S + sl) * H + h) * 2;
+            sdy += o[0];
+            sdyx += o[1];
+        }
+        if (b == 0) {
+            float* gm = a.grads + m * a.p_ms;
+            gm[a.g_off + h] = (float)sdyx;
+            gm[a.b_off + h] = (float)sdy;
+        }
+        const float gam = a.params[m * a.p_ms + a.g_off + h];
+        sc[0] = gam * inv / ((float)a.B * rowe);
+        sc[1] = (float)sdy;
+        sc[2] = (float)sdyx;
+    }
+    __syncthreads();
+    const float ca = sc[0], fb = sc[1], fg = sc[2];
+    const float n = (float)a.B * rowe;
+    const float* xr = a.x + m * a.x_ms + ((long long)b * H + h) * W * a.x_ps;
+    const long long zo = ((long long)b * H + h) * rowe;
+    const float* zr = a.z + m * a.z_ms + zo;
+    const float* dzr = a.bcast ? nullptr : a.dz + m * a.dz_ms + zo;
+    const float* dgr = a.bcast ? a.dg + m * a.dg_ms + (long long)b * Cin : nullptr;
+    float* dxr = a.dx + m * a.dx_ms + ((long long)b * H + h) * W * a.dx_ps;
     for (int e = tid; e < rowe; e += 256) {
         const int w = e / Cin, c = e - w * Cin;
-        const float* p = xm + (long long)w * a.x_ps + c;
-        float* q = dxm + (long long)w * a.dx_ps + c;
-        for (int b = 0; b < B; ++b) {
-            const float dy = dy_at(b, e, c);
-            const float xh = (p[b * xb] - mean) * inv;
-            const float v = ca * (n * dy - fb - xh * fg);
-            if (a.accumulate) q[b * db] += v; else q[b * db] = v;
-        }
+        const float dy = bn_dy(a, zr, dzr, dgr, e, c);
+        const float xh = (xr[(long long)w * a.x_ps + c] - mean) * inv;
+        const float v = ca * (n * dy - fb - xh * fg);
+        float* q = dxr + (long long)w * a.dx_ps + c;
+        if (a.accumulate) *q += v; else *q = v;
     }
 }
 
@@ -734,6 +787,8 @@ struct DnPlan {
     long long z_ms_max = 0;
     long long dz_off = 0, dz_ms = 0, dt_off = 0, dt_ms = 0, part_off = 0, part_ms = 0;
     long long head_off = 0, head_ms = 0, lr_off = 0;
+    long long bnp_off = 0;      // fp64 BN slice partials [n][S][H][2] (shared by all sites)
+    std::vector<int> bn_S, bn_bs;   // per layer: batch slices and samples per slice
     float *params = nullptr, *grads = nullptr, *m = nullptr, *v = nullptr, *state = nullptr, *act = nullptr;
     bool bound = false;
 };
@@ -861,6 +916,21 @@ int build_plan(DnPlan& p) {
             part_max = std::max(part_max, (long long)ly.G * Kw * ly.cout);
         }
     }
+    // BN batch slices: enough (h, slice, member) workgroups to fill the chip
+    long long bnp_max = 0;
+    p.bn_S.assign(ls.size(), 1);
+    p.bn_bs.assign(ls.size(), B);
+    for (size_t i = 0; i < ls.size(); ++i) {
+        const Layer& ly = ls[i];
+        if (ly.kind == K_CONV0) continue;
+        const int want = std::max(1, (2048 + ly.H * p.n - 1) / (ly.H * p.n));
+        const int bs = (B + std::min(B, want) - 1) / std::min(B, want);
+        p.bn_bs[i] = bs;
+        p.bn_S[i] = (B + bs - 1) / bs;
+        bnp_max = std::max(bnp_max, (long long)p.bn_S[i] * ly.H * 2);
+    }
+    long long bnp_ms;
+    p.bnp_off = ar.take(bnp_max * 2, &bnp_ms);   // doubles = 2 floats (arena offsets are 64-float aligned)
     p.dz_off = ar.take(dz_max, &p.dz_ms);
     p.dt_off = ar.take(std::max(dt_max, 1LL), &p.dt_ms);
     p.part_off = ar.take(part_max, &p.part_ms);
@@ -997,7 +1067,13 @@ int enqueue_forward(DnPlan& p, const float* x, const int* labels, const int* ord
             continue;
         }
         BnArgs bn = bn_args(p, ly, train);
-        hipLaunchKernelGGL(dn_bn_fwd_kernel, dim3(ly.H, n), dim3(256), 0, s, bn);
+        const size_t li = &ly - p.layers.data();
+        double* bnp = reinterpret_cast<double*>(p.act + p.bnp_off);
+        if (train)
+            hipLaunchKernelGGL(dn_bn_stats_kernel, dim3(ly.H, p.bn_S[li], n), dim3(256), 0, s, bn, bnp, p.bn_S[li],
+                               p.bn_bs[li]);
+        hipLaunchKernelGGL(dn_bn_apply_kernel, dim3(B * ly.H, n), dim3(256), 0, s, bn, (const double*)bnp,
+                           p.bn_S[li]);
         if (ly.kind == K_HEAD) {
             HeadArgs h = head_args(p, labels, order, ord_ms, row0, train);
             h.loss_out = loss_out; h.loss_sum = loss_sum; h.correct = correct;
@@ -1026,6 +1102,13 @@ int enqueue_forward(DnPlan& p, const float* x, const int* labels, const int* ord
     return MPO_OK;
 }
 
+void enqueue_bn_bwd(DnPlan& p, const BnArgs& bn, int li, hipStream_t s) {
+    double* bnp = reinterpret_cast<double*>(p.act + p.bnp_off);
+    const int S = p.bn_S[li];
+    hipLaunchKernelGGL(dn_bn_bwd_reduce_kernel, dim3(bn.H, S, p.n), dim3(256), 0, s, bn, bnp, S, p.bn_bs[li]);
+    hipLaunchKernelGGL(dn_bn_bwd_apply_kernel, dim3(p.B * bn.H, p.n), dim3(256), 0, s, bn, (const double*)bnp, S);
+}
+
 int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_ms, long long row0, hipStream_t s) {
     const int B = p.B, n = p.n;
     for (int i = (int)p.layers.size() - 1; i >= 0; --i) {
@@ -1036,7 +1119,7 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
             HeadArgs h = head_args(p, nullptr, nullptr, 0, 0, true);
             bn.bcast = 1; bn.dg = h.dg; bn.dg_ms = h.h_ms; bn.inv_hw = 1.f / (ly.H * ly.W);
             bn.dx = p.act + p.dcat_off[st]; bn.dx_ms = p.cat_ms[st]; bn.dx_ps = p.sC[st]; bn.accumulate = 0;
-            hipLaunchKernelGGL(dn_bn_bwd_kernel, dim3(ly.H, n), dim3(256), 0, s, bn);
+            enqueue_bn_bwd(p, bn, i, s);
             continue;
         }
         // dOut of this layer's conv and the input it saw
@@ -1079,7 +1162,7 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
         bn.dz = p.act + p.dz_off; bn.dz_ms = p.dz_ms;
         bn.dx = p.act + p.dcat_off[st]; bn.dx_ms = p.cat_ms[st]; bn.dx_ps = p.sC[st];
         bn.accumulate = ly.kind == K_DENSE ? 1 : 0;
-        hipLaunchKernelGGL(dn_bn_bwd_kernel, dim3(ly.H, n), dim3(256), 0, s, bn);
+        enqueue_bn_bwd(p, bn, i, s);
     }
     MPO_LAUNCH_CHECK();
     return MPO_OK;
