@@ -74,26 +74,56 @@ class TrialEvaluator:
         return out
 
     def train_units(self, units, seed_base=0):
-        """Train the given (trial, fold, spec) units as one population; returns
+        """Train the given (trial, fold, spec) units as populations -- one for the
+        test_mnist units, one per DenseNet architecture; returns
         {(trial, fold): history dict}."""
-        from .population import PopulationEngine, TrialSpec
+        from .models import DenseNetSpec
+
+        out = {}
+        mnist = [u for u in units if not isinstance(u[2], DenseNetSpec)]
+        out.update(self._train_mnist(mnist, seed_base))
+        groups = {}
+        for u in units:
+            if isinstance(u[2], DenseNetSpec):
+                groups.setdefault(u[2].arch.key(), []).append(u)
+        for us in groups.values():
+            out.update(self._train_densenet(us, seed_base))
+        return out
+
+    def _uid(self, seed_base, t, f):
+        # seeds depend on the unit's identity only, never on how units are
+        # sharded or batched: results are independent of the world size
+        return (self.init_seed + 1000003 * (seed_base + t) + f) & 0x7FFFFFFF
+
+    def _train_mnist(self, units, seed_base):
+        from .population import PopulationEngine, TrialSpec, glorot_uniform_init
 
         if not units:
             return {}
-        from .population import glorot_uniform_init
-
         specs, folds, init = [], [], []
         for (t, f, spec, _) in units:
-            # seeds depend on the unit's identity only, never on how units are
-            # sharded or batched: results are independent of the world size
-            uid = (self.init_seed + 1000003 * (seed_base + t) + f) & 0x7FFFFFFF
+            uid = self._uid(seed_base, t, f)
             s = TrialSpec(spec.nb_filters, spec.kernel_size, spec.pool_size, spec.dense, spec.lr, spec.dropout,
                           seed=uid)
             specs.append(s)
             folds.append(f)
             init.append(glorot_uniform_init(s, uid))
         eng = PopulationEngine(specs, batch=self.batch, device=self.device, init=init)
-        hist = eng.fit_folds(self.x, self.y, folds, self.n_fold, self.epochs)
+        return self._histories(units, eng.fit_folds(self.x, self.y, folds, self.n_fold, self.epochs))
+
+    def _train_densenet(self, units, seed_base):
+        from .densenet import DenseNetPopulation, he_uniform_init
+
+        arch = units[0][2].arch
+        layers = arch.layers()
+        lrs = [u[2].lr for u in units]
+        folds = [u[1] for u in units]
+        init = [he_uniform_init(layers, self._uid(seed_base, t, f)) for (t, f, _, _) in units]
+        pop = DenseNetPopulation(arch, lrs, batch=self.batch, device=self.device, init=init)
+        return self._histories(units, pop.fit_folds(self.x, self.y, folds, self.n_fold, self.epochs))
+
+    @staticmethod
+    def _histories(units, hist):
         out = {}
         for i, (t, f, _, _) in enumerate(units):
             out[(t, f)] = {"val_loss": [float(v) for v in hist["val_loss"][i]],

@@ -48,6 +48,26 @@ class DenseNetArch:
         return _lib.MpoDnArch(int(H), int(W), int(C), int(self.nb_classes), int(self.depth),
                               int(self.nb_dense_block), int(self.growth_rate), int(self.nb_filter))
 
+    def layers(self):
+        """Layer geometry (densenet.py:155-196), as the C plan builds it."""
+        H, W, C0 = self.img_dim
+        L = (self.depth - 4) // 3
+        f, stage = self.nb_filter, 0
+        out = [dict(kind="conv0", stage=0, H=H, W=W, cin=C0, cout=f, ks=3, coff=0)]
+        for blk in range(self.nb_dense_block):
+            for _ in range(L):
+                out.append(dict(kind="dense", stage=stage, H=H, W=W, cin=f, cout=self.growth_rate, ks=3, coff=f))
+                f += self.growth_rate
+            if blk < self.nb_dense_block - 1:
+                out.append(dict(kind="trans", stage=stage, H=H, W=W, cin=f, cout=f, ks=1, coff=0))
+                H, W, stage = H // 2, W // 2, stage + 1
+        out.append(dict(kind="head", stage=stage, H=H, W=W, cin=f, cout=self.nb_classes, ks=0, coff=0))
+        return out
+
+    def key(self):
+        return (tuple(self.img_dim), self.nb_classes, self.depth, self.nb_dense_block, self.growth_rate,
+                self.nb_filter)
+
     @classmethod
     def from_spec(cls, spec):
         """From a ``test_densenet`` / ``DenseNetModel`` JSON spec (models.py)."""

@@ -8,7 +8,8 @@
   names the dimension ``dropout`` (option3:131): the dimension is dead and
   the rate stays 0.25 -- reproduced here.
 * ``test_cnn`` / ``test_densenet`` -- mpiLAPI.py:178-201 (topclass CNN, DenseNet)
-  as JSON specs (not trainable by the MNIST population engine).
+  as JSON specs; a DenseNet spec ingests into a :class:`DenseNetSpec` that the
+  DenseNet population engine (densenet.py) trains.
 * ``BuilderFromFunction`` -- hyperparameter_search_option3.py:22-31: zips the
   named dimensions with a parameter list, calls ``model_fn(**named)`` and wraps
   the JSON in a ``ModelFromJson`` with settable ``comm`` / ``device`` and
@@ -97,9 +98,32 @@ def test_densenet(nb_classes=3, img_dim=(150, 94, 5), depth=10, nb_dense_block=3
         )
 
 
+class DenseNetSpec:
+    """A DenseNet trial: the architecture (densenet.py:135) and its Adam lr, which
+    the reference compiles into the model (base_model.py:67-71) and searches."""
+
+    def __init__(self, arch, lr):
+        self.arch = arch
+        self.lr = float(lr)
+
+    def flops_per_sample_train(self):
+        from .densenet import flops_per_sample_train
+
+        return flops_per_sample_train(self.arch.layers())
+
+
 def spec_from_json(json_str, lr=1e-3, seed=0):
-    """Ingest a test_mnist-topology Keras JSON into a device TrialSpec."""
+    """Ingest a Keras JSON into a device spec: the test_mnist Sequential topology
+    -> :class:`TrialSpec`; a DenseNet spec (``test_densenet`` / ``DenseNetModel``)
+    -> :class:`DenseNetSpec` (its own compiled lr, the searched dimension)."""
     d = json.loads(json_str)
+    cfg = d.get("config")
+    if d.get("class_name") == "Model" and isinstance(cfg, dict) and cfg.get("arch") == "densenet":
+        from .densenet import DenseNetArch
+
+        if float(cfg.get("dropout_rate", 0.0)) != 0.0:
+            raise ValueError("DenseNet population trains dropout_rate 0 (the reference grid, base_model.py:88)")
+        return DenseNetSpec(DenseNetArch.from_spec(cfg), cfg.get("lr", lr))
     if d.get("class_name") != "Sequential":
         raise ValueError("population engine trains the test_mnist Sequential topology only")
     layers = d["config"]["layers"] if isinstance(d["config"], dict) else d["config"]
@@ -236,6 +260,6 @@ def flops_of_params(model_fn, names, params):
     return spec.flops_per_sample_train()
 
 
-__all__ = ["test_mnist", "test_cnn", "test_densenet", "spec_from_json", "ModelFromJson", "BuilderFromFunction",
+__all__ = ["test_mnist", "test_cnn", "test_densenet", "spec_from_json", "DenseNetSpec", "ModelFromJson", "BuilderFromFunction",
            "BaseModel", "CNNModel", "DenseNetModel", "mnist_space", "topclass_space", "gan_space",
            "threaded_skopt_space"]

@@ -136,3 +136,21 @@ def test_fit_folds_reference_config_runs():
     assert h["val_loss"].shape == (5, 2) and np.isfinite(h["val_loss"]).all()
     assert h["train_loss"].shape == (5, 2 * h["steps_per_epoch"])
     assert np.isfinite(h["train_loss"]).all()
+
+
+def test_trial_evaluator_routes_densenet_specs():
+    """BuilderFromFunction(test_densenet) -> TrialEvaluator trains DenseNet trials
+    as one population and returns fold-mean validation losses (FOMs)."""
+    from mpi_opt_amd.blocks import TrialEvaluator
+    from mpi_opt_amd.densenet import synthetic_cifar
+    from mpi_opt_amd.models import BuilderFromFunction, test_densenet
+    from mpi_opt_amd.space import Real
+
+    prov = BuilderFromFunction(lambda llr: test_densenet(nb_classes=10, img_dim=(16, 16, 3), depth=7,
+                                                         lr=10.0 ** llr), [Real(-5.0, 1.0, name="llr")])
+    x, y = synthetic_cifar(n=120, img_dim=(16, 16, 3), seed=1)
+    ev = TrialEvaluator(prov, x, y, n_fold=2, epochs=1, batch=20)
+    foms = ev.evaluate([[-3.0], [-2.0], [-4.0]])
+    assert len(foms) == 3 and all(np.isfinite(foms))
+    # distinct learning rates give distinct fold-mean validation losses
+    assert len(set(round(f, 6) for f in foms)) == 3

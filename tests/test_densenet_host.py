@@ -84,3 +84,22 @@ def test_flops_reference_config():
     assert flops_per_sample_fwd(layers) == od.flops_per_sample_fwd(layers)
     assert flops_per_sample_train(layers) == od.flops_per_sample_train(layers)
     assert np.isclose(flops_per_sample_fwd(layers) / 1e6, 22.8, atol=0.5)
+
+
+def test_python_layer_geometry_matches_oracle_and_spec_ingestion():
+    from mpi_opt_amd.densenet import DenseNetArch
+    from mpi_opt_amd.models import DenseNetModel, DenseNetSpec, spec_from_json, test_densenet
+
+    for img, depth, blocks in [((32, 32, 3), 10, 3), ((9, 11, 2), 7, 2), ((150, 94, 5), 13, 3)]:
+        arch = DenseNetArch(img_dim=img, nb_classes=4, depth=depth, nb_dense_block=blocks)
+        ref = od.arch_layers(img_dim=img, nb_classes=4, depth=depth, nb_dense_block=blocks)
+        got = arch.layers()
+        assert [{k: l[k] for k in ("kind", "H", "W", "cin", "cout")} for l in got] == \
+               [{k: l[k] for k in ("kind", "H", "W", "cin", "cout")} for l in ref]
+    spec = spec_from_json(DenseNetModel(input_shape=(32, 32, 3)).build([10, 3, 12, 0.0, 16, -3]))
+    assert isinstance(spec, DenseNetSpec) and abs(spec.lr - 1e-3) < 1e-15
+    assert spec.arch.key() == ((32, 32, 3), 3, 10, 3, 12, 16)
+    assert spec.flops_per_sample_train() == od.flops_per_sample_train(od.arch_layers(img_dim=(32, 32, 3),
+                                                                                     nb_classes=3))
+    with pytest.raises(ValueError):
+        spec_from_json(test_densenet(dropout_rate=0.2))

@@ -30,8 +30,10 @@ def test_builder_from_function_maps_names():
 def test_unsupported_topologies_raise():
     with pytest.raises(ValueError):
         M.spec_from_json(M.test_cnn(kernel_size=3))
+    # DenseNet specs are trainable now (DenseNet population); dropout is not
+    assert isinstance(M.spec_from_json(M.test_densenet()), M.DenseNetSpec)
     with pytest.raises(ValueError):
-        M.spec_from_json(M.test_densenet())
+        M.spec_from_json(M.test_densenet(dropout_rate=0.5))
 
 
 def test_base_models_interface():
