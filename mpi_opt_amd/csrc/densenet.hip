@@ -246,15 +246,24 @@ __global__ __launch_bounds__(256) void dn_conv_kernel(ConvArgs a) {
 }
 
 // ============================================================================
-// Weight gradient: dW[(ky,kx,c)][n] = sum_{b,y,x} in[b][y+ky-P][x+kx-P][c] * dout[b][y][x][n]
-// One workgroup = (member, 256-row m-group, group of spg samples); loops over its
-// samples' row chunks (<= 128 pixels), staging the input rows (+ halo) and the
-// dOut rows in LDS; 4 waves x up to 4 m-tiles.  One partial slab per group.
+// Weight gradient of a 3x3 'same' conv:
+//   dW[(ky,kx,c)][n] = sum_{b,y,x} in[b][y+ky-1][x+kx-1][c] * dout[b][y][x][n]
+// GEMM view M = 9 cin weight rows, N = cout, K = pixels.  One workgroup =
+// (member, 768-row m-group, group of spg samples): 8 waves x up to 6 m-tiles, so
+// every DenseNet layer of the reference grid (M <= 684) stages each input row
+// chunk exactly once.  Per row chunk (<= 128 pixels) the input rows + halo and
+// the dOut rows are staged in LDS; the zero halo columns / padding channels are
+// written once per workgroup, the data with float4 loads when the channel
+// counts allow (runtime-uniform branch).  One partial slab per sample group.
 // ============================================================================
+constexpr int kWgWaves = 8;
+constexpr int kWgMT = 6;
+constexpr int kWgRows = kWgWaves * kWgMT * 16;   // 768
+
 template <int MT, int NT>
 __device__ __forceinline__ void dn_wgrad_chunk(const float* __restrict__ img, const float* __restrict__ dl,
-                                               const int* __restrict__ ptab, const int (&aoff)[4], int ns, int nk4,
-                                               int krow, int kcol, f32x4 (&acc)[4][NT]) {
+                                               const int* __restrict__ ptab, const int (&aoff)[kWgMT], int ns, int nk4,
+                                               int krow, int kcol, f32x4 (&acc)[kWgMT][NT]) {
     float a0[MT], a1[MT], b0[NT], b1[NT];
     auto rd = [&](int s, float (&av)[MT], float (&bv)[NT]) {
         const int p = 4 * s + krow;
@@ -284,10 +293,11 @@ __device__ __forceinline__ void dn_wgrad_chunk(const float* __restrict__ img, co
     }
 }
 
-template <int KS, int NT>
-__global__ __launch_bounds__(256) void dn_wgrad_kernel(WgArgs a) {
+template <int NT>
+__global__ __launch_bounds__(kWgWaves * 64) void dn_wgrad3_kernel(WgArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    constexpr int P = (KS - 1) / 2;
+    constexpr int KS = 3, P = 1;
+    constexpr int NTH = kWgWaves * 64;
     const int m = blockIdx.z, grp = blockIdx.y, mg = blockIdx.x;
     const int H = a.H, W = a.W, Cin = a.Cin, N = a.N;
     const int Kw = KS * KS * Cin;
@@ -296,8 +306,7 @@ __global__ __launch_bounds__(256) void dn_wgrad_kernel(WgArgs a) {
     const int ns = wg_ns(NT);
     const int R = a.R;
     const int rows = R + KS - 1;
-    const int row_elems = Wp * Cp;
-    const int img_elems = rows * row_elems;
+    const int img_elems = rows * Wp * Cp;
     const int np = 4 * (((R * W + 3) >> 2) + 1);   // pixel slots incl. one zero k-step of slack
     float* img = smem;
     float* dl = smem + r4(img_elems);
@@ -306,14 +315,13 @@ __global__ __launch_bounds__(256) void dn_wgrad_kernel(WgArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int krow = lane >> 4, kcol = lane & 15;
     const int mtiles = (Kw + 15) >> 4;
-    const int t0 = mg * 16;
-    const int mine = __builtin_amdgcn_readfirstlane(min(4, max(0, (mtiles - t0 - wave + 3) / 4)));
-    if (mine == 0 && mtiles - t0 <= 0) return;   // whole workgroup idle (never happens for a sized grid)
+    const int t0 = mg * (kWgRows / 16);
+    const int mine = __builtin_amdgcn_readfirstlane(min(kWgMT, max(0, (mtiles - t0 - wave + kWgWaves - 1) / kWgWaves)));
 
-    int aoff[4];
+    int aoff[kWgMT];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r = (t0 + wave + 4 * i) * 16 + (lane & 15);
+    for (int i = 0; i < kWgMT; ++i) {
+        const int r = (t0 + wave + kWgWaves * i) * 16 + (lane & 15);
         int off = 0;   // rows past Kw read finite LDS; their partials are never stored
         if (r < Kw) {
             const int tap = r / Cin, c = r - tap * Cin;
@@ -322,13 +330,20 @@ __global__ __launch_bounds__(256) void dn_wgrad_kernel(WgArgs a) {
         }
         aoff[i] = off;
     }
-    for (int p = tid; p < np; p += 256) ptab[p] = p < R * W ? ((p / W) * Wp + (p % W)) * Cp : 0;
-    f32x4 acc[4][NT];
+    // zero everything once: halo columns, padding channels and dOut padding stay zero
+    for (int e = tid; e < r4(img_elems) + np * ns; e += NTH) smem[e] = 0.f;
+    for (int p = tid; p < np; p += NTH) ptab[p] = p < R * W ? ((p / W) * Wp + (p % W)) * Cp : 0;
+    f32x4 acc[kWgMT][NT];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < kWgMT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // vector staging when every row segment is float4-aligned (uniform)
+    const bool vin = ((Cin & 3) == 0) && ((a.in_ps & 3) == 0) && !a.order &&
+                     ((reinterpret_cast<uintptr_t>(a.in) & 15) == 0);
+    const bool vdo = ((N & 3) == 0) && ((a.dout_ps & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.dout) & 15) == 0);
+    const int C4 = Cin >> 2, N4 = N >> 2;
     const int b0 = grp * a.spg, b1 = min(a.B, b0 + a.spg);
     const float* inm = a.in + m * a.in_ms;
     const float* dom = a.dout + m * a.dout_ms;
@@ -337,33 +352,62 @@ __global__ __launch_bounds__(256) void dn_wgrad_kernel(WgArgs a) {
                                    : inm + (long long)b * H * W * a.in_ps;
         for (int y0 = 0; y0 < H; y0 += R) {
             const int Mc = min(R, H - y0) * W;
-            __syncthreads();   // the previous chunk's MFMAs are done with the LDS
-            for (int e = tid; e < img_elems; e += 256) {
-                const int r = e / row_elems, rem = e - r * row_elems;
-                const int col = rem / Cp, c = rem - col * Cp;
-                const int gy = y0 + r - P, gx = col - P;
-                float v = 0.f;
-                if (gy >= 0 && gy < H && gx >= 0 && gx < W && c < Cin) v = src[((long long)gy * W + gx) * a.in_ps + c];
-                img[e] = v;
+            __syncthreads();   // the previous chunk's MFMAs are done with the LDS (and the zero fill)
+            if (vin) {
+                const int tot = rows * W * C4;
+                for (int e = tid; e < tot; e += NTH) {
+                    const int pix = e / C4, c4 = e - pix * C4;
+                    const int r = pix / W, x = pix - r * W;
+                    const int gy = y0 + r - P;
+                    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (gy >= 0 && gy < H)
+                        v = *reinterpret_cast<const float4*>(src + ((long long)gy * W + x) * a.in_ps + 4 * c4);
+                    *reinterpret_cast<float4*>(img + (r * Wp + x + P) * Cp + 4 * c4) = v;
+                }
+            } else {
+                const int tot = rows * W * Cin;
+                for (int e = tid; e < tot; e += NTH) {
+                    const int pix = e / Cin, c = e - pix * Cin;
+                    const int r = pix / W, x = pix - r * W;
+                    const int gy = y0 + r - P;
+                    float v = 0.f;
+                    if (gy >= 0 && gy < H) v = src[((long long)gy * W + x) * a.in_ps + c];
+                    img[(r * Wp + x + P) * Cp + c] = v;
+                }
             }
             const float* dsrc = dom + ((long long)b * H + y0) * W * a.dout_ps;
-            for (int e = tid; e < np * ns; e += 256) {
-                const int p = e / ns, n = e - p * ns;
-                dl[e] = (p < Mc && n < N) ? dsrc[(long long)p * a.dout_ps + n] : 0.f;
+            const int npix = R * W;   // rows past Mc are zeroed (the last chunk of a sample)
+            if (vdo) {
+                for (int e = tid; e < npix * N4; e += NTH) {
+                    const int p = e / N4, n4 = e - p * N4;
+                    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (p < Mc) v = *reinterpret_cast<const float4*>(dsrc + (long long)p * a.dout_ps + 4 * n4);
+                    *reinterpret_cast<float4*>(dl + p * ns + 4 * n4) = v;
+                }
+            } else {
+                for (int e = tid; e < npix * N; e += NTH) {
+                    const int p = e / N, n = e - p * N;
+                    dl[p * ns + n] = p < Mc ? dsrc[(long long)p * a.dout_ps + n] : 0.f;
+                }
             }
             __syncthreads();
             const int nk4 = (Mc + 3) >> 2;
-            if (mine == 4) dn_wgrad_chunk<4, NT>(img, dl, ptab, aoff, ns, nk4, krow, kcol, acc);
-            else if (mine == 3) dn_wgrad_chunk<3, NT>(img, dl, ptab, aoff, ns, nk4, krow, kcol, acc);
-            else if (mine == 2) dn_wgrad_chunk<2, NT>(img, dl, ptab, aoff, ns, nk4, krow, kcol, acc);
-            else if (mine == 1) dn_wgrad_chunk<1, NT>(img, dl, ptab, aoff, ns, nk4, krow, kcol, acc);
+            switch (mine) {
+                case 6: dn_wgrad_chunk<6, NT>(img, dl, ptab, aoff, ns, nk4, krow, kcol, acc); break;
+                case 5: dn_wgrad_chunk<5, NT>(img, dl, ptab, aoff, ns, nk4, krow, kcol, acc); break;
+                case 4: dn_wgrad_chunk<4, NT>(img, dl, ptab, aoff, ns, nk4, krow, kcol, acc); break;
+                case 3: dn_wgrad_chunk<3, NT>(img, dl, ptab, aoff, ns, nk4, krow, kcol, acc); break;
+                case 2: dn_wgrad_chunk<2, NT>(img, dl, ptab, aoff, ns, nk4, krow, kcol, acc); break;
+                case 1: dn_wgrad_chunk<1, NT>(img, dl, ptab, aoff, ns, nk4, krow, kcol, acc); break;
+                default: break;
+            }
         }
     }
     float* part = a.part + m * a.part_ms + (long long)grp * Kw * N;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < kWgMT; ++i) {
         if (i >= mine) break;
-        const int mt = t0 + wave + 4 * i;
+        const int mt = t0 + wave + kWgWaves * i;
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
             const int n = j * 16 + kcol;
@@ -375,6 +419,87 @@ __global__ __launch_bounds__(256) void dn_wgrad_kernel(WgArgs a) {
             }
         }
     }
+}
+
+// ============================================================================
+// Weight gradient of a 1x1 conv (the transitions): dW[c][n] = sum_p z[p][c] dout[p][n],
+// a plain GEMM with tiny M = cin and N = cout and K = the group's pixels, which are
+// contiguous in both operands.  Split-K inside the workgroup: every wave holds all
+// MT x NT tiles and streams every 8th k-step straight from global memory (no LDS
+// staging); the 8 partial accumulators are summed through LDS in fixed order.
+// ============================================================================
+template <int MT, int NT>
+__global__ __launch_bounds__(kWgWaves * 64) void dn_wgrad1_kernel(WgArgs a) {
+    __shared__ __attribute__((aligned(16))) float red[kWgWaves - 1][MT * NT * 4 * 64];
+    const int m = blockIdx.z, grp = blockIdx.y;
+    const int Cin = a.Cin, N = a.N;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int krow = lane >> 4, kcol = lane & 15;
+    const int HW = a.H * a.W;
+    const int b0 = grp * a.spg, b1 = min(a.B, b0 + a.spg);
+    const long long p0 = (long long)b0 * HW, p1 = (long long)b1 * HW;
+    const float* z = a.in + m * a.in_ms;
+    const float* d = a.dout + m * a.dout_ms;
+    bool am[MT], bm[NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) am[i] = i * 16 + kcol < Cin;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) bm[j] = j * 16 + kcol < N;
+    f32x4 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // k-step s covers pixels [p0 + 4s, p0 + 4s + 4); wave w takes s = w, w + 8, ...
+    const long long nsteps = (p1 - p0 + 3) >> 2;
+    float av[2][MT], bv[2][NT];
+    auto ld = [&](long long s, float (&A)[MT], float (&Bv)[NT]) {
+        const long long p = p0 + 4 * s + krow;
+        const bool ok = p < p1;
+        const float* zp = z + p * a.in_ps + kcol;
+        const float* dp = d + p * a.dout_ps + kcol;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) A[i] = (ok && am[i]) ? zp[i * 16] : 0.f;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) Bv[j] = (ok && bm[j]) ? dp[j * 16] : 0.f;
+    };
+    // A operand: lane (row = lane & 15 = channel c, k = krow = pixel); B: (k = pixel, col = n)
+    long long s = wave;
+    if (s < nsteps) ld(s, av[0], bv[0]);
+    int cur = 0;
+    for (; s < nsteps; s += kWgWaves) {
+        if (s + kWgWaves < nsteps) ld(s + kWgWaves, av[cur ^ 1], bv[cur ^ 1]);
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[cur][i], bv[cur][j], acc[i][j], 0, 0, 0);
+        cur ^= 1;
+    }
+    if (wave > 0) {
+        float* r = red[wave - 1];
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) r[((i * NT + j) * 4 + q) * 64 + lane] = acc[i][j][q];
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    float* part = a.part + m * a.part_ms + (long long)grp * Cin * N;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float v = acc[i][j][q];
+                for (int w = 0; w < kWgWaves - 1; ++w) v += red[w][((i * NT + j) * 4 + q) * 64 + lane];
+                const int row = i * 16 + krow * 4 + q, n = j * 16 + kcol;
+                if (row < Cin && n < N) part[(long long)row * N + n] = v;
+            }
 }
 
 // grads[w_off + e] = sum_g part[g][e]  (fixed order: deterministic)
@@ -817,6 +942,7 @@ size_t conv_lds(int R, int W, int ks, int cin) {
 }
 
 size_t wg_lds(int R, int W, int ks, int cin, int nt) {
+    if (ks == 1) return 0;   // dn_wgrad1: static LDS only
     const int img = (R + ks - 1) * (W + ks - 1) * wg_cp(cin);
     const int np = 4 * (((R * W + 3) >> 2) + 1);
     return (size_t)(r4(img) + np * wg_ns(nt) + np) * sizeof(float);
@@ -908,7 +1034,7 @@ int build_plan(DnPlan& p) {
             ly.R = rows_per_chunk(ly.H, ly.W);
             ly.Rw = ly.R;
             const long long Kw = (long long)taps * ly.cin;
-            const int mgroups = (int)((Kw + 255) / 256);
+            const int mgroups = ly.ks == 1 ? 1 : (int)((Kw + kWgRows - 1) / kWgRows);
             const int gt = std::max(1, (target + mgroups * p.n - 1) / (mgroups * p.n));
             const int G0 = std::min(B, gt);
             ly.spg = (B + G0 - 1) / G0;
@@ -950,11 +1076,11 @@ void launch_conv_t(const ConvArgs& a, dim3 grid, size_t lds, hipStream_t s) {
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a);
 }
 
-template <int KS, int NT>
-void launch_wg_t(const WgArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-    auto kern = dn_wgrad_kernel<KS, NT>;
+template <int NT>
+void launch_wg3_t(const WgArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+    auto kern = dn_wgrad3_kernel<NT>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a);
+    hipLaunchKernelGGL(kern, grid, dim3(kWgWaves * 64), lds, s, a);
 }
 
 template <int KS>
@@ -975,21 +1101,43 @@ int launch_conv(const ConvArgs& a, int n_members, int B, hipStream_t s) {
     return MPO_OK;
 }
 
-template <int KS>
-int launch_wgrad(const WgArgs& a, int n_members, int G, hipStream_t s) {
+// 1x1 weight gradient: MT x NT tiles per wave (<= 6 x 6, i.e. cin, cout <= 96)
+template <int MT>
+void launch_wg1_mt(const WgArgs& a, dim3 grid, int nt, hipStream_t s) {
+    switch (nt) {
+        case 1: hipLaunchKernelGGL((dn_wgrad1_kernel<MT, 1>), grid, dim3(kWgWaves * 64), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((dn_wgrad1_kernel<MT, 2>), grid, dim3(kWgWaves * 64), 0, s, a); break;
+        case 3: hipLaunchKernelGGL((dn_wgrad1_kernel<MT, 3>), grid, dim3(kWgWaves * 64), 0, s, a); break;
+        case 4: hipLaunchKernelGGL((dn_wgrad1_kernel<MT, 4>), grid, dim3(kWgWaves * 64), 0, s, a); break;
+        default: break;
+    }
+}
+
+int launch_wgrad(const WgArgs& a, int ks, int n_members, int G, hipStream_t s) {
     const int nt = (a.N + 15) / 16;
-    const int Kw = KS * KS * a.Cin;
-    const dim3 grid((Kw + 255) / 256, G, n_members);
-    const size_t lds = wg_lds(a.R, a.W, KS, a.Cin, nt);
+    if (ks == 1) {
+        const int mt = (a.Cin + 15) / 16;
+        if (mt > 4 || nt > 4) { mpo::set_error("dn_wgrad1: cin %d / cout %d > 64 unsupported", a.Cin, a.N); return MPO_ENOTSUP; }
+        const dim3 grid(1, G, n_members);
+        switch (mt) {
+            case 1: launch_wg1_mt<1>(a, grid, nt, s); break;
+            case 2: launch_wg1_mt<2>(a, grid, nt, s); break;
+            case 3: launch_wg1_mt<3>(a, grid, nt, s); break;
+            case 4: launch_wg1_mt<4>(a, grid, nt, s); break;
+            default: break;
+        }
+        return MPO_OK;
+    }
+    const int Kw = 9 * a.Cin;
+    const dim3 grid((Kw + kWgRows - 1) / kWgRows, G, n_members);
+    const size_t lds = wg_lds(a.R, a.W, 3, a.Cin, nt);
     if (lds > ((size_t)160 << 10)) { mpo::set_error("dn_wgrad: LDS %zu B exceeds 160 KiB", lds); return MPO_ENOTSUP; }
     switch (nt) {
-        case 1: launch_wg_t<KS, 1>(a, grid, lds, s); break;
-        case 2: launch_wg_t<KS, 2>(a, grid, lds, s); break;
-        case 3: launch_wg_t<KS, 3>(a, grid, lds, s); break;
-        case 4: launch_wg_t<KS, 4>(a, grid, lds, s); break;
-        case 5: launch_wg_t<KS, 5>(a, grid, lds, s); break;
-        case 6: launch_wg_t<KS, 6>(a, grid, lds, s); break;
-        default: mpo::set_error("dn_wgrad: %d output channels unsupported (max 96)", a.N); return MPO_ENOTSUP;
+        case 1: launch_wg3_t<1>(a, grid, lds, s); break;
+        case 2: launch_wg3_t<2>(a, grid, lds, s); break;
+        case 3: launch_wg3_t<3>(a, grid, lds, s); break;
+        case 4: launch_wg3_t<4>(a, grid, lds, s); break;
+        default: mpo::set_error("dn_wgrad: %d output channels unsupported (max 64)", a.N); return MPO_ENOTSUP;
     }
     return MPO_OK;
 }
@@ -1144,8 +1292,7 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
         } else {
             w.in = p.act + ly.z_off; w.in_ms = ((long long)B * ly.H * ly.W * ly.cin + 63) & ~63LL; w.in_ps = ly.cin;
         }
-        if (ly.ks == 3) DN_TRY(launch_wgrad<3>(w, n, ly.G, s));
-        else DN_TRY(launch_wgrad<1>(w, n, ly.G, s));
+        DN_TRY(launch_wgrad(w, ly.ks, n, ly.G, s));
         const long long cnt = (long long)ly.ks * ly.ks * ly.cin * ly.cout;
         hipLaunchKernelGGL(dn_wgrad_reduce_kernel, flat_grid(cnt, n), dim3(256), 0, s, (const float*)(p.act + p.part_off),
                            p.part_ms, ly.G, cnt, p.grads, p.n_params, ly.w_off);
@@ -1195,8 +1342,8 @@ int mpo_dn_create(const MpoDnArch* arch, int n_members, int batch, void** handle
         if (ly.kind == K_HEAD) continue;
         if (conv_lds(ly.R, ly.W, ly.ks, ly.cin) > ((size_t)160 << 10) ||
             conv_lds(ly.R, ly.W, ly.ks, ly.cout) > ((size_t)160 << 10) ||
-            wg_lds(ly.Rw, ly.W, ly.ks, ly.cin, (ly.cout + 15) / 16) > ((size_t)160 << 10) || ly.cout > 96 ||
-            (ly.kind != K_CONV0 && ly.cin > 96)) {
+            wg_lds(ly.Rw, ly.W, ly.ks, ly.cin, (ly.cout + 15) / 16) > ((size_t)160 << 10) || ly.cout > 64 ||
+            (ly.kind != K_CONV0 && ly.cin > 96) || (ly.ks == 1 && ly.cin > 64)) {
             mpo::set_error("mpo_dn_create: layer (cin %d, cout %d, %dx%d) exceeds the kernels' LDS / channel range",
                            ly.cin, ly.cout, ly.H, ly.W);
             return MPO_ENOTSUP;
