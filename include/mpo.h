@@ -98,6 +98,24 @@ int mpo_gp_prepare(const double* X, const double* y_norm, int n, int d, const do
                    double amp, double noise, double y_mean, double y_std,
                    MpoGpModel* model, void* ws, size_t ws_bytes, void* stream);
 
+/* Workspace bytes for mpo_gp_lml_grad (n <= 2048, d <= 32, batch thetas); 0 if unsupported. */
+size_t mpo_gp_lml_ws_bytes(int n, int d, int batch);
+
+/* Log-marginal likelihood and its gradient for `batch` hyper-parameter vectors at
+ * once (one workgroup each): sklearn GaussianProcessRegressor(normalize_y=True,
+ * alpha=1e-10).log_marginal_likelihood(theta, eval_gradient=True) for skopt's
+ * kernel C * Matern(ls, nu=2.5) + WhiteKernel (sklearn _gpr.py:537-655), the
+ * objective of the L-BFGS-B refit that skopt.Optimizer.tell runs from
+ * Coordinator.fit (coordinator.py:63-79).
+ *   X [n][d], y_norm [n] (normalised targets)      device
+ *   theta [batch][d+2] = log[amp, ls_0..ls_{d-1}, noise]  (sklearn kernel.theta)
+ *   lml [batch], grad [batch][d+2], info [batch]    device outputs
+ * info[b] = j+1 when the Cholesky fails at column j: lml = -inf, grad = 0 (as
+ * sklearn's LinAlgError branch); 0 otherwise. */
+int mpo_gp_lml_grad(const double* X, const double* y_norm, int n, int d,
+                    const double* theta, int batch, double* lml, double* grad,
+                    int32_t* info, void* ws, size_t ws_bytes, void* stream);
+
 /* Workspace bytes for mpo_gp_acq_score over m candidates. */
 size_t mpo_gp_score_ws_bytes(const MpoGpModel* model, int64_t m, int k);
 

@@ -1,0 +1,412 @@
+// gp_fit.hip -- GP hyper-parameter fit on device: log-marginal likelihood and its
+// gradient for a batch of hyper-parameter vectors (gfx950, fp64).
+//
+// SURVEY §8a G1 / §8f rank 1.  skopt's Optimizer.tell refits
+//   C(1,(0.01,1000)) * Matern(ls, (0.01,100), nu=2.5) + WhiteKernel()
+// with sklearn's GaussianProcessRegressor(normalize_y=True, alpha=1e-10):
+// L-BFGS-B over theta = log[amp, ls_0..ls_{d-1}, noise] from the kernel's start
+// and n_restarts_optimizer uniform draws, each evaluation being
+// log_marginal_likelihood(theta, eval_gradient=True)
+// (sklearn gaussian_process/_gpr.py:296-337 and :537-655, kernels.py:1596-1724).
+// The reference reaches it from Coordinator.fit (/root/reference/coordinator.py:63-79).
+//
+// One workgroup (1024 threads) evaluates one theta; a launch covers a batch of
+// thetas (the restarts advance in lockstep on the host), so the fit costs one
+// launch per L-BFGS iteration instead of B host evaluations.
+//
+// Per workgroup, n <= 200 (the factor fits the 160 KB LDS as a packed triangle):
+//   1. K = amp * Matern52(|x_i/ls - x_j/ls|) + (noise + 1e-10) I   -> LDS, packed
+//      lower, column-major
+//   2. right-looking Cholesky in LDS, one barrier per column (the pivot scaling
+//      of column j-1 is deferred into step j: it touches no column step j reads)
+//   3. the factor moves to the global workspace (row-major packed) and L^-1 is
+//      built in the LDS (row-major packed): thread c forward-substitutes e_c,
+//      reading row i of L wave-uniformly and its own column from LDS
+//   4. z = L^-1 y, alpha = L^-T z;  lml = -y.alpha/2 - sum log L_jj - n/2 log 2pi
+//   5. per pair (i >= j): K^-1_ij = sum_m L^-1_mi L^-1_mj (LDS), W = a_i a_j - K^-1_ij,
+//      recompute dK_ij/dtheta and accumulate W dK (x2 off the diagonal)
+//   6. fixed-order reduction -> grad = 0.5 * sum_ij W_ij dK_ij/dtheta
+// For n > 200 the same code runs with the factor and L^-1 in the global workspace.
+// Everything is deterministic: fixed summation orders, no atomics.
+
+#include "mpo_internal.h"
+
+#include <cmath>
+#include <cstdlib>
+
+namespace {
+
+constexpr int kFitThreads = 1024;
+constexpr int kFitWaves = kFitThreads / 64;
+constexpr int kFitMaxN = 2048;
+constexpr int kFitLdsMaxN = 200;  // 200*201/2 doubles = 160800 B of the 163840 B LDS
+constexpr double kSqrt5 = 2.236067977499789696409173668731276235;
+constexpr double kLog2Pi = 1.837877066409345483560659472811235280;
+constexpr double kFitJitter = 1e-10;  // sklearn GaussianProcessRegressor alpha (_gpr.py:207)
+
+struct LmlArgs {
+    const double* X;      // [n][d]
+    const double* y;      // [n] normalised targets
+    int n, d;
+    const double* theta;  // [B][d+2]
+    double* lml;          // [B]
+    double* grad;         // [B][d+2]
+    int32_t* info;        // [B]
+    double* ws;           // per theta: ws_stride doubles
+    long long ws_stride;
+    int stop;             // diagnostics only (env MPO_FIT_DEBUG): return after phase 2/3/4
+};
+
+__host__ __device__ inline long long fit_tri(long long n) { return n * (n + 1) / 2; }
+
+// per-theta workspace (doubles): xs [n][d] | z [n] | alpha [n] | factor, packed [n(n+1)/2]
+// | L^-1 [n][n] (global variant only)
+__host__ __device__ inline long long fit_ws_doubles(int n, int d, bool lds) {
+    auto al = [](long long x) { return (x + 31) & ~31LL; };
+    return al((long long)n * d) + 2 * al(n) + al(fit_tri(n)) + (lds ? 0 : al((long long)n * n));
+}
+
+__device__ __forceinline__ double wave_sum_bcast(double v) {
+    // fixed butterfly; lane 0's result is broadcast so every lane holds the same bits
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    return __shfl(v, 0);
+}
+
+// v_readlane of a double at a wave-uniform lane (two 32-bit halves -> SGPRs)
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const unsigned long long u = __double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
+template <bool kLds, int DP>
+__global__ __launch_bounds__(kFitThreads) void lml_grad_kernel(LmlArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double fsm[];
+    const int b = blockIdx.x;
+    const int n = a.n, d = a.d;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const double* th = a.theta + (long long)b * (d + 2);
+    auto al = [](long long x) { return (x + 31) & ~31LL; };
+    double* ws = a.ws + (long long)b * a.ws_stride;
+    double* xs = ws;
+    double* z = xs + al((long long)n * d);
+    double* alpha = z + al(n);
+    double* Lg = alpha + al(n);              // global packed factor
+    double* Linv_g = Lg + al(fit_tri(n));    // global variant: L^-1 [n][n]
+    // LDS variant: the factor is built in LDS (column-major packed) and copied to Lg
+    // (row-major packed) before L^-1 takes the LDS over (row-major packed).
+    // Global variant: the factor lives in Lg column-major, L^-1 in Linv_g.
+    double* Lp = kLds ? fsm : Lg;
+    auto cidx = [n](int i, int j) { return j * n - j * (j - 1) / 2 + (i - j); };
+    auto ridx = [](int i, int j) { return i * (i + 1) / 2 + j; };
+
+    // kernel.theta setter: params = exp(theta) (sklearn kernels.py Hyperparameter theta)
+    const double amp = exp(th[0]);
+    const double noise = exp(th[d + 1]);
+    double ls[DP];
+#pragma unroll
+    for (int c = 0; c < DP; ++c) ls[c] = c < d ? exp(th[1 + c]) : 1.0;
+
+    // ---- 1. K (packed lower, column-major) from xs = X / ls (pdist(X / ls))
+    for (int e = tid; e < n * d; e += kFitThreads) {
+        const int c = e % d;
+        double lc = 1.0;
+#pragma unroll
+        for (int q = 0; q < DP; ++q)
+            if (q == c) lc = ls[q];
+        xs[e] = a.X[e] / lc;
+    }
+    __syncthreads();
+    for (int j = wave; j < n; j += kFitWaves) {
+        double xj[DP];
+#pragma unroll
+        for (int c = 0; c < DP; ++c) xj[c] = c < d ? xs[j * d + c] : 0.0;
+        for (int i = j + lane; i < n; i += 64) {
+            double v;
+            if (i == j) {
+                v = amp * 1.0 + noise + kFitJitter;
+            } else {
+                double r2 = 0.0;
+#pragma unroll
+                for (int c = 0; c < DP; ++c)
+                    if (c < d) {
+                        const double t = xs[i * d + c] - xj[c];
+                        r2 += t * t;
+                    }
+                const double k = sqrt(r2) * kSqrt5;
+                v = amp * ((1.0 + k + k * k / 3.0) * exp(-k));
+            }
+            Lp[cidx(i, j)] = v;
+        }
+    }
+    __syncthreads();
+
+    // ---- 2. Cholesky, one barrier per column
+    double logdet = 0.0, prev_rs = 0.0;
+    int fail = 0;
+    for (int j = 0; j < n; ++j) {
+        const double dj = Lp[cidx(j, j)];
+        if (!(dj > 0.0) || !isfinite(dj)) { fail = j + 1; break; }  // uniform: every thread reads dj
+        const double rs = sqrt(dj);
+        logdet += log(rs);
+        const double inv = 1.0 / dj;
+        if (j > 0) {  // finalise column j-1 (not read by this step's update)
+            const int c0 = cidx(j - 1, j - 1);
+            for (int e = tid; e < n - j + 1; e += kFitThreads) Lp[c0 + e] = e == 0 ? prev_rs : Lp[c0 + e] / prev_rs;
+        }
+        const int cj = cidx(j, j);
+        for (int k = j + 1 + wave; k < n; k += kFitWaves) {
+            const double lkj = Lp[cj + (k - j)] * inv;
+            const int ck = cidx(k, k);
+            for (int i = k + lane; i < n; i += 64) Lp[ck + (i - k)] -= Lp[cj + (i - j)] * lkj;
+        }
+        prev_rs = rs;
+        __syncthreads();
+    }
+    if (fail) {  // sklearn: LinAlgError -> (-inf, zeros)
+        if (tid == 0) { a.lml[b] = -INFINITY; a.info[b] = fail; }
+        for (int c = tid; c < d + 2; c += kFitThreads) a.grad[(long long)b * (d + 2) + c] = 0.0;
+        return;
+    }
+    if (tid == 0) Lp[cidx(n - 1, n - 1)] = prev_rs;
+    __syncthreads();
+    if (a.stop == 2) return;
+
+    // ---- 3. L^-1 by columns: thread c forward-substitutes e_c.  Row i of L is read
+    // wave-uniformly (scalar loads); the solution column is the thread's own
+    // (LDS in the LDS variant).  Entries above the diagonal are never stored or read.
+    if (kLds) {
+        for (int i = wave; i < n; i += kFitWaves)
+            for (int j = lane; j <= i; j += 64) Lg[ridx(i, j)] = fsm[cidx(i, j)];
+        __syncthreads();
+    }
+    auto lrow = [&](int i, int k) -> double { return kLds ? Lg[ridx(i, k)] : Lg[cidx(i, k)]; };
+    auto lv = [&](int m, int j) -> double { return kLds ? fsm[ridx(m, j)] : Linv_g[m * n + j]; };
+    auto lv_set = [&](int m, int j, double v) {
+        if (kLds) fsm[ridx(m, j)] = v;
+        else Linv_g[m * n + j] = v;
+    };
+    if (kLds) {
+        // n <= 200 < 256: row i of L is held across the wave (lane l: L_i,l+64t, t < 4)
+        // and read with readlane (k is wave-uniform); row i+1 is loaded while row i
+        // is consumed, so the loop sees no global latency.
+        const int c = wave * 64 + lane;
+        const int cr = c < n ? c : n - 1;  // lanes past n read a valid column, store nothing
+        const int c0 = wave * 64;
+        if (c0 < n) {
+            auto load_row = [&](int i, double (&r)[4]) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int k = 64 * t + lane;
+                    r[t] = (i < n && k <= i) ? Lg[ridx(i, k)] : 0.0;
+                }
+            };
+            double cur[4], nxt[4];
+            load_row(c0, cur);
+            for (int i = c0; i < n; ++i) {
+                load_row(i + 1, nxt);
+                double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int kb = 64 * t;
+                    const int k0 = max(c0, kb), k1 = min(i, kb + 64);
+                    int k = k0;
+                    // batches of 8: all LDS loads issued before the FMAs (the stores of
+                    // earlier rows would otherwise pin every load behind the previous FMA)
+                    for (; k + 7 < k1; k += 8) {
+                        double v[8];
+                        int r = ridx(k, cr);
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) {
+                            v[u] = fsm[r];
+                            r += k + u + 1;
+                        }
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) {
+                            const double l = readlane_f64(cur[t], k + u - kb);
+                            if (u & 1) s1 += k + u >= cr ? l * v[u] : 0.0;
+                            else s0 += k + u >= cr ? l * v[u] : 0.0;
+                        }
+                    }
+                    for (; k < k1; ++k) s0 += k >= cr ? readlane_f64(cur[t], k - kb) * fsm[ridx(k, cr)] : 0.0;
+                }
+                double lii = 0.0;
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    if ((i >> 6) == t) lii = readlane_f64(cur[t], i & 63);
+                const double x = i == cr ? 1.0 / lii : -(s0 + s1) / lii;
+                if (c < n && i >= c) fsm[ridx(i, c)] = x;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) cur[t] = nxt[t];
+            }
+        }
+    } else {
+        for (int c0 = wave * 64; c0 < n; c0 += kFitThreads) {
+            const int c = c0 + lane;
+            const int cr = c < n ? c : n - 1;
+            for (int i = c0; i < n; ++i) {
+                double s0 = 0.0;
+                for (int k = c0; k < i; ++k) s0 += k >= cr ? lrow(i, k) * lv(k, cr) : 0.0;
+                const double lii = lrow(i, i);
+                const double x = i == cr ? 1.0 / lii : -s0 / lii;
+                if (c < n && i >= c) lv_set(i, c, x);
+            }
+        }
+    }
+    __syncthreads();
+    if (a.stop == 3) return;
+
+    // ---- 4. alpha = L^-T L^-1 y
+    for (int i = tid; i < n; i += kFitThreads) {
+        double s = 0.0;
+        for (int k = 0; k <= i; ++k) s += lv(i, k) * a.y[k];
+        z[i] = s;
+    }
+    __syncthreads();
+    for (int j = tid; j < n; j += kFitThreads) {
+        double s = 0.0;
+        for (int i = j; i < n; ++i) s += lv(i, j) * z[i];
+        alpha[j] = s;
+    }
+    __syncthreads();
+    if (a.stop == 4) return;
+
+    // ---- 5. pairs (i >= j): W_ij dK_ij / dtheta
+    double g[DP + 2];
+#pragma unroll
+    for (int c = 0; c < DP + 2; ++c) g[c] = 0.0;
+    for (int i = wave; i < n; i += kFitWaves) {
+        const double ai = alpha[i];
+        double xi[DP];
+#pragma unroll
+        for (int c = 0; c < DP; ++c) xi[c] = c < d ? a.X[i * d + c] : 0.0;
+        for (int j = lane; j <= i; j += 64) {
+            double k0 = 0.0, k1 = 0.0;
+            int m = i;
+            if (kLds) {
+                int r = ridx(i, 0);  // start of row m (packed row-major), advanced by m + 1
+                for (; m + 1 < n; m += 2) {
+                    k0 += fsm[r + i] * fsm[r + j];
+                    r += m + 1;
+                    k1 += fsm[r + i] * fsm[r + j];
+                    r += m + 2;
+                }
+                if (m < n) k0 += fsm[r + i] * fsm[r + j];
+            } else {
+                for (; m < n; ++m) k0 += lv(m, i) * lv(m, j);
+            }
+            const double kinv = k0 + k1;
+            const double W = (ai * alpha[j] - kinv) * (i == j ? 1.0 : 2.0);
+            // Matern gradient (kernels.py:1747-1767): D = (x_i - x_j)^2 / ls^2
+            double D[DP], r2 = 0.0;
+#pragma unroll
+            for (int c = 0; c < DP; ++c) {
+                if (c < d) {
+                    const double t = xi[c] - a.X[j * d + c];
+                    D[c] = t * t / (ls[c] * ls[c]);
+                    r2 += D[c];
+                } else {
+                    D[c] = 0.0;
+                }
+            }
+            const double s = sqrt(5.0 * r2);
+            const double e = exp(-s);
+            const double Mij = i == j ? 1.0 : (1.0 + s + s * s / 3.0) * e;
+            g[0] += W * (amp * Mij);
+            const double f = W * amp * (5.0 / 3.0) * (s + 1.0) * e;
+#pragma unroll
+            for (int c = 0; c < DP; ++c) g[1 + c] += f * D[c];
+            if (i == j) g[DP + 1] += W * noise;
+        }
+    }
+
+    // ---- 6. fixed-order reduction: lanes (butterfly) -> waves (LDS, in order)
+    __syncthreads();  // the pair pass is done with the LDS copy of L^-1
+    double* red = fsm;  // [kFitWaves][DP + 2]
+#pragma unroll
+    for (int c = 0; c < DP + 2; ++c) {
+        const double v = wave_sum_bcast(g[c]);
+        if (lane == 0) red[wave * (DP + 2) + c] = v;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double ya = 0.0;
+        for (int i = 0; i < n; ++i) ya += a.y[i] * alpha[i];
+        a.lml[b] = -0.5 * ya - logdet - 0.5 * n * kLog2Pi;
+        a.info[b] = 0;
+        double* out = a.grad + (long long)b * (d + 2);
+        for (int c = 0; c < d + 2; ++c) {
+            const int src = c == 0 ? 0 : (c == d + 1 ? DP + 1 : c);
+            double s = 0.0;
+            for (int w = 0; w < kFitWaves; ++w) s += red[w * (DP + 2) + src];
+            out[c] = 0.5 * s;
+        }
+    }
+}
+
+inline int fit_dp(int d) {
+    if (d <= 4) return 4;
+    if (d <= 8) return 8;
+    if (d <= 16) return 16;
+    if (d <= 32) return 32;
+    return -1;
+}
+
+template <bool kLds, int DP>
+int launch_lml(const LmlArgs& a, int B, hipStream_t s) {
+    auto kern = lml_grad_kernel<kLds, DP>;
+    const size_t lds = kLds ? (size_t)fit_tri(a.n) * sizeof(double) : (size_t)kFitWaves * (DP + 2) * sizeof(double);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(B), dim3(kFitThreads), lds, s, a);
+    MPO_LAUNCH_CHECK();
+    return MPO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t mpo_gp_lml_ws_bytes(int n, int d, int batch) {
+    if (n <= 0 || n > kFitMaxN || fit_dp(d) < 0 || batch <= 0) return 0;
+    return (size_t)fit_ws_doubles(n, d, n <= kFitLdsMaxN) * sizeof(double) * batch + 256;
+}
+
+int mpo_gp_lml_grad(const double* X, const double* y_norm, int n, int d, const double* theta, int batch,
+                    double* lml, double* grad, int32_t* info, void* ws, size_t ws_bytes, void* stream) {
+    MPO_GUARD_BEGIN
+    MPO_CHECK_ARG(X && y_norm && theta && lml && grad && info && ws, "mpo_gp_lml_grad: null pointer");
+    MPO_CHECK_ARG(n > 0 && d > 0 && batch > 0, "mpo_gp_lml_grad: bad shape n=%d d=%d batch=%d", n, d, batch);
+    const int dp = fit_dp(d);
+    if (dp < 0 || n > kFitMaxN) {
+        mpo::set_error("mpo_gp_lml_grad: n=%d d=%d outside n<=%d, d<=32", n, d, kFitMaxN);
+        return MPO_ENOTSUP;
+    }
+    MPO_CHECK_ARG(ws_bytes >= mpo_gp_lml_ws_bytes(n, d, batch), "mpo_gp_lml_grad: workspace too small (%zu < %zu)",
+                  ws_bytes, mpo_gp_lml_ws_bytes(n, d, batch));
+    const bool use_lds = n <= kFitLdsMaxN;
+    LmlArgs a{X, y_norm, n, d, theta, lml, grad, info,
+              reinterpret_cast<double*>(mpo::align_up(reinterpret_cast<uintptr_t>(ws), 256)),
+              fit_ws_doubles(n, d, use_lds), 0};
+    if (const char* e = getenv("MPO_FIT_DEBUG")) a.stop = atoi(e);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (use_lds) {
+        switch (dp) {
+            case 4: return launch_lml<true, 4>(a, batch, s);
+            case 8: return launch_lml<true, 8>(a, batch, s);
+            case 16: return launch_lml<true, 16>(a, batch, s);
+            default: return launch_lml<true, 32>(a, batch, s);
+        }
+    }
+    switch (dp) {
+        case 4: return launch_lml<false, 4>(a, batch, s);
+        case 8: return launch_lml<false, 8>(a, batch, s);
+        case 16: return launch_lml<false, 16>(a, batch, s);
+        default: return launch_lml<false, 32>(a, batch, s);
+    }
+    MPO_GUARD_END
+}
+
+}  // extern "C"

@@ -18,10 +18,11 @@ is un-vendored and unpinned; its published ``Optimizer`` algorithm is restated:
 
 MI355X mapping: the candidate scoring (posterior + EI/PI/LCB + top-k over the
 candidate batch) runs in ``libmpo.so`` on the GPU (:class:`~mpi_opt_amd.gp.DeviceGP`),
-together with the GP factorisation.  The LML hyper-parameter search (sklearn's
-L-BFGS-B on ~15 parameters) and the 5 x 20-iteration polish of single points stay
-on the host -- they are the reference's host-side control flow, not the
-per-candidate hot path (SURVEY §8f rank 1 moves the LML fit on device next).
+together with the GP factorisation, and so does the objective of the GP
+hyper-parameter refit (:mod:`~mpi_opt_amd.gp_fit`: LML + gradient, all L-BFGS-B
+restarts batched into one launch per iteration).  The L-BFGS-B control flow itself
+and the 5 x 20-iteration polish of single points stay on the host: they are the
+reference's host-side control flow, not per-candidate work.
 """
 from __future__ import annotations
 
@@ -32,29 +33,20 @@ import numpy as np
 from scipy.optimize import fmin_l_bfgs_b
 from scipy.stats import norm
 
+from .gp_fit import fit_lml
 from .space import Space, check_random_state
 
 SQRT5 = math.sqrt(5.0)
 
 
 # --------------------------------------------------------------------------
-# GP hyper-parameter fit (host, sklearn -- the arithmetic base skopt subclasses)
+# GP hyper-parameter fit (device LML objective, sklearn's restart/L-BFGS-B loop)
 # --------------------------------------------------------------------------
-def fit_gp_hyperparameters(Xt, y, random_state=None, n_restarts_optimizer=2):
+def fit_gp_hyperparameters(Xt, y, random_state=None, n_restarts_optimizer=2, device=None):
     """skopt's GP fit: sklearn GaussianProcessRegressor with the cook_estimator
-    kernel + WhiteKernel, normalize_y.  Returns (amp, length_scale, noise)."""
-    from sklearn.gaussian_process import GaussianProcessRegressor
-    from sklearn.gaussian_process.kernels import ConstantKernel, Matern, WhiteKernel
-
-    D = Xt.shape[1]
-    kern = ConstantKernel(1.0, (0.01, 1000.0)) * Matern(
-        length_scale=np.ones(D), length_scale_bounds=[(0.01, 100)] * D, nu=2.5) + WhiteKernel()
-    gpr = GaussianProcessRegressor(kernel=kern, normalize_y=True, n_restarts_optimizer=n_restarts_optimizer,
-                                   random_state=random_state)
-    gpr.fit(Xt, y)
-    p = gpr.kernel_.get_params()
-    return float(p["k1__k1__constant_value"]), np.atleast_1d(p["k1__k2__length_scale"]).astype(float), \
-        float(p["k2__noise_level"])
+    kernel + WhiteKernel, normalize_y, L-BFGS-B restarts -- the objective
+    (LML + gradient) evaluated by ``mpo_gp_lml_grad``.  Returns (amp, length_scale, noise)."""
+    return fit_lml(Xt, y, random_state=random_state, n_restarts_optimizer=n_restarts_optimizer, device=device)
 
 
 class GPModel:
@@ -151,7 +143,7 @@ class Optimizer:
     def __init__(self, dimensions, base_estimator="gp", n_random_starts=None, n_initial_points=10,
                  initial_point_generator="random", acq_func="gp_hedge", acq_optimizer="auto",
                  random_state=None, model_queue_size=None, acq_func_kwargs=None, acq_optimizer_kwargs=None,
-                 device=None):
+                 device=None, _gp_seed=None):
         self.rng = check_random_state(random_state)
         self.space = Space(dimensions)
         if n_random_starts is not None:
@@ -161,6 +153,10 @@ class Optimizer:
         if base_estimator not in ("gp", "dummy"):
             raise ValueError(f"base_estimator {base_estimator!r}: this build supports 'gp' and 'dummy'")
         self.base_estimator_ = base_estimator
+        # skopt cooks the estimator once, with random_state=rng.randint(...); a copy()
+        # receives the cooked estimator (no draw), and every refit clones it, so the
+        # GP restarts draw from the same seed at every fit.
+        self._gp_seed = self.rng.randint(0, np.iinfo(np.int32).max) if _gp_seed is None else _gp_seed
         if acq_func not in ("gp_hedge", "EI", "PI", "LCB"):
             raise ValueError(f"acq_func {acq_func!r} not supported")
         self.acq_func = acq_func
@@ -193,7 +189,7 @@ class Optimizer:
                         initial_point_generator=self._initial_point_generator, acq_func=self.acq_func,
                         acq_optimizer=self.acq_optimizer, acq_func_kwargs=self.acq_func_kwargs,
                         acq_optimizer_kwargs=self.acq_optimizer_kwargs, random_state=random_state,
-                        device=self.device)
+                        device=self.device, _gp_seed=self._gp_seed)
         opt._initial_samples = self._initial_samples
         if hasattr(self, "gains_"):
             opt.gains_ = np.copy(self.gains_)
@@ -256,8 +252,7 @@ class Optimizer:
     def _fit_and_propose(self):
         Xt = self.space.transform(self.Xi)
         y = np.asarray(self.yi, dtype=float)
-        seed = self.rng.randint(0, np.iinfo(np.int32).max)
-        amp, ls, noise = fit_gp_hyperparameters(Xt, y, random_state=seed)
+        amp, ls, noise = fit_gp_hyperparameters(Xt, y, random_state=self._gp_seed, device=self.device)
         est = GPModel(Xt, y, amp, ls, noise, device=self.device)
         if hasattr(self, "next_xs_") and self.acq_func == "gp_hedge":
             self.gains_ -= est.predict_mean(np.vstack(self.next_xs_))
