@@ -323,8 +323,12 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
 // 16-pixel MFMA tile is a 4x4 spatial patch, so a tap whose receptive field lies
 // entirely in the halo for that patch is skipped (wave-uniform branch) -- the
 // padded formulation otherwise multiplies zeros for (H1/H2)^2 of its work.
-// One workgroup = (member, sample, output rows [y0, y0+R)), R = 4 or 8;
-// K loop = taps (one LDS weight slice of F4 rows per tap, double-buffered).
+// The halo is virtual in the LDS too: only the dz2 rows the chunk reads are
+// staged (unpadded, [rows][H2][Fp]); a lane whose tap pixel falls in the halo
+// reads a zero block instead.  (A padded image is up to 5x larger at k=10 and
+// capped the chunk at 4 rows -- 5 tiles on 4 waves.)
+// One workgroup = (member, sample, output rows [y0, y0+R)), R = 4*floor(16/CT)
+// (<= 16 tiles of 4x4, at most 4 per wave); K loop = (tap, 16-channel block).
 // ============================================================================
 template <int NT>
 __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvItem* __restrict__ items) {
@@ -333,36 +337,33 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
     const Member& mb = a.mem[it.member];
     const int k = mb.k, F = mb.F, H2 = mb.H2, Ho = mb.H1;
     const int pad = k - 1;
-    const int Wp = H2 + 2 * pad;
     const int F4 = (F + 3) & ~3;
     const int Fp = dgrad_fp(F);
     const int N = F;
     const int R = it.R, y0 = it.y0;
-    const int rows = R + k - 1;
+    const int gy_lo = max(0, y0 - pad), gy_hi = min(H2, y0 + R);   // dz2 rows read by this chunk
+    const int rows = gy_hi - gy_lo;
     const float* in = a.act + mb.dz2 + (long long)it.b * H2 * H2 * F;
     const float* W = a.act + mb.w2t;
     float* out = a.act + mb.dz1 + (long long)it.b * Ho * Ho * F;
     const float* relu_mask = a.act + mb.a1 + (long long)it.b * Ho * Ho * F;
 
-    float* img = smem;  // [rows][Wp][Fp], channels >= F zero (+16 floats of slack)
-    const int img_elems = rows * Wp * Fp + 16;
+    float* img = smem;  // [rows][H2][Fp], channels >= F zero; then a 64-float zero block
+    const int zoff = align4(rows * H2 * Fp);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: tile logic stays scalar
     const int krow = lane >> 4, kcol = lane & 15;
 
-    for (int e = tid; e < img_elems; e += 256) img[e] = 0.f;
+    for (int e = tid; e < zoff + 64; e += 256) img[e] = 0.f;
     __syncthreads();
-    for (int r = 0; r < rows && a.debug != 2; ++r) {
-        const int gy = y0 + r - pad;
-        if (gy < 0 || gy >= H2) continue;
-        stage_row(in + (long long)gy * H2 * F, img + (r * Wp + pad) * Fp, H2 * F, F, Fp, tid);
-    }
+    for (int r = 0; r < rows && a.debug != 2; ++r)
+        stage_row(in + (long long)(gy_lo + r) * H2 * F, img + r * H2 * Fp, H2 * F, F, Fp, tid);
 
     // ---- this wave's 4x4 tiles, their tap rectangles and the wave's union rectangle
     const int CT = (Ho + 3) >> 2;
     const int bands = (R + 3) >> 2;
     const int T = bands * CT;
-    int pb[4], kylo[4], kyhi[4], kxlo[4], kxhi[4];
+    int py[4], px[4], kylo[4], kyhi[4], kxlo[4], kxhi[4];
     bool has[4];
     int uy0 = k, uy1 = 0, ux0 = k, ux1 = 0;
     const int dy = (lane & 15) >> 2, dx = lane & 3;
@@ -381,8 +382,11 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
             uy0 = min(uy0, kylo[i]); uy1 = max(uy1, kyhi[i]);
             ux0 = min(ux0, kxlo[i]); ux1 = max(ux1, kxhi[i]);
         }
+        // tap (ky, kx) reads dz2 pixel (y + ky - pad, x + kx - pad): LDS row py + ky, column px + kx
         const int y = ty0 + dy, x = tx0 + dx;
-        pb[i] = (y < ty1 && x < tx1) ? ((y - y0) * Wp + x) * Fp : 0;
+        const bool pix = y < ty1 && x < tx1;
+        py[i] = pix ? y - pad - gy_lo : -(1 << 20);   // an invalid output pixel never reads the image
+        px[i] = x - pad;
     }
     f32x4 acc[4][NT];
 #pragma unroll
@@ -409,17 +413,24 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
     auto advance = [&](int& ky, int& kx, int& cb) {
         if (++cb == CB) { cb = 0; if (++kx == ux1) { kx = ux0; ++ky; } }
     };
-    auto compute = [&](int ky, int kx, int cb, const float (&bw)[4][NT]) {
+    // A fragments of a group: 4 k-steps x 4 tiles, read from the LDS image one group
+    // ahead of their MFMAs (like the B fragments), so no MFMA waits on its own reads
+    auto readA = [&](int ky, int kx, int cb, float (&av)[4][4]) {
+        const int coff = cb * 16 + krow;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int ry = py[i] + ky, cx = px[i] + kx;
+            const int base = ((unsigned)ry < (unsigned)rows && (unsigned)cx < (unsigned)H2)
+                                 ? (ry * H2 + cx) * Fp + coff : zoff + krow;   // halo -> zero block
+#pragma unroll
+            for (int u = 0; u < 4; ++u) av[u][i] = img[base + u * 4];
+        }
+    };
+    auto compute = [&](int ky, int kx, int cb, const float (&av)[4][4], const float (&bw)[4][NT]) {
         bool live[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             live[i] = has[i] && ky >= kylo[i] && ky < kyhi[i] && kx >= kxlo[i] && kx < kxhi[i];
-        const int toff = (ky * Wp + kx) * Fp + cb * 16 + krow;
-        float av[4][4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) av[u][i] = img[pb[i] + toff + u * 4];
         const int nu = min(4, (F4 - cb * 16) >> 2);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -433,21 +444,32 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
             }
         }
     };
-    float b0[4][NT], b1[4][NT];
+    float b0[4][NT], b1[4][NT], a0[4][4], a1[4][4];
     int cky = uy0, ckx = ux0, ccb = 0;   // group g
     int nky = uy0, nkx = ux0, ncb = 0;   // group g + 1
     if (ngroups) {
         load_group(cky, ckx, ccb, b0);
+        readA(cky, ckx, ccb, a0);
         advance(nky, nkx, ncb);
     }
     for (int g = 0; g < ngroups; g += 2) {
-        if (g + 1 < ngroups) load_group(nky, nkx, ncb, b1);
-        compute(cky, ckx, ccb, b0);
+        if (g + 1 < ngroups) {
+            load_group(nky, nkx, ncb, b1);
+            readA(nky, nkx, ncb, a1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        compute(cky, ckx, ccb, a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
         if (g + 1 >= ngroups) break;
         cky = nky; ckx = nkx; ccb = ncb;
         advance(nky, nkx, ncb);
-        if (g + 2 < ngroups) load_group(nky, nkx, ncb, b0);
-        compute(cky, ckx, ccb, b1);
+        if (g + 2 < ngroups) {
+            load_group(nky, nkx, ncb, b0);
+            readA(nky, nkx, ncb, a0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        compute(cky, ckx, ccb, a1, b1);
+        __builtin_amdgcn_sched_barrier(0);
         cky = nky; ckx = nkx; ccb = ncb;
         advance(nky, nkx, ncb);
     }
@@ -1122,10 +1144,9 @@ size_t conv_lds_bytes(int rows, int Wp, int Cin, int K, int nt) {
     return (size_t)(align4(rows * Wp * Fp) + ((K + 15) & ~15) + kKoffSlack) * sizeof(float);
 }
 
-size_t dgrad_lds_bytes(int R, int k, int F, int nt) {
-    (void)nt;
-    const int Wp = kImg;  // H2 + 2(k-1) == 28
-    return (size_t)align4((R + k - 1) * Wp * dgrad_fp(F) + 16) * sizeof(float);
+size_t dgrad_lds_bytes(int R, int k, int F, int H2) {
+    const int rows = std::min(H2, R + k - 1);   // dz2 rows of the widest chunk (unpadded)
+    return (size_t)(align4(rows * H2 * dgrad_fp(F)) + 64) * sizeof(float);
 }
 
 size_t wg_lds_bytes(int k, int Hin, int Cin, int Ho, int F) {
@@ -1202,7 +1223,7 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         m.pend = po;
         // wgrad sample groups (partial slabs reduced in a fixed order): ~10
         // samples per conv2 block, ~4 per conv1 block (its GEMM is tiny)
-        const int spg2 = std::max(1, env_int("MPO_WG_SPG2", 10)), spg1 = std::max(1, env_int("MPO_WG_SPG1", 4));
+        const int spg2 = std::max(1, env_int("MPO_WG_SPG2", 4)), spg1 = std::max(1, env_int("MPO_WG_SPG1", 4));
         m.g2 = std::max(1, std::min(B, (B + spg2 - 1) / spg2));
         m.g1 = std::max(1, std::min(B, (B + spg1 - 1) / spg1));
         m.a1 = aalloc((long long)B * m.H1 * m.H1 * F);
@@ -1236,12 +1257,14 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         const int k = m.k, F = m.F, nt = m.nt;
         const int R1 = choose_rows(m.H1, [&](int R) { return conv_lds_bytes(R + k - 1, kImg, 1, k * k, nt); }, kc1, kc2);
         const int R2 = choose_rows(m.H2, [&](int R) { return conv_lds_bytes(R + k - 1, m.H1, F, k * k * F, nt); }, kc1, kc2);
-        // dgrad: 4x4-pixel tiles in bands of 4 rows; 8-row chunks unless only 4 fit 2 blocks/CU
+        // dgrad: 4x4-pixel tiles in bands of 4 rows, <= 16 tiles (4 per wave) per chunk:
+        // R = 4 * floor(16 / CT); 4-row bands fewer if the LDS budget asks for it
         const size_t dgb = (size_t)kdg << 10;
-        const int Rd = (dgrad_lds_bytes(8, k, F, nt) <= dgb || dgrad_lds_bytes(4, k, F, nt) > dgb) ? 8 : 4;
+        int Rd = 4 * std::max(1, 16 / ((m.H1 + 3) / 4));
+        while (Rd > 4 && dgrad_lds_bytes(Rd, k, F, m.H2) > dgb) Rd -= 4;
         const size_t l1 = conv_lds_bytes(R1 + k - 1, kImg, 1, k * k, nt);
         const size_t l2 = conv_lds_bytes(R2 + k - 1, m.H1, F, k * k * F, nt);
-        const size_t ld = dgrad_lds_bytes(Rd, k, F, nt);
+        const size_t ld = dgrad_lds_bytes(Rd, k, F, m.H2);
         L1[i] = l1; L2[i] = l2; LD[i] = ld;
         for (int b = 0; b < B; ++b) {
             for (int y = 0; y < m.H1; y += R1) P.conv1.push_back({i, b, y, std::min(R1, m.H1 - y)});
