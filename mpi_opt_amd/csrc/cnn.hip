@@ -530,8 +530,8 @@ __host__ __device__ constexpr inline int round64(int x) { return (x + 63) & ~63;
 // of k-step s+1 are issued before the MFMAs of k-step s.
 template <int MT, int NT>
 __device__ __forceinline__ void wgrad_row(const float* __restrict__ img, const float* __restrict__ dl,
-                                          const int (&abase)[kWgMaxMT], const int (&astep)[kWgMaxMT], int dstride,
-                                          int nk4, int krow, int kcol, f32x4 (&acc)[kWgMaxMT][NT]) {
+                                          const int (&abase)[MT], const int (&astep)[MT], int dstride,
+                                          int nk4, int krow, int kcol, f32x4 (&acc)[MT][NT]) {
     float a0[MT], a1[MT], b0[NT], b1[NT];
     auto rd = [&](int s, float (&av)[MT], float (&bv)[NT]) {
         const int x = 4 * s + krow;
@@ -560,7 +560,11 @@ __device__ __forceinline__ void wgrad_row(const float* __restrict__ img, const f
     }
 }
 
-template <int OP, int NT>
+// MT = the m-tiles every wave of this launch runs (the plan buckets m-groups by
+// ceil(tiles / 8)): a single loop body keeps the kernel at <= 128 VGPRs, i.e. two
+// 8-wave workgroups per CU.  A wave with fewer real tiles multiplies the constant
+// zero row for the rest (never written back).
+template <int OP, int NT, int MT>
 __global__ __launch_bounds__(kWgThreads) void conv_wgrad_kernel(StepArgs a, const WgItem* __restrict__ items) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const WgItem it = items[blockIdx.x];
@@ -601,9 +605,9 @@ __global__ __launch_bounds__(kWgThreads) void conv_wgrad_kernel(StepArgs a, cons
 
     // per lane, per tile: A row (ky, kx*Cin + c) -> ring address ring_row(y+ky)*rowS + col + x*Cin;
     // rows past Kw read the constant 0 (padding) or 1 (the bias row) with x stride 0
-    int tky[kWgMaxMT], tcol[kWgMaxMT], astep[kWgMaxMT];
+    int tky[MT], tcol[MT], astep[MT];
 #pragma unroll
-    for (int i = 0; i < kWgMaxMT; ++i) {
+    for (int i = 0; i < MT; ++i) {
         const int m = (t0 + wave + kWgWaves * i) * 16 + (lane & 15);
         int ky = 0, col = m == Kw ? kOne : kZero, st = 0;
         if (m < Kw) {
@@ -616,9 +620,9 @@ __global__ __launch_bounds__(kWgThreads) void conv_wgrad_kernel(StepArgs a, cons
         tcol[i] = col;
         astep[i] = st;
     }
-    f32x4 acc[kWgMaxMT][NT];
+    f32x4 acc[MT][NT];
 #pragma unroll
-    for (int i = 0; i < kWgMaxMT; ++i)
+    for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -659,20 +663,15 @@ __global__ __launch_bounds__(kWgThreads) void conv_wgrad_kernel(StepArgs a, cons
                 dma(inb + (y + k + 1) * rowf, rowf, ring + sl * rowS);
                 dma(dob + (y + 2) * dcnt, dcnt, dl + ((y + 2) % 3) * dS);
             }
-            int abase[kWgMaxMT];
+            int abase[MT];
 #pragma unroll
-            for (int i = 0; i < kWgMaxMT; ++i) {
+            for (int i = 0; i < MT; ++i) {
                 int sl = slot0 + tky[i];
                 sl = sl >= RS ? sl - RS : sl;
                 abase[i] = astep[i] ? sl * rowS + tcol[i] : tcol[i];
             }
             const float* dcur = dl + (y % 3) * dS;
-            if (a.debug != 1) {
-                if (mine == 4) wgrad_row<4, NT>(ring, dcur, abase, astep, N, nk4, krow, kcol, acc);
-                else if (mine == 3) wgrad_row<3, NT>(ring, dcur, abase, astep, N, nk4, krow, kcol, acc);
-                else if (mine == 2) wgrad_row<2, NT>(ring, dcur, abase, astep, N, nk4, krow, kcol, acc);
-                else if (mine == 1) wgrad_row<1, NT>(ring, dcur, abase, astep, N, nk4, krow, kcol, acc);
-            }
+            if (a.debug != 1 && mine > 0) wgrad_row<MT, NT>(ring, dcur, abase, astep, N, nk4, krow, kcol, acc);
             slot0 = slot0 + 1 == RS ? 0 : slot0 + 1;
             // retire the DMA issued one row ago (row y+1's data); this row's stays in flight
             if (ahead) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
@@ -682,7 +681,7 @@ __global__ __launch_bounds__(kWgThreads) void conv_wgrad_kernel(StepArgs a, cons
     }
     float* part = a.act + part_off + (long long)it.group * (Kw + 1) * N;
 #pragma unroll
-    for (int i = 0; i < kWgMaxMT; ++i) {
+    for (int i = 0; i < MT; ++i) {
         if (i >= mine) break;
         const int mt = t0 + wave + kWgWaves * i;
 #pragma unroll
@@ -1065,7 +1064,11 @@ __global__ void kfold_gather_kernel(const float* __restrict__ X, const int* __re
 struct Seg {
     int nt, begin, end;
     size_t lds;
+    int sub;   // wgrad: m-tiles per wave (WgItem::R); 0 for the other ops
 };
+inline int item_sub(const WgItem& x) { return x.R; }
+template <class T>
+inline int item_sub(const T&) { return 0; }
 struct Bucketed {
     std::vector<Seg> segs;
 };
@@ -1174,12 +1177,12 @@ int lds_class(size_t lds) { return (int)std::min<size_t>(8, ((size_t)160 << 10) 
 
 template <class T>
 void bucket_segs(std::vector<T>& items, Bucketed& bk, const std::vector<Member>& mem, const std::vector<size_t>& lds) {
-    auto key = [&](const T& x) { return mem[x.member].nt * 16 + (8 - lds_class(lds[x.member])); };
+    auto key = [&](const T& x) { return (mem[x.member].nt * 8 + item_sub(x)) * 16 + (8 - lds_class(lds[x.member])); };
     std::stable_sort(items.begin(), items.end(), [&](const T& x, const T& y) { return key(x) < key(y); });
     bk.segs.clear();
     for (int i = 0; i < (int)items.size();) {
         const int kk = key(items[i]);
-        Seg sg{mem[items[i].member].nt, i, i, 0};
+        Seg sg{mem[items[i].member].nt, i, i, 0, item_sub(items[i])};
         while (i < (int)items.size() && key(items[i]) == kk) {
             sg.lds = std::max(sg.lds, lds[items[i].member]);
             ++i;
@@ -1187,6 +1190,13 @@ void bucket_segs(std::vector<T>& items, Bucketed& bk, const std::vector<Member>&
         sg.end = i;
         bk.segs.push_back(sg);
     }
+}
+
+// m-tiles per wave of wgrad m-group mg for a GEMM of Kw + 1 rows (bias row included)
+int wg_mt(int Kw, int mg) {
+    const int mtiles = (Kw + 1 + 15) / 16;
+    const int tiles = std::min(kWgRows / 16, mtiles - mg * (kWgRows / 16));
+    return std::max(1, std::min(kWgMaxMT, (tiles + kWgWaves - 1) / kWgWaves));
 }
 
 int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
@@ -1280,11 +1290,11 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         const int K2 = k * k * F, K1w = k * k;
         for (int g = 0; g < m.g2; ++g) {
             const int b0 = (int)((long long)B * g / m.g2), b1 = (int)((long long)B * (g + 1) / m.g2);
-            for (int mg = 0; mg * kWgRows <= K2; ++mg) P.wg2.push_back({i, mg, b0, b1, g, 0});
+            for (int mg = 0; mg * kWgRows <= K2; ++mg) P.wg2.push_back({i, mg, b0, b1, g, wg_mt(K2, mg)});
         }
         for (int g = 0; g < m.g1; ++g) {
             const int b0 = (int)((long long)B * g / m.g1), b1 = (int)((long long)B * (g + 1) / m.g1);
-            for (int mg = 0; mg * kWgRows <= K1w; ++mg) P.wg1.push_back({i, mg, b0, b1, g, 0});
+            for (int mg = 0; mg * kWgRows <= K1w; ++mg) P.wg1.push_back({i, mg, b0, b1, g, wg_mt(K1w, mg)});
         }
         P.lds_wg_max = std::max({P.lds_wg_max, lw2, lw1});
         auto tiles = [&](std::vector<GemmItem>& v, int M, int N) {
@@ -1373,9 +1383,10 @@ hipError_t launch_dgrad_nt(const StepArgs& a, const ConvItem* items, int count, 
 }
 
 template <int OP, int NT>
-hipError_t launch_wg_nt(const StepArgs& a, const WgItem* items, int count, size_t lds, hipStream_t s) {
+hipError_t launch_wg_nt(const StepArgs& a, const WgItem* items, int count, size_t lds, int mt, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    auto kern = conv_wgrad_kernel<OP, NT>;
+    auto kern = mt == 1 ? conv_wgrad_kernel<OP, NT, 1> : mt == 2 ? conv_wgrad_kernel<OP, NT, 2>
+              : mt == 3 ? conv_wgrad_kernel<OP, NT, 3> : conv_wgrad_kernel<OP, NT, 4>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(count), dim3(kWgThreads), lds, s, a, items);
     return hipGetLastError();
@@ -1385,7 +1396,7 @@ template <class Fn>
 hipError_t launch_segs(Plan& P, const Bucketed& bk, const char* name, hipStream_t s, Fn launch_nt) {
     for (const Seg& sg : bk.segs) {
         if (hipError_t e = launch_nt(sg)) return e;
-        P.timer.mark(std::string(name) + "/nt" + std::to_string(sg.nt) +
+        P.timer.mark(std::string(name) + "/nt" + std::to_string(sg.nt) + (sg.sub ? "/mt" + std::to_string(sg.sub) : "") +
                          (P.timer_detail ? "/occ" + std::to_string(lds_class(sg.lds)) + "/n" + std::to_string(sg.end - sg.begin) : ""),
                      s);
     }
@@ -1423,8 +1434,8 @@ hipError_t launch_dgrad(Plan& P, const StepArgs& a, hipStream_t s) {
 template <int OP>
 struct WgLaunch {
     template <int NT>
-    static hipError_t go(const StepArgs& a, const WgItem* items, int count, size_t lds, hipStream_t s) {
-        return launch_wg_nt<OP, NT>(a, items, count, lds, s);
+    static hipError_t go(const StepArgs& a, const WgItem* items, int count, size_t lds, int mt, hipStream_t s) {
+        return launch_wg_nt<OP, NT>(a, items, count, lds, mt, s);
     }
 };
 
@@ -1432,7 +1443,7 @@ template <int OP>
 hipError_t launch_wg(Plan& P, const StepArgs& a, size_t table_off, const Bucketed& bk, hipStream_t s) {
     const WgItem* base = dev_table<WgItem>(P, table_off);
     return launch_segs(P, bk, OP == WG_CONV1 ? "conv1_wgrad" : "conv2_wgrad", s, [&](const Seg& sg) {
-        return MPO_NT_SWITCH(WgLaunch<OP>::template go, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, s);
+        return MPO_NT_SWITCH(WgLaunch<OP>::template go, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, sg.sub, s);
     });
 }
 
