@@ -363,14 +363,17 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
     const int CT = (Ho + 3) >> 2;
     const int bands = (R + 3) >> 2;
     const int T = bands * CT;
+    // contiguous tiles per wave (neighbours along a band share most live taps, so the
+    // wave's union tap rectangle wastes fewer groups than a round-robin spread)
+    const int per = (T + 3) >> 2;
     int py[4], px[4], kylo[4], kyhi[4], kxlo[4], kxhi[4];
     bool has[4];
     int uy0 = k, uy1 = 0, ux0 = k, ux1 = 0;
     const int dy = (lane & 15) >> 2, dx = lane & 3;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int ti = wave + 4 * i;
-        has[i] = ti < T;
+        const int ti = wave * per + i;
+        has[i] = i < per && ti < T;
         const int band = ti / CT, ct = ti - band * CT;
         const int ty0 = y0 + 4 * band, tx0 = 4 * ct;
         const int ty1 = min(ty0 + 4, y0 + R), tx1 = min(tx0 + 4, Ho);
@@ -478,7 +481,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         if (!has[i]) continue;
-        const int ti = wave + 4 * i;
+        const int ti = wave * per + i;
         const int band = ti / CT, ct = ti - band * CT;
         const int ty0 = y0 + 4 * band, tx0 = 4 * ct;
         const int ty1 = min(ty0 + 4, y0 + R), tx1 = min(tx0 + 4, Ho);
