@@ -62,6 +62,20 @@ def load_traffic(kernel, config_key):
         return None
 
 
+def load_population_pmc():
+    """rocprofv3 counters of the 320-member population step (committed summary,
+    scripts/pmc_train_summary.py): MFMA-busy fraction of the MFMA training kernels
+    (SQ_VALU_MFMA_BUSY_CYCLES over SIMD cycles, GUI-time weighted) and HBM bytes per
+    train batch.  None if absent."""
+    try:
+        e = json.load(open(os.path.join(ROOT, "profiles", "pmc_summary.json")))["population_step"]
+        return {"mfma_busy": e["mfma_busy"], "hbm_bytes_per_train_batch": e["hbm_bytes_per_train_step"],
+                "per_kernel_mfma_busy": {k: v["mfma_busy"] for k, v in e["per_kernel"].items()},
+                "source": e["source"]}
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def cpu_baseline_ei(n=200, d=10, sample=150_000):
     """skopt's literal K_inv einsum posterior + EI (the oracle restatement) timed on
     the host: single-threaded einsum, as skopt calls it."""
@@ -340,7 +354,8 @@ def bench_train(args, torch, dist, ws, rank, dev):
         "roofline": {"kernel": "population step (all conv/dense MFMA kernels)", "bound": "mfma",
                      "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None,
-                     "algorithmic_flops_per_step": flops},
+                     "algorithmic_flops_per_step": flops,
+                     "pmc": load_population_pmc() if n_trials == 64 else None},
         "_trials": trials,
     }
 
