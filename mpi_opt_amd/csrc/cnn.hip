@@ -713,8 +713,17 @@ __global__ void wgrad_reduce_kernel(StepArgs a, const MItem* __restrict__ items,
     float* gb = a.grads + (conv ? mb.b2 : mb.b1);
     for (long long i = (long long)blockIdx.x * per_block + threadIdx.x; i < S && i < (long long)(blockIdx.x + 1) * per_block;
          i += blockDim.x) {
+        // slabs summed in slab order; loads issued 8 at a time ahead of the adds
         float s = 0.f;
-        for (int q = 0; q < G; ++q) s += part[q * S + i];
+        int q = 0;
+        for (; q + 8 <= G; q += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = part[(q + u) * S + i];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += v[u];
+        }
+        for (; q < G; ++q) s += part[q * S + i];
         if (i < Sw) gw[i] = s; else gb[i - Sw] = s;
     }
 }
@@ -795,16 +804,23 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(StepArgs a, const MItem* 
     const unsigned char* am = reinterpret_cast<const unsigned char*>(a.act + mb.am) + (long long)b * K1;
     float* dz2 = a.act + mb.dz2 + (long long)b * H2 * H2 * F;
     const int n = H2 * H2 * F;
-    for (int e = threadIdx.x; e < n; e += blockDim.x) {
-        const int f = e % F, q = e / F;
-        const int x = q % H2, y = q / H2;
-        const int py = y / p, px = x / p;
+    // division-free walk over (y, x, f): each thread advances by blockDim.x elements
+    const float inv_p = 1.f / (float)p;   // floor((x + 0.5) / p) is exact for x < 64, p <= 13
+    const int step = blockDim.x, df = step % F, dq = step / F;
+    int f = threadIdx.x % F, q = threadIdx.x / F;
+    int x = q % H2, y = q / H2;
+    for (int e = threadIdx.x; e < n; e += step) {
+        const int py = (int)(((float)y + 0.5f) * inv_p), px = (int)(((float)x + 0.5f) * inv_p);
         float v = 0.f;
         if (py < s && px < s) {
             const int j = (py * s + px) * F + f;
             if (am[j] == (y - py * p) * p + (x - px * p)) v = dp[j];
         }
         dz2[e] = a2[e] > 0.f ? v : 0.f;
+        f += df;
+        x += dq;
+        if (f >= F) { f -= F; ++x; }
+        while (x >= H2) { x -= H2; ++y; }
     }
 }
 
