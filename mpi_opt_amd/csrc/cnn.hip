@@ -825,7 +825,8 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(StepArgs a, const MItem* 
 }
 
 // ============================================================================
-// Grouped dense GEMMs (MFMA f32 16x16x4), 64x64 tiles, 4 waves as 2x2 of 32x32.
+// Grouped dense GEMMs (MFMA f32 16x16x4), 64x64 tiles, 4 waves as 2x2 of 32x32;
+// K in chunks of 32, the next chunk's global loads in flight during the MFMAs.
 // ============================================================================
 template <int OP>
 struct DenseGeom {
@@ -876,7 +877,8 @@ __device__ __forceinline__ DenseGeom<OP> dense_geom(const StepArgs& a, const Mem
 
 template <int OP>
 __global__ __launch_bounds__(256) void dense_kernel(StepArgs a, const GemmItem* __restrict__ items) {
-    constexpr int BM = 64, BN = 64, BK = 16;
+    constexpr int BM = 64, BN = 64, BK = 32;
+    constexpr int EA = BM * BK / 256, EB = BN * BK / 256;   // staged elements per thread
     __shared__ float As[BK][BM + 1];
     __shared__ float Bs[BK][BN + 16];
     const GemmItem it = items[blockIdx.x];
@@ -890,21 +892,48 @@ __global__ __launch_bounds__(256) void dense_kernel(StepArgs a, const GemmItem* 
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < g.K; k0 += BK) {
-        __syncthreads();
-        for (int e = tid; e < BM * BK; e += 256) {
+    // (i, kk) / (j, kk) of this thread's staged elements: fixed for the whole K loop
+    auto a_ik = [&](int q, int& i, int& kk) {
+        const int e = tid + 256 * q;
+        if (g.sak == 1) { i = e / BK; kk = e % BK; } else { kk = e / BM; i = e % BM; }
+    };
+    auto b_jk = [&](int q, int& j, int& kk) {
+        const int e = tid + 256 * q;
+        if (g.sbj == 1) { kk = e / BN; j = e % BN; } else { j = e / BK; kk = e % BK; }
+    };
+    float ra[EA], rb[EB];
+    auto load = [&](int k0) {   // global -> registers (chunk k0), in flight during the MFMAs
+#pragma unroll
+        for (int q = 0; q < EA; ++q) {
             int i, kk;
-            if (g.sak == 1) { i = e / BK; kk = e % BK; } else { kk = e / BM; i = e % BM; }
+            a_ik(q, i, kk);
             const int gi = it.m0 + i, gk = k0 + kk;
-            As[kk][i] = (gi < g.M && gk < g.K) ? g.A[gi * g.sai + gk * g.sak] : 0.f;
+            ra[q] = (gi < g.M && gk < g.K) ? g.A[gi * g.sai + gk * g.sak] : 0.f;
         }
-        for (int e = tid; e < BN * BK; e += 256) {
+#pragma unroll
+        for (int q = 0; q < EB; ++q) {
             int j, kk;
-            if (g.sbj == 1) { kk = e / BN; j = e % BN; } else { j = e / BK; kk = e % BK; }
+            b_jk(q, j, kk);
             const int gj = it.n0 + j, gk = k0 + kk;
-            Bs[kk][j] = (gj < g.N && gk < g.K) ? g.Bm[gk * g.sbk + gj * g.sbj] : 0.f;
+            rb[q] = (gj < g.N && gk < g.K) ? g.Bm[gk * g.sbk + gj * g.sbj] : 0.f;
+        }
+    };
+    load(0);
+    for (int k0 = 0; k0 < g.K; k0 += BK) {
+#pragma unroll
+        for (int q = 0; q < EA; ++q) {
+            int i, kk;
+            a_ik(q, i, kk);
+            As[kk][i] = ra[q];
+        }
+#pragma unroll
+        for (int q = 0; q < EB; ++q) {
+            int j, kk;
+            b_jk(q, j, kk);
+            Bs[kk][j] = rb[q];
         }
         __syncthreads();
+        if (k0 + BK < g.K) load(k0 + BK);
 #pragma unroll
         for (int ks = 0; ks < BK; ks += 4) {
             float af[2], bf[2];
@@ -917,6 +946,7 @@ __global__ __launch_bounds__(256) void dense_kernel(StepArgs a, const GemmItem* 
 #pragma unroll
                 for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
         }
+        __syncthreads();
     }
     const unsigned base1 = drop_base(mb.seed, a.step, 1);
     const unsigned base0 = drop_base(mb.seed, a.step, 0);
