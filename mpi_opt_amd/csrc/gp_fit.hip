@@ -190,35 +190,69 @@ __global__ __launch_bounds__(kFitThreads) void lml_grad_kernel(LmlArgs a) {
         else Linv_g[m * n + j] = v;
     };
     if (kLds) {
-        // n <= 200 < 256: row i of L is held across the wave (lane l: L_i,l+64t, t < 4)
-        // and read with readlane (k is wave-uniform); row i+1 is loaded while row i
-        // is consumed, so the loop sees no global latency.
-        const int c = wave * 64 + lane;
-        const int cr = c < n ? c : n - 1;  // lanes past n read a valid column, store nothing
-        const int c0 = wave * 64;
-        if (c0 < n) {
-            auto load_row = [&](int i, double (&r)[4]) {
+        // Blocked in 64-row blocks (n <= 200: at most 4), the dtrtri scheme:
+        //  3a. every diagonal block is inverted at once, one wave per block, thread c
+        //      forward-substituting e_c inside its block (chains of <= 64 rows
+        //      instead of n);
+        //  3b. block row bi, from the top: T = L[bi][:bi] X[:bi][bj] (all 16 waves,
+        //      T written where X[bi][bj] goes), then X[bi][bj] = -inv(L[bi][bi]) T in
+        //      place (each wave owns whole columns, so its reads of T precede its
+        //      writes).
+        const int nblk = (n + 63) >> 6;
+        if (wave < nblk) {
+            // row i of the block's L is held across the wave (lane l: L_{i,c0+l}) and
+            // read with readlane (k is wave-uniform); row i+1 loads while i is used
+            const int c0 = wave * 64, ce = min(c0 + 64, n);
+            const int c = c0 + lane;
+            const int cr = c < ce ? c : ce - 1;  // lanes past the block read a valid column, store nothing
+            auto ld = [&](int i) -> double { return (i < ce && c <= i) ? Lg[ridx(i, c)] : 0.0; };
+            double cur = ld(c0);
+            for (int i = c0; i < ce; ++i) {
+                const double nxt = ld(i + 1);
+                double s0 = 0.0, s1 = 0.0;
+                int k = c0;
+                // batches of 8: all LDS loads issued before the FMAs
+                for (; k + 7 < i; k += 8) {
+                    double v[8];
+                    int r = ridx(k, cr);
 #pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int k = 64 * t + lane;
-                    r[t] = (i < n && k <= i) ? Lg[ridx(i, k)] : 0.0;
+                    for (int u = 0; u < 8; ++u) {
+                        v[u] = fsm[r];
+                        r += k + u + 1;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const double l = readlane_f64(cur, k + u - c0);
+                        if (u & 1) s1 += k + u >= cr ? l * v[u] : 0.0;
+                        else s0 += k + u >= cr ? l * v[u] : 0.0;
+                    }
                 }
-            };
-            double cur[4], nxt[4];
-            load_row(c0, cur);
-            for (int i = c0; i < n; ++i) {
-                load_row(i + 1, nxt);
+                for (; k < i; ++k) s0 += k >= cr ? readlane_f64(cur, k - c0) * fsm[ridx(k, cr)] : 0.0;
+                const double lii = readlane_f64(cur, i - c0);
+                const double x = i == cr ? 1.0 / lii : -(s0 + s1) / lii;
+                if (c < ce && i >= c) fsm[ridx(i, c)] = x;
+                cur = nxt;
+            }
+        }
+        __syncthreads();
+        for (int bi = 1; bi < nblk; ++bi) {
+            const int bi0 = bi * 64, bie = min(bi0 + 64, n), rows = bie - bi0;
+            // T_ic = sum_{k=c}^{bi0-1} L_ik X_kc: wave task (row i, column block bj),
+            // lane = column; L_i,k for k < bi0 held in registers (chunk q: k = 64q + lane)
+            for (int t = wave; t < rows * bi; t += kFitWaves) {
+                const int i = bi0 + t / bi, bj = t % bi;
+                const int c = bj * 64 + lane;
+                double lr[3];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) lr[q] = (q >= bj && q < bi) ? Lg[ridx(i, 64 * q + lane)] : 0.0;
                 double s0 = 0.0, s1 = 0.0;
 #pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int kb = 64 * t;
-                    const int k0 = max(c0, kb), k1 = min(i, kb + 64);
-                    int k = k0;
-                    // batches of 8: all LDS loads issued before the FMAs (the stores of
-                    // earlier rows would otherwise pin every load behind the previous FMA)
-                    for (; k + 7 < k1; k += 8) {
+                for (int q = 0; q < 3; ++q) {
+                    if (q < bj || q >= bi) continue;
+                    for (int kk = 0; kk < 64; kk += 8) {
+                        const int k = 64 * q + kk;
                         double v[8];
-                        int r = ridx(k, cr);
+                        int r = ridx(k, c);
 #pragma unroll
                         for (int u = 0; u < 8; ++u) {
                             v[u] = fsm[r];
@@ -226,22 +260,36 @@ __global__ __launch_bounds__(kFitThreads) void lml_grad_kernel(LmlArgs a) {
                         }
 #pragma unroll
                         for (int u = 0; u < 8; ++u) {
-                            const double l = readlane_f64(cur[t], k + u - kb);
-                            if (u & 1) s1 += k + u >= cr ? l * v[u] : 0.0;
-                            else s0 += k + u >= cr ? l * v[u] : 0.0;
+                            const double l = readlane_f64(lr[q], kk + u);
+                            if (u & 1) s1 += k + u >= c ? l * v[u] : 0.0;
+                            else s0 += k + u >= c ? l * v[u] : 0.0;
                         }
                     }
-                    for (; k < k1; ++k) s0 += k >= cr ? readlane_f64(cur[t], k - kb) * fsm[ridx(k, cr)] : 0.0;
                 }
-                double lii = 0.0;
-#pragma unroll
-                for (int t = 0; t < 4; ++t)
-                    if ((i >> 6) == t) lii = readlane_f64(cur[t], i & 63);
-                const double x = i == cr ? 1.0 / lii : -(s0 + s1) / lii;
-                if (c < n && i >= c) fsm[ridx(i, c)] = x;
-#pragma unroll
-                for (int t = 0; t < 4; ++t) cur[t] = nxt[t];
+                fsm[ridx(i, c)] = s0 + s1;
             }
+            __syncthreads();
+            // X_ic = -sum_{m=bi0}^{i} inv(L_bb)_im T_mc: lane = row, wave-owned columns
+            // c = wave + 16 j (64 bi columns); T_mc is a broadcast LDS read
+            {
+                const int i = bi0 + lane;
+                const int ir = i < bie ? i : bie - 1;
+                const int ncol = 4 * bi;  // 64 bi / 16 waves
+                double acc[12];
+#pragma unroll
+                for (int j = 0; j < 12; ++j) acc[j] = 0.0;
+                for (int m = bi0; m < bie; ++m) {
+                    const double dm = m <= ir ? fsm[ridx(ir, m)] : 0.0;
+                    const int rm = ridx(m, 0);
+#pragma unroll
+                    for (int j = 0; j < 12; ++j)
+                        if (j < ncol) acc[j] += dm * fsm[rm + wave + 16 * j];
+                }
+#pragma unroll
+                for (int j = 0; j < 12; ++j)
+                    if (j < ncol && i < bie) fsm[ridx(i, wave + 16 * j)] = -acc[j];
+            }
+            __syncthreads();
         }
     } else {
         for (int c0 = wave * 64; c0 < n; c0 += kFitThreads) {
