@@ -17,11 +17,12 @@
 // Per workgroup, n <= 200 (the factor fits the 160 KB LDS as a packed triangle):
 //   1. K = amp * Matern52(|x_i/ls - x_j/ls|) + (noise + 1e-10) I   -> LDS, packed
 //      lower, column-major
-//   2. right-looking Cholesky in LDS, one barrier per column (the pivot scaling
-//      of column j-1 is deferred into step j: it touches no column step j reads)
+//   2. Cholesky in LDS, blocked by 8-column panels (update / diagonal block /
+//      rows below, three barriers per panel); the global variant is right-looking,
+//      one barrier per column
 //   3. the factor moves to the global workspace (row-major packed) and L^-1 is
-//      built in the LDS (row-major packed): thread c forward-substitutes e_c,
-//      reading row i of L wave-uniformly and its own column from LDS
+//      built in the LDS (row-major packed), blocked by 64 rows: diagonal blocks
+//      inverted in parallel, then block rows from the top
 //   4. z = L^-1 y, alpha = L^-T z;  lml = -y.alpha/2 - sum log L_jj - n/2 log 2pi
 //   5. per pair (i >= j): K^-1_ij = sum_m L^-1_mi L^-1_mj (LDS), W = a_i a_j - K^-1_ij,
 //      recompute dK_ij/dtheta and accumulate W dK (x2 off the diagonal)
@@ -144,10 +145,107 @@ __global__ __launch_bounds__(kFitThreads) void lml_grad_kernel(LmlArgs a) {
     }
     __syncthreads();
 
-    // ---- 2. Cholesky, one barrier per column
+    // ---- 2. Cholesky
     double logdet = 0.0, prev_rs = 0.0;
     int fail = 0;
-    for (int j = 0; j < n; ++j) {
+    if (kLds) {
+        // Blocked by PW-column panels, three barriers per panel instead of one per column:
+        //  (u) A[p0:, panel] -= L[p0:, :p0] L[panel, :p0]^T   (all waves; task = column j
+        //      x 64-row chunk, lane = row: column-major reads are lane-contiguous)
+        //  (d) the diagonal block by wave 0, left-looking (lane = row; L_jj comes from
+        //      lane j with readlane, so the wave needs no barrier between columns)
+        //  (s) the rows below the block, left-looking against the finished block
+        // A non-positive / non-finite pivot propagates (sqrt -> NaN or 0) and is found
+        // by the diagonal scan below.
+        constexpr int PW = 8;   // panel width (a multiple of 8: the update's k batches)
+        for (int p0 = 0; p0 < n; p0 += PW) {
+            const int pe = min(p0 + PW, n);
+            if (p0 > 0) {
+                const int nch = (n - p0 + 63) >> 6;
+                for (int t = wave; t < (pe - p0) * nch; t += kFitWaves) {
+                    const int j = p0 + t / nch, i = p0 + 64 * (t % nch) + lane;
+                    const bool act = i >= j && i < n;
+                    const int ir = act ? i : j;
+                    double s0 = 0.0, s1 = 0.0;
+                    for (int k = 0; k < p0; k += 8) {
+                        double x[8], y[8];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) {
+                            x[u] = fsm[cidx(ir, k + u)];
+                            y[u] = fsm[cidx(j, k + u)];
+                        }
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) {
+                            if (u & 1) s1 += x[u] * y[u];
+                            else s0 += x[u] * y[u];
+                        }
+                    }
+                    if (act) fsm[cidx(i, j)] -= s0 + s1;
+                }
+                __syncthreads();
+            }
+            // left-looking panel dot: sum_{k=p0}^{j-1} L_rk L_jk for row r >= j
+            auto pdot = [&](int r, int j) -> double {
+                double s0 = 0.0, s1 = 0.0;
+                int k = p0;
+                for (; k + 7 < j; k += 8) {
+                    double x[8], y[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        x[u] = fsm[cidx(r, k + u)];
+                        y[u] = fsm[cidx(j, k + u)];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        if (u & 1) s1 += x[u] * y[u];
+                        else s0 += x[u] * y[u];
+                    }
+                }
+                for (; k < j; ++k) s0 += fsm[cidx(r, k)] * fsm[cidx(j, k)];
+                return s0 + s1;
+            };
+            if (wave == 0) {
+                const int i = p0 + lane;
+                const bool act = i < pe;
+                for (int j = p0; j < pe; ++j) {
+                    const int ir = (act && i >= j) ? i : j;
+                    const double s = fsm[cidx(ir, j)] - pdot(ir, j);
+                    const double ljj = sqrt(readlane_f64(s, j - p0));
+                    if (act && i >= j) fsm[cidx(i, j)] = i == j ? ljj : s / ljj;
+                }
+            }
+            __syncthreads();
+            if (pe < n) {
+                for (int c = wave; 64 * c < n - pe; c += kFitWaves) {
+                    const int i = pe + 64 * c + lane;
+                    const bool act = i < n;
+                    const int ir = act ? i : n - 1;
+                    for (int j = p0; j < pe; ++j) {
+                        const double s = fsm[cidx(ir, j)] - pdot(ir, j);
+                        if (act) fsm[cidx(i, j)] = s / fsm[cidx(j, j)];
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        // every wave scans the diagonal the same way (same bits): first bad pivot, log det
+        int f = 0;
+        double ld = 0.0;
+        for (int j = lane; j < n; j += 64) {
+            const double r = fsm[cidx(j, j)];
+            if (!(r > 0.0) || !isfinite(r)) {
+                if (!f) f = j + 1;
+            } else {
+                ld += log(r);
+            }
+        }
+        int fm = f ? f : 0x7fffffff;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) fm = min(fm, __shfl_xor(fm, off));
+        fail = fm == 0x7fffffff ? 0 : fm;
+        logdet = wave_sum_bcast(ld);
+    }
+    for (int j = 0; j < (kLds ? 0 : n); ++j) {
         const double dj = Lp[cidx(j, j)];
         if (!(dj > 0.0) || !isfinite(dj)) { fail = j + 1; break; }  // uniform: every thread reads dj
         const double rs = sqrt(dj);
@@ -171,7 +269,7 @@ __global__ __launch_bounds__(kFitThreads) void lml_grad_kernel(LmlArgs a) {
         for (int c = tid; c < d + 2; c += kFitThreads) a.grad[(long long)b * (d + 2) + c] = 0.0;
         return;
     }
-    if (tid == 0) Lp[cidx(n - 1, n - 1)] = prev_rs;
+    if (!kLds && tid == 0) Lp[cidx(n - 1, n - 1)] = prev_rs;
     __syncthreads();
     if (a.stop == 2) return;
 
