@@ -434,13 +434,25 @@ __global__ __launch_bounds__(kFitThreads) void lml_grad_kernel(LmlArgs a) {
             int m = i;
             if (kLds) {
                 int r = ridx(i, 0);  // start of row m (packed row-major), advanced by m + 1
-                for (; m + 1 < n; m += 2) {
+                // batches of 8 rows: all 16 LDS loads issued before the FMAs
+                for (; m + 7 < n; m += 8) {
+                    double x[8], y[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        x[u] = fsm[r + i];
+                        y[u] = fsm[r + j];
+                        r += m + u + 1;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        if (u & 1) k1 += x[u] * y[u];
+                        else k0 += x[u] * y[u];
+                    }
+                }
+                for (; m < n; ++m) {
                     k0 += fsm[r + i] * fsm[r + j];
                     r += m + 1;
-                    k1 += fsm[r + i] * fsm[r + j];
-                    r += m + 2;
                 }
-                if (m < n) k0 += fsm[r + i] * fsm[r + j];
             } else {
                 for (; m < n; ++m) k0 += lv(m, i) * lv(m, j);
             }
