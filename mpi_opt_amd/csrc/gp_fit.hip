@@ -428,7 +428,7 @@ __global__ __launch_bounds__(kFitThreads) void lml_grad_kernel(LmlArgs a) {
         const double ai = alpha[i];
         double xi[DP];
 #pragma unroll
-        for (int c = 0; c < DP; ++c) xi[c] = c < d ? a.X[i * d + c] : 0.0;
+        for (int c = 0; c < DP; ++c) xi[c] = c < d ? xs[i * d + c] : 0.0;
         for (int j = lane; j <= i; j += 64) {
             double k0 = 0.0, k1 = 0.0;
             int m = i;
@@ -463,8 +463,9 @@ __global__ __launch_bounds__(kFitThreads) void lml_grad_kernel(LmlArgs a) {
 #pragma unroll
             for (int c = 0; c < DP; ++c) {
                 if (c < d) {
-                    const double t = xi[c] - a.X[j * d + c];
-                    D[c] = t * t / (ls[c] * ls[c]);
+                    // (x_i/ls - x_j/ls)^2: xs is phase 1's X / ls (no division per pair)
+                    const double t = xi[c] - xs[j * d + c];
+                    D[c] = t * t;
                     r2 += D[c];
                 } else {
                     D[c] = 0.0;

@@ -11,7 +11,7 @@ from oracle import gp_ei as O
 from tests.conftest import ROOT
 
 G = np.load(os.path.join(ROOT, "tests", "golden", "gp_lml.npz"))
-CASES = ["n200_d10", "n12_d5", "n57_d3", "n230_d4"]
+CASES = ["n200_d10", "n12_d5", "n57_d3", "n230_d4", "n130_d6"]
 
 
 @pytest.mark.parametrize("name", CASES)

@@ -14,7 +14,7 @@ from tests.conftest import ROOT
 
 pytestmark = pytest.mark.gpu
 G = np.load(os.path.join(ROOT, "tests", "golden", "gp_lml.npz"))
-CASES = ["n200_d10", "n12_d5", "n57_d3", "n230_d4"]
+CASES = ["n200_d10", "n12_d5", "n57_d3", "n230_d4", "n130_d6"]
 
 
 def _rel_tol(X, theta):
