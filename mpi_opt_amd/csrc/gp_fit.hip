@@ -55,7 +55,7 @@ struct LmlArgs {
     int32_t* info;        // [B]
     double* ws;           // per theta: ws_stride doubles
     long long ws_stride;
-    int stop;             // diagnostics only (env MPO_FIT_DEBUG): return after phase 2/3/4
+    int stop;             // diagnostics only (env MPO_FIT_DEBUG): return after phase 1/2/3/4
 };
 
 __host__ __device__ inline long long fit_tri(long long n) { return n * (n + 1) / 2; }
@@ -144,6 +144,7 @@ __global__ __launch_bounds__(kFitThreads) void lml_grad_kernel(LmlArgs a) {
         }
     }
     __syncthreads();
+    if (a.stop == 1) return;
 
     // ---- 2. Cholesky
     double logdet = 0.0, prev_rs = 0.0;
@@ -167,12 +168,17 @@ __global__ __launch_bounds__(kFitThreads) void lml_grad_kernel(LmlArgs a) {
                     const bool act = i >= j && i < n;
                     const int ir = act ? i : j;
                     double s0 = 0.0, s1 = 0.0;
+                    // cidx(r, k+1) - cidx(r, k) = n - k - 1 for every row r, so one running
+                    // address serves both rows (L_jk sits ir - j doubles before L_{ir,k})
+                    const int dlt = ir - j;
+                    int ad = ir;  // cidx(ir, 0)
                     for (int k = 0; k < p0; k += 8) {
                         double x[8], y[8];
 #pragma unroll
                         for (int u = 0; u < 8; ++u) {
-                            x[u] = fsm[cidx(ir, k + u)];
-                            y[u] = fsm[cidx(j, k + u)];
+                            x[u] = fsm[ad];
+                            y[u] = fsm[ad - dlt];
+                            ad += n - (k + u) - 1;
                         }
 #pragma unroll
                         for (int u = 0; u < 8; ++u) {
@@ -184,25 +190,21 @@ __global__ __launch_bounds__(kFitThreads) void lml_grad_kernel(LmlArgs a) {
                 }
                 __syncthreads();
             }
-            // left-looking panel dot: sum_{k=p0}^{j-1} L_rk L_jk for row r >= j
+            // left-looking panel dot: sum_{k=p0}^{j-1} L_rk L_jk for row r >= j (j - p0 < PW):
+            // all loads issued at once at clamped (valid) addresses, summed in k order
             auto pdot = [&](int r, int j) -> double {
-                double s0 = 0.0, s1 = 0.0;
-                int k = p0;
-                for (; k + 7 < j; k += 8) {
-                    double x[8], y[8];
+                double x[PW - 1], y[PW - 1];
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        x[u] = fsm[cidx(r, k + u)];
-                        y[u] = fsm[cidx(j, k + u)];
-                    }
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        if (u & 1) s1 += x[u] * y[u];
-                        else s0 += x[u] * y[u];
-                    }
+                for (int u = 0; u < PW - 1; ++u) {
+                    const int k = min(p0 + u, j);
+                    x[u] = fsm[cidx(r, k)];
+                    y[u] = fsm[cidx(j, k)];
                 }
-                for (; k < j; ++k) s0 += fsm[cidx(r, k)] * fsm[cidx(j, k)];
-                return s0 + s1;
+                double s = 0.0;
+#pragma unroll
+                for (int u = 0; u < PW - 1; ++u)
+                    if (p0 + u < j) s += x[u] * y[u];
+                return s;
             };
             if (wave == 0) {
                 const int i = p0 + lane;
