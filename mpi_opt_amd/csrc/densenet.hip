@@ -96,6 +96,28 @@ struct BnArgs {
 };
 
 // ---- shared reductions -----------------------------------------------------------
+// e = (r*W + x)*C + c walked by a fixed step with mixed-radix adds: the staging loops
+// divide once per thread instead of twice per element
+struct Walk3 {
+    int r, x, c, sr, sx, sc, W, C;
+    __device__ __forceinline__ Walk3(int e, int W_, int C_, int step) : W(W_), C(C_) {
+        const int p = e / C_, ps = step / C_;
+        c = e - p * C_;
+        r = p / W_;
+        x = p - r * W_;
+        sc = step - ps * C_;
+        sr = ps / W_;
+        sx = ps - sr * W_;
+    }
+    __device__ __forceinline__ void next() {
+        c += sc;
+        x += sx;
+        r += sr;
+        if (c >= C) { c -= C; ++x; }
+        if (x >= W) { x -= W; ++r; }
+    }
+};
+
 __device__ __forceinline__ double block_sum(double v, double* red) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -185,9 +207,9 @@ __global__ __launch_bounds__(256) void dn_conv_kernel(ConvArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int krow = lane >> 4, kcol = lane & 15;
 
-    for (int e = tid; e < img_elems; e += 256) {
-        const int r = e / row_elems, rem = e - r * row_elems;
-        const int col = rem / Cp, c = rem - col * Cp;
+    Walk3 wk(tid, Wp, Cp, 256);
+    for (int e = tid; e < img_elems; e += 256, wk.next()) {
+        const int r = wk.r, col = wk.x, c = wk.c;
         const int gy = y0 + r - P, gx = col - P;
         float v = 0.f;
         if (gy >= 0 && gy < H && gx >= 0 && gx < W && c < Cin) v = src[((long long)gy * W + gx) * a.in_ps + c];
@@ -355,9 +377,9 @@ __global__ __launch_bounds__(kWgWaves * 64) void dn_wgrad3_kernel(WgArgs a) {
             __syncthreads();   // the previous chunk's MFMAs are done with the LDS (and the zero fill)
             if (vin) {
                 const int tot = rows * W * C4;
-                for (int e = tid; e < tot; e += NTH) {
-                    const int pix = e / C4, c4 = e - pix * C4;
-                    const int r = pix / W, x = pix - r * W;
+                Walk3 wk(tid, W, C4, NTH);
+                for (int e = tid; e < tot; e += NTH, wk.next()) {
+                    const int r = wk.r, x = wk.x, c4 = wk.c;
                     const int gy = y0 + r - P;
                     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
                     if (gy >= 0 && gy < H)
@@ -366,9 +388,9 @@ __global__ __launch_bounds__(kWgWaves * 64) void dn_wgrad3_kernel(WgArgs a) {
                 }
             } else {
                 const int tot = rows * W * Cin;
-                for (int e = tid; e < tot; e += NTH) {
-                    const int pix = e / Cin, c = e - pix * Cin;
-                    const int r = pix / W, x = pix - r * W;
+                Walk3 wk(tid, W, Cin, NTH);
+                for (int e = tid; e < tot; e += NTH, wk.next()) {
+                    const int r = wk.r, x = wk.x, c = wk.c;
                     const int gy = y0 + r - P;
                     float v = 0.f;
                     if (gy >= 0 && gy < H) v = src[((long long)gy * W + x) * a.in_ps + c];
