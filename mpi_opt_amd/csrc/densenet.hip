@@ -96,6 +96,22 @@ struct BnArgs {
 };
 
 // ---- shared reductions -----------------------------------------------------------
+// e = q*C + c walked by a fixed step (one division per thread, not per element)
+struct Walk2 {
+    int q, c, sq, sc, C;
+    __device__ __forceinline__ Walk2(int e, int C_, int step) : C(C_) {
+        q = e / C_;
+        c = e - q * C_;
+        sq = step / C_;
+        sc = step - sq * C_;
+    }
+    __device__ __forceinline__ void next() {
+        c += sc;
+        q += sq;
+        if (c >= C) { c -= C; ++q; }
+    }
+};
+
 // e = (r*W + x)*C + c walked by a fixed step with mixed-radix adds: the staging loops
 // divide once per thread instead of twice per element
 struct Walk3 {
@@ -577,8 +593,9 @@ __global__ __launch_bounds__(256) void dn_bn_stats_kernel(BnArgs a, double* __re
     const float* xm = a.x + m * a.x_ms + (long long)h * W * a.x_ps;
     const int b0 = sl * bs, b1 = min(a.B, b0 + bs);
     double s = 0.0, q = 0.0;
-    for (int e = tid; e < rowe; e += 256) {
-        const int w = e / Cin, c = e - w * Cin;
+    Walk2 wk(tid, Cin, 256);
+    for (int e = tid; e < rowe; e += 256, wk.next()) {
+        const int w = wk.q, c = wk.c;
         const float* p = xm + (long long)w * a.x_ps + c;
         for (int b = b0; b < b1; ++b) {
             const double v = p[b * bstride];
@@ -639,8 +656,9 @@ __global__ __launch_bounds__(256) void dn_bn_apply_kernel(BnArgs a, const double
     const float s = sc[0], t = sc[1];
     const float* xr = a.x + m * a.x_ms + ((long long)b * H + h) * W * a.x_ps;
     float* zr = a.z + m * a.z_ms + ((long long)b * H + h) * rowe;
-    for (int e = tid; e < rowe; e += 256) {
-        const int w = e / Cin, c = e - w * Cin;
+    Walk2 wk(tid, Cin, 256);
+    for (int e = tid; e < rowe; e += 256, wk.next()) {
+        const int w = wk.q, c = wk.c;
         const float y = xr[(long long)w * a.x_ps + c] * s + t;
         zr[e] = y > 0.f ? y : expm1f(y);
     }
@@ -672,8 +690,9 @@ __global__ __launch_bounds__(256) void dn_bn_bwd_reduce_kernel(BnArgs a, double*
         const float* zr = a.z + m * a.z_ms + zo;
         const float* dzr = a.bcast ? nullptr : a.dz + m * a.dz_ms + zo;
         const float* dgr = a.bcast ? a.dg + m * a.dg_ms + (long long)b * Cin : nullptr;
-        for (int e = tid; e < rowe; e += 256) {
-            const int w = e / Cin, c = e - w * Cin;
+        Walk2 wk(tid, Cin, 256);
+        for (int e = tid; e < rowe; e += 256, wk.next()) {
+            const int w = wk.q, c = wk.c;
             const float dy = bn_dy(a, zr, dzr, dgr, e, c);
             const float xh = (xr[(long long)w * a.x_ps + c] - mean) * inv;
             sdy += dy;
@@ -723,8 +742,9 @@ __global__ __launch_bounds__(256) void dn_bn_bwd_apply_kernel(BnArgs a, const do
     const float* dzr = a.bcast ? nullptr : a.dz + m * a.dz_ms + zo;
     const float* dgr = a.bcast ? a.dg + m * a.dg_ms + (long long)b * Cin : nullptr;
     float* dxr = a.dx + m * a.dx_ms + ((long long)b * H + h) * W * a.dx_ps;
-    for (int e = tid; e < rowe; e += 256) {
-        const int w = e / Cin, c = e - w * Cin;
+    Walk2 wk(tid, Cin, 256);
+    for (int e = tid; e < rowe; e += 256, wk.next()) {
+        const int w = wk.q, c = wk.c;
         const float dy = bn_dy(a, zr, dzr, dgr, e, c);
         const float xh = (xr[(long long)w * a.x_ps + c] - mean) * inv;
         const float v = ca * (n * dy - fb - xh * fg);
