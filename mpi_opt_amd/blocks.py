@@ -11,13 +11,18 @@ loops barrier -> recv params from rank 0 -> build the Keras model ->
   ``hist["history"]["0"]["val_loss"][-1]`` convention of option0:71-82),
   non-finite losses clamped to the clipped-BCE ceiling 16.12 (a diverged trial
   must never hang or poison the GP);
-* :class:`PopulationComm` is an MPI-communicator stand-in for the unchanged
-  :class:`~mpi_opt_amd.coordinator.Coordinator`: ``send`` records the
+* :class:`PopulationComm` is an MPI-communicator stand-in for the reference's
+  unchanged ``Coordinator`` (coordinator.py:7-150) or this build's
+  :class:`~mpi_opt_amd.scheduler.AskTellScheduler`: ``send`` records the
   parameters each rank of a block receives (tag 4), ``irecv`` from a block
   master returns a request whose ``test()`` answers "not done" while some block
-  is still idle and, once every block is busy, trains all launched blocks
+  is still idle or another block's result is waiting to be collected and, once
+  every block is busy and nothing is waiting, trains all launched blocks
   together -- the blocks the reference runs concurrently on MPI ranks run
-  concurrently as population members on the GPU;
+  concurrently as population members on the GPU.  After the exit broadcast
+  (``send(None)``) the ``Barrier`` trains the trials still in flight, as the
+  reference's blocks finish theirs before reading the exit message
+  (process_block.py:104-121); their FOMs are never told (coordinator.py:98-101);
 * :class:`DistributedEvaluator` shards (trial, fold) units over the ranks of a
   torch.distributed group (RCCL over xGMI) by longest-processing-time on the
   per-unit FLOPs, with no data-path collective: rank 0 broadcasts the batch of
@@ -61,6 +66,7 @@ class TrialEvaluator:
         self.history_dir = history_dir
         self.init_seed = init_seed
         self.n_evaluated = 0
+        self.train_s = 0.0          # wall seconds spent training populations (synchronised)
 
     def units(self, params_list):
         """(trial index, fold) pairs with their training FLOPs (LPT cost)."""
@@ -77,6 +83,15 @@ class TrialEvaluator:
         """Train the given (trial, fold, spec) units as populations -- one for the
         test_mnist units, one per DenseNet architecture; returns
         {(trial, fold): history dict}."""
+        import time
+
+        t0 = time.perf_counter()
+        try:
+            return self._train_units(units, seed_base)
+        finally:
+            self.train_s += time.perf_counter() - t0
+
+    def _train_units(self, units, seed_base):
         from .models import DenseNetSpec
 
         out = {}
@@ -128,6 +143,9 @@ class TrialEvaluator:
         for i, (t, f, _, _) in enumerate(units):
             out[(t, f)] = {"val_loss": [float(v) for v in hist["val_loss"][i]],
                            "val_acc": [float(v) for v in hist["val_acc"][i]]}
+            for key in ("dropped_train_samples", "dropped_val_samples"):
+                if key in hist:
+                    out[(t, f)][key] = int(hist[key][i])
         return out
 
     def foms(self, params_list, results):
@@ -167,9 +185,11 @@ class _Request:
     def test(self):
         c = self.comm
         if self.block not in c.results:
+            if c.results:
+                return False, None      # other results are waiting: let the scheduler collect them first
             if len(c.busy) < c.num_blocks:
-                return False, None      # another block is idle: let the coordinator fill it first
-            c.evaluate_pending()
+                return False, None      # another block is idle: let the scheduler fill it first
+            c.evaluate_pending()        # every block busy, nothing ready: train the launched blocks together
         c.busy.discard(self.block)
         return True, c.results.pop(self.block)
 
@@ -177,14 +197,16 @@ class _Request:
 class PopulationComm:
     """MPI-communicator stand-in for :class:`Coordinator` (size = 1 + blocks x block_size)."""
 
-    def __init__(self, num_blocks, block_size, evaluator):
+    def __init__(self, num_blocks, block_size, evaluator, train_tail=True):
         self.num_blocks, self.block_size, self.evaluator = num_blocks, block_size, evaluator
+        self.train_tail = train_tail
         self.received = {}       # rank -> last params
         self.pending = {}        # block -> params launched, not yet trained
         self.results = {}        # block -> fom
         self.exited = set()
         self.busy = set()        # launched blocks whose result has not been collected
         self.batches = []        # sizes of the populations trained
+        self.tail = []           # (params, fom) of trials trained after the exit broadcast (never told)
 
     def Get_size(self):
         return 1 + self.num_blocks * self.block_size
@@ -223,7 +245,14 @@ class PopulationComm:
             self.results[b] = f
 
     def Barrier(self):
-        pass
+        if self.train_tail and self.exited and self.pending:
+            launched = {b: list(p) for b, p in self.pending.items()}
+            self.evaluate_pending()
+            self.tail = [(launched[b], self.results[b]) for b in sorted(launched)]
+
+    @property
+    def trials_trained(self):
+        return sum(self.batches)
 
 
 class DistributedEvaluator:

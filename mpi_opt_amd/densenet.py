@@ -282,6 +282,10 @@ class DenseNetPopulation:
         n_va = min(len(v) for v in va)
         steps_per_epoch = n_tr // B
         val_batches = n_va // B
+        if steps_per_epoch == 0 or val_batches == 0:
+            raise ValueError(f"fold too small for batch {B}: {n_tr} train / {n_va} validation samples")
+        dropped_tr = [len(t) - steps_per_epoch * B for t in tr]     # reported, never hidden
+        dropped_va = [len(v) - val_batches * B for v in va]
         order_tr = torch.from_numpy(np.stack([t[:n_tr] for t in tr])).to(self.device)
         order_va = torch.from_numpy(np.stack([v[:n_va] for v in va])).to(self.device)
         val_loss = torch.zeros(self.n, epochs, dtype=torch.float32, device=self.device)
@@ -299,7 +303,8 @@ class DenseNetPopulation:
             val_loss[:, ep] = self.val_loss_sum / denom + self.penalty()
             val_acc[:, ep] = self.val_correct.to(torch.float32) / denom
         out = {"val_loss": val_loss.cpu().numpy(), "val_acc": val_acc.cpu().numpy(),
-               "steps_per_epoch": steps_per_epoch, "val_batches": val_batches}
+               "steps_per_epoch": steps_per_epoch, "val_batches": val_batches,
+               "dropped_train_samples": dropped_tr, "dropped_val_samples": dropped_va}
         if record_train_loss:
             out["train_loss"] = torch.stack(tl, 1).cpu().numpy() if tl else np.zeros((self.n, 0))
         return out

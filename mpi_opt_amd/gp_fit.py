@@ -79,14 +79,17 @@ class DeviceLML:
         B = thetas.shape[0]
         if thetas.shape[1] != self.d + 2:
             raise ValueError(f"theta has {thetas.shape[1]} entries, expected d+2={self.d + 2}")
-        self._ensure(B)
-        self.theta_d[:B].copy_(torch.from_numpy(thetas))
-        _lib.check(_lib.lib().mpo_gp_lml_grad(
-            _lib.ptr(self.X), _lib.ptr(self.y), self.n, self.d, _lib.ptr(self.theta_d), B,
-            _lib.ptr(self.lml_d), _lib.ptr(self.grad_d), _lib.ptr(self.info_d),
-            _lib.ptr(self.ws), self.ws_bytes, _lib.stream_handle(self.device)), "mpo_gp_lml_grad")
-        return (self.lml_d[:B].cpu().numpy().copy(), self.grad_d[:B].cpu().numpy().copy(),
-                self.info_d[:B].cpu().numpy().copy())
+        # runs on the lockstep worker threads, whose current HIP device is the
+        # thread-local default: pin this objective's device for the launch
+        with torch.cuda.device(self.device):
+            self._ensure(B)
+            self.theta_d[:B].copy_(torch.from_numpy(thetas))
+            _lib.check(_lib.lib().mpo_gp_lml_grad(
+                _lib.ptr(self.X), _lib.ptr(self.y), self.n, self.d, _lib.ptr(self.theta_d), B,
+                _lib.ptr(self.lml_d), _lib.ptr(self.grad_d), _lib.ptr(self.info_d),
+                _lib.ptr(self.ws), self.ws_bytes, _lib.stream_handle(self.device)), "mpo_gp_lml_grad")
+            return (self.lml_d[:B].cpu().numpy().copy(), self.grad_d[:B].cpu().numpy().copy(),
+                    self.info_d[:B].cpu().numpy().copy())
 
 
 class _Lockstep:

@@ -7,14 +7,16 @@
   The reference reads ``args.get('drop_out', 0.25)`` while its search space
   names the dimension ``dropout`` (option3:131): the dimension is dead and
   the rate stays 0.25 -- reproduced here.
-* ``test_cnn`` / ``test_densenet`` -- mpiLAPI.py:178-201 (topclass CNN, DenseNet)
-  as JSON specs; a DenseNet spec ingests into a :class:`DenseNetSpec` that the
-  DenseNet population engine (densenet.py) trains.
+* ``test_densenet`` -- mpiLAPI.py:197-201 (DenseNet) as a JSON spec that
+  ingests into a :class:`DenseNetSpec` the DenseNet population engine
+  (densenet.py) trains.  The topclass CNN and the 3-D GAN (mpiLAPI.py:178-195,
+  option3:110-114, 144-168) are out of scope: their data and models
+  are not in the BASELINE configs, so no builder is offered for them.
 * ``BuilderFromFunction`` -- hyperparameter_search_option3.py:22-31: zips the
   named dimensions with a parameter list, calls ``model_fn(**named)`` and wraps
   the JSON in a ``ModelFromJson`` with settable ``comm`` / ``device`` and
   ``get_device_name`` (used by process_block.py:64-67).
-* ``BaseModel`` / ``CNNModel`` / ``DenseNetModel`` -- base_model.py:8-92:
+* ``BaseModel`` / ``DenseNetModel`` -- base_model.py:8-19, 57-92:
   ``build(params) -> json``, ``get_parameter_grid()``, ``get_name()``.
 """
 from __future__ import annotations
@@ -65,24 +67,6 @@ def test_mnist(**args):
         _layer("Dense", name="dense_2", units=nb_classes, activation="linear", use_bias=True,
                kernel_initializer="glorot_uniform", bias_initializer="zeros"),
         _layer("Activation", name="activation_4", activation="softmax"),
-    ]
-    return _sequential(layers)
-
-
-def test_cnn(**args):
-    """Topclass CNN spec (mpiLAPI.py:178-195); ``llr`` is lost by to_json there too."""
-    dropout = float(args.get("dropout", 0.5))
-    ks = int(args.get("kernel_size", 3))
-    layers = [
-        _layer("Conv2D", filters=32, kernel_size=[ks, ks], strides=[3, 3], activation="relu",
-               batch_input_shape=[None, 150, 94, 5], padding="valid"),
-        _layer("Conv2D", filters=32, kernel_size=[ks, ks], strides=[3, 3], activation="relu", padding="valid"),
-        _layer("MaxPooling2D", pool_size=[2, 2], strides=[2, 2], padding="valid"),
-        _layer("Dropout", rate=dropout / 2),
-        _layer("Flatten"),
-        _layer("Dense", units=128, activation="relu"),
-        _layer("Dropout", rate=dropout),
-        _layer("Dense", units=3, activation="softmax"),
     ]
     return _sequential(layers)
 
@@ -188,22 +172,6 @@ class BaseModel:
         raise NotImplementedError
 
 
-class CNNModel(BaseModel):
-    """base_model.py:21-55 (topclass CNN; ``lr = 10 ** params[2]``)."""
-
-    def __init__(self, input_shape=(150, 94, 5)):
-        self.input_shape = input_shape
-
-    def build(self, params):
-        return test_cnn(kernel_size=int(params[0]), dropout=float(params[1]))
-
-    def get_parameter_grid(self):
-        return [(3, 9), (.0, .5), (-5, 1)]
-
-    def get_name(self):
-        return "CNN_model"
-
-
 class DenseNetModel(BaseModel):
     """base_model.py:57-92."""
 
@@ -232,34 +200,10 @@ def mnist_space():
             Real(0.0, 1.0, name="dropout")]
 
 
-def topclass_space():
-    """option3:110-114."""
-    from .space import Integer, Real
-
-    return [Real(0.0, 1.0, name="dropout"), Integer(1, 6, name="kernel_size"), Real(1., 10., name="llr")]
-
-
-def gan_space():
-    """option3:146-152."""
-    from .space import Categorical, Integer, Real
-
-    return [Integer(50, 400, name="latent_size"), Real(0.0, 1.0, name="discr_drop_out"),
-            Categorical([1, 2, 5, 6, 8], name="gen_weight"), Categorical([0.1, 0.2, 1, 2, 10], name="aux_weight"),
-            Categorical([0.1, 0.2, 1, 2, 10], name="ecal_weight")]
-
-
-def threaded_skopt_space(n_par=2):
-    """threaded_skopt.py:148 demo space."""
-    from .space import Real
-
-    return [Real(-20, 20) for _ in range(n_par)]
-
-
 def flops_of_params(model_fn, names, params):
     spec = spec_from_json(model_fn(**dict(zip(names, params))))
     return spec.flops_per_sample_train()
 
 
-__all__ = ["test_mnist", "test_cnn", "test_densenet", "spec_from_json", "DenseNetSpec", "ModelFromJson", "BuilderFromFunction",
-           "BaseModel", "CNNModel", "DenseNetModel", "mnist_space", "topclass_space", "gan_space",
-           "threaded_skopt_space"]
+__all__ = ["test_mnist", "test_densenet", "spec_from_json", "DenseNetSpec", "ModelFromJson", "BuilderFromFunction",
+           "BaseModel", "DenseNetModel", "mnist_space"]

@@ -33,6 +33,7 @@ import numpy as np
 from scipy.optimize import fmin_l_bfgs_b
 from scipy.stats import norm
 
+from . import _lib
 from .gp_fit import fit_lml
 from .space import Space, check_random_state
 
@@ -138,7 +139,11 @@ class OptimizeResult(dict):
 
 
 class Optimizer:
-    """Drop-in for ``skopt.Optimizer`` (GP base estimator, device acquisition)."""
+    """Drop-in for ``skopt.Optimizer`` (GP base estimator, device acquisition).
+
+    ``acq_optimizer_kwargs["n_restarts_optimizer"]`` (default 5) may exceed the
+    device top-k width (``MPO_TOPK_MAX`` = 8); the acquisition rows are then
+    sorted whole on the device instead."""
 
     def __init__(self, dimensions, base_estimator="gp", n_random_starts=None, n_initial_points=10,
                  initial_point_generator="random", acq_func="gp_hedge", acq_optimizer="auto",
@@ -266,11 +271,10 @@ class Optimizer:
         xi = self.acq_func_kwargs.get("xi", 0.01)
         kappa = self.acq_func_kwargs.get("kappa", 1.96)
         k = 1 if self.acq_optimizer == "sampling" else min(self.n_restarts_optimizer, X.shape[0])
-        scored = est.dev.score(X, y_opt, acqs=tuple(self.cand_acq_funcs_), xi=xi, kappa=kappa, k=k,
-                               want_mu_sd=False, want_values=False)
+        top = self._score_topk(est, X, y_opt, xi, kappa, k)
         self.next_xs_ = []
         for acq in self.cand_acq_funcs_:
-            idx = scored["topk"][acq][0].cpu().numpy()
+            idx = top[acq]
             if self.acq_optimizer == "sampling":
                 next_x = X[idx[0]]
             else:
@@ -292,6 +296,20 @@ class Optimizer:
         else:
             next_x = self.next_xs_[0]
         self._next_x = self.space.inverse_transform(next_x.reshape(1, -1))[0]
+
+    def _score_topk(self, est, X, y_opt, xi, kappa, k):
+        """skopt's ``np.argsort(values)[:k]`` per acquisition (lowest index first on
+        ties).  The device top-k holds up to MPO_TOPK_MAX entries; a larger
+        ``n_restarts_optimizer`` takes the full value rows and a stable sort."""
+        acqs = tuple(self.cand_acq_funcs_)
+        if k <= _lib.MPO_TOPK_MAX:
+            scored = est.dev.score(X, y_opt, acqs=acqs, xi=xi, kappa=kappa, k=k, want_mu_sd=False,
+                                   want_values=False)
+            return {a: scored["topk"][a][0].cpu().numpy() for a in acqs}
+        import torch
+
+        scored = est.dev.score(X, y_opt, acqs=acqs, xi=xi, kappa=kappa, k=0, want_mu_sd=False, want_values=True)
+        return {a: torch.sort(scored["values"][a], stable=True)[1][:k].cpu().numpy() for a in acqs}
 
     def _result(self):
         if not self.yi:

@@ -250,10 +250,18 @@ class PopulationEngine:
             t, v = kfold_split(n_samples, n_fold, int(folds[i]))
             tr.append(t)
             va.append(v)
+        # members step in lock-step on full batches: every member trains on the
+        # first steps_per_epoch*B indices of its fold and validates on the first
+        # val_batches*B; what that leaves out (uneven folds, a partial last batch
+        # that Keras would still run) is reported in the history, never hidden
         n_tr = min(len(t) for t in tr)
         n_va = min(len(v) for v in va)
         steps_per_epoch = n_tr // B
         val_batches = n_va // B
+        if steps_per_epoch == 0 or val_batches == 0:
+            raise ValueError(f"fold too small for batch {B}: {n_tr} train / {n_va} validation samples")
+        dropped_tr = [len(t) - steps_per_epoch * B for t in tr]
+        dropped_va = [len(v) - val_batches * B for v in va]
         order_tr = torch.from_numpy(np.stack([t[:n_tr] for t in tr])).to(self.device)
         order_va = torch.from_numpy(np.stack([v[:n_va] for v in va])).to(self.device)
         val_loss = torch.zeros(self.n, epochs, dtype=torch.float32, device=self.device)
@@ -271,7 +279,8 @@ class PopulationEngine:
             val_loss[:, ep] = self.val_loss_sum / denom
             val_acc[:, ep] = self.val_correct.to(torch.float32) / denom
         out = {"val_loss": val_loss.cpu().numpy(), "val_acc": val_acc.cpu().numpy(),
-               "steps_per_epoch": steps_per_epoch, "val_batches": val_batches}
+               "steps_per_epoch": steps_per_epoch, "val_batches": val_batches,
+               "dropped_train_samples": dropped_tr, "dropped_val_samples": dropped_va}
         if record_train_loss:
             out["train_loss"] = torch.stack(tl, 1).cpu().numpy() if tl else np.zeros((self.n, 0))
         return out

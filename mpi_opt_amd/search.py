@@ -67,6 +67,73 @@ def block_layout(world_size, block_size):
     return divmod(world_size - 1, block_size)
 
 
+def run_search(args, x=None, y=None, log=print):
+    """Run the option3 search for parsed ``args``; returns a report dict (rank 0)
+    or None (ranks > 0, which serve their shards until rank 0 is done).
+
+    The report splits the wall time into the optimizer (ask = GP refits of the
+    cl_min batch + acquisition, tell = the refit on told results) and the
+    device training of the populations, and counts the trials trained."""
+    import time
+
+    import torch
+
+    from .blocks import DistributedEvaluator, PopulationComm, TrialEvaluator
+    from .models import BuilderFromFunction, mnist_space, test_mnist
+    from .population import synthetic_mnist
+    from .scheduler import AskTellScheduler
+
+    num_blocks, left_over = block_layout(args.world_size, args.block_size)
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if ws > 1:
+        import torch.distributed as dist
+
+        if not dist.is_initialized():
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    provider = BuilderFromFunction(model_fn=test_mnist, parameters=mnist_space())
+    if x is None:
+        x, y = synthetic_mnist(args.n_samples, seed=0, device=dev)
+    evaluator = TrialEvaluator(provider, x, y, n_fold=args.n_fold, epochs=args.epochs, batch=args.batch,
+                               lr=args.lr, device=dev, history_dir=args.history_dir)
+    local_eval = evaluator
+    if dist is not None:
+        evaluator = DistributedEvaluator(evaluator)
+        if evaluator.rank != 0:
+            evaluator.serve()
+            return None
+    comm = PopulationComm(num_blocks, args.block_size, evaluator)
+    sched = AskTellScheduler(comm, num_blocks, provider.parameters, checkpoint=args.checkpoint,
+                             target_fom=args.target_objective, verbose=args.verbose)
+    if args.previous_state:
+        sched.load(args.previous_state)
+    t0 = time.perf_counter()
+    state = sched.run(num_iterations=args.num_iterations)
+    wall = time.perf_counter() - t0
+    if dist is not None:
+        evaluator.shutdown()
+    tm = sched.timings
+    report = {
+        "wall_s": wall,
+        "trials_trained": comm.trials_trained,
+        "trials_told": len(state.fom_list),
+        "populations": list(comm.batches),
+        "num_blocks": num_blocks,
+        "optimizer_s": tm["ask_s"] + tm["tell_s"],
+        "ask_s": tm["ask_s"], "tell_s": tm["tell_s"], "asks": tm["asks"], "tells": tm["tells"],
+        "train_s": local_eval.train_s,
+        "trials_per_hour": 3600.0 * comm.trials_trained / wall if wall > 0 else None,
+        "best_fom": state.best_fom, "best_params": state.best_params,
+    }
+    log(f"search done: {report['trials_trained']} trials trained ({report['trials_told']} told) in "
+        f"{wall:.1f} s; optimizer {report['optimizer_s']:.2f} s, training {report['train_s']:.1f} s; "
+        f"best {state.best_fom} at {state.best_params}")
+    return report
+
+
 def main(argv=None):
     args = make_parser().parse_args(argv)
     check_sanity(args)
@@ -79,43 +146,10 @@ def main(argv=None):
         print("The last block is going to be made of {} nodes, make inconsistent block size {}".format(
             left_over, args.block_size))
         return 1
-
-    import torch
-
-    from .blocks import DistributedEvaluator, PopulationComm, TrialEvaluator
-    from .coordinator import Coordinator
-    from .models import BuilderFromFunction, mnist_space, test_mnist
-    from .population import synthetic_mnist
-
-    ws = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if ws > 1:
+    run_search(args)
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local)
-    provider = BuilderFromFunction(model_fn=test_mnist, parameters=mnist_space())
-    x, y = synthetic_mnist(args.n_samples, seed=0, device=dev)
-    evaluator = TrialEvaluator(provider, x, y, n_fold=args.n_fold, epochs=args.epochs, batch=args.batch,
-                               lr=args.lr, device=dev, history_dir=args.history_dir)
-    if dist is not None:
-        evaluator = DistributedEvaluator(evaluator)
-        if evaluator.rank != 0:
-            evaluator.serve()
-            dist.destroy_process_group()
-            return 0
-    comm = PopulationComm(num_blocks, args.block_size, evaluator)
-    Coordinator.checkpoint_file = args.checkpoint
-    coord = Coordinator(comm, num_blocks, provider.parameters)
-    if args.previous_state:
-        coord.load(args.previous_state)
-    if args.target_objective:
-        coord.target_fom = args.target_objective
-    coord.run(num_iterations=args.num_iterations)
-    if dist is not None:
-        evaluator.shutdown()
         dist.destroy_process_group()
     return 0
 

@@ -2,6 +2,8 @@ import json
 import math
 import random
 
+import pytest
+
 from mpi_opt_amd.blocks import FOM_CEILING, PopulationComm, TrialEvaluator, lpt_assign
 from mpi_opt_amd.models import BuilderFromFunction, mnist_space
 from mpi_opt_amd.models import test_mnist as mnist_model_fn
@@ -34,11 +36,11 @@ class StubOpt:
 
 
 def test_population_comm_drives_coordinator(tmp_path, monkeypatch):
-    from mpi_opt_amd.coordinator import Coordinator
+    from mpi_opt_amd.scheduler import AskTellScheduler
 
     monkeypatch.chdir(tmp_path)
 
-    class C(Coordinator):
+    class C(AskTellScheduler):
         optimizer_factory = staticmethod(lambda d, r: StubOpt())
 
         def save(self, fn=None):
@@ -51,10 +53,39 @@ def test_population_comm_drives_coordinator(tmp_path, monkeypatch):
     c.run(num_iterations=10)
     # launched blocks are trained together: the first batch holds all 4 blocks
     assert comm.batches[0] == 4
-    assert sum(comm.batches) == len(c.fom_list)
+    # every trial launched is trained (the in-flight tail after the exit broadcast
+    # too, as the reference's blocks finish theirs); only the told ones reach fom_list
+    assert sum(comm.batches) == 10 == len(c.fom_list) + len(comm.results)
     assert comm.exited == set(range(1, 21))
     for p, f in zip(c.param_list, c.fom_list):
         assert f == sum(p) / 1000.0
+    for p, f in comm.tail:
+        assert f == sum(p) / 1000.0
+
+
+@pytest.mark.parametrize("blocks,iters,seed", [(4, 10, 0), (4, 25, 1), (3, 17, 5), (8, 40, 2), (2, 9, 7)])
+def test_population_width_is_kept(tmp_path, monkeypatch, blocks, iters, seed):
+    """Ready results are collected before anything trains, so every population
+    except the tail trained at the exit holds exactly ``num_blocks`` trials."""
+    from mpi_opt_amd.scheduler import AskTellScheduler
+
+    monkeypatch.chdir(tmp_path)
+
+    class C(AskTellScheduler):
+        optimizer_factory = staticmethod(lambda d, r: StubOpt())
+
+        def save(self, fn=None):
+            pass
+
+    random.seed(seed)
+    comm = PopulationComm(blocks, 2, FakeEval())
+    c = C(comm, blocks, [(0, 1)])
+    c.run(num_iterations=iters)
+    assert sum(comm.batches) == iters
+    assert all(b == blocks for b in comm.batches[:-1]), comm.batches
+    assert 0 < comm.batches[-1] <= blocks
+    told = len(c.fom_list)
+    assert told == iters - blocks           # the reference leaves num_blocks trials untold
 
 
 def test_lpt_balances():
