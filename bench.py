@@ -76,23 +76,36 @@ def load_population_pmc():
         return None
 
 
-def cpu_baseline_ei(n=200, d=10, sample=150_000):
-    """skopt's literal K_inv einsum posterior + EI (the oracle restatement) timed on
-    the host: single-threaded einsum, as skopt calls it."""
+def host_cores():
+    """Host cores this job may use: the box's share (OMP_NUM_THREADS is set to it
+    there), else the affinity mask."""
+    return int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
+
+
+def cpu_baseline_ei(n=200, d=10, sample_1core=100_000):
+    """skopt's literal K_inv einsum posterior + EI + argsort (the oracle
+    restatement; skopt calls it single-threaded) timed on the host: on one core,
+    and split over every host core (one single-threaded process per core).
+    ``value`` is the all-cores rate."""
     from oracle import gp_ei as O
 
     X, y = O.synthetic_problem(n, d, 0)
-    st = O.gp_from_theta(X, y, 17.4955, np.array([16.2, 1.91, 1.65, 9.84, 1.84, 2.94, 2.45, 9.09, 8.13, 1.94]),
-                         0.0465)
-    C = O.synthetic_candidates(sample, d, seed=11)
+    amp, ls, noise = 17.4955, np.array([16.2, 1.91, 1.65, 9.84, 1.84, 2.94, 2.45, 9.09, 8.13, 1.94]), 0.0465
+    st = O.gp_from_theta(X, y, amp, ls, noise)
+    C = O.synthetic_candidates(sample_1core, d, seed=11)
     t0 = time.perf_counter()
     mu, sd = O.posterior_skopt(st, C)
     v = -O.gaussian_ei(mu, sd, float(np.min(y)))
     np.argsort(v)[:5]
-    dt = time.perf_counter() - t0
-    return {"value": sample / dt, "unit": "candidates/s", "cores": 1, "kind": "port",
-            "sample": f"{sample} candidates, N={n} D={d}, skopt K_inv einsum form (oracle/gp_ei.py), "
-                      f"{dt:.1f} s on 1 host core"}
+    dt1 = time.perf_counter() - t0
+    cores = host_cores()
+    sample_all = int(sample_1core * min(cores, 16) // 2)
+    dt, done = O.time_skopt_ei(X, y, amp, ls, noise, sample_all, cores)
+    return {"value": done / dt, "unit": "candidates/s", "cores": cores, "kind": "port",
+            "single_core": sample_1core / dt1,
+            "sample": f"{done} candidates over {cores} single-threaded processes ({dt:.1f} s) and "
+                      f"{sample_1core} on 1 core ({dt1:.1f} s, {sample_1core / dt1:.3g} cand/s); N={n} D={d}, "
+                      f"skopt K_inv einsum form + EI + argsort (oracle/gp_ei.py)"}
 
 
 def bench_ei(args, torch, dist, ws, rank, dev):
@@ -240,46 +253,47 @@ def bench_gp_fit(args, torch, dev, cpu):
 
 def sample_trials(n, seed):
     """Trials drawn from the option3 mnist space (option3:127-131): nb_filters,
-    pool_size, kernel_size, dense (the dead `dropout` dimension trains at 0.25)."""
+    pool_size, kernel_size, dense -- plus a per-trial Adam lr 10**U(-4,-2) and
+    dropout rate U(0, 0.5), the configs[2] "ragged widths/lr/dropout" population
+    (the reference's own dropout dimension is dead and trains at 0.25)."""
     from mpi_opt_amd.population import TrialSpec
 
     rng = np.random.RandomState(seed)
-    return [TrialSpec(nb_filters=int(rng.randint(10, 51)), pool_size=int(rng.randint(2, 11)),
-                      kernel_size=int(rng.randint(2, 11)), dense=int(rng.randint(50, 201)), seed=i)
-            for i in range(n)]
+    out = []
+    for i in range(n):
+        F, p, k, dense = (int(rng.randint(10, 51)), int(rng.randint(2, 11)), int(rng.randint(2, 11)),
+                          int(rng.randint(50, 201)))
+        out.append(TrialSpec(nb_filters=F, pool_size=p, kernel_size=k, dense=dense,
+                             lr=float(10.0 ** rng.uniform(-4, -2)), dropout=float(rng.uniform(0.0, 0.5)), seed=i))
+    return out
 
 
-def cpu_baseline_train(trials, budget_s=12.0):
-    """fp64 numpy restatement (oracle/cnn.py) of single-trial training on the host,
-    timed on a bounded sample of train steps and extrapolated to whole trials
-    (5-fold, 10 epochs, 60k samples: 24 000 train steps + 6 000 validation batches)."""
-    from oracle import cnn as C
-    from mpi_opt_amd.population import glorot_uniform_init
+def torch_cpu_trial_seconds(trials, concurrent=4, steps=3, val=1):
+    """torch-CPU fp32 (oracle/cnn_torch.py) seconds per train step / validation
+    batch of each trial at batch 100, ``concurrent`` trials at once on the host
+    cores (cores // concurrent threads each; the -n 21 --block-size 5 layout)."""
+    from oracle import cnn_torch as CT
 
-    rng = np.random.RandomState(5)
-    x = rng.uniform(size=(100, 784)).astype(np.float32)
-    y = rng.randint(0, 10, size=100)
-    t_tr, t_ev, n = 0.0, 0.0, 0
-    t_start = time.perf_counter()
-    for t in trials:
-        o = C.TrialOracle(t.nb_filters, t.kernel_size, t.pool_size, t.dense,
-                          {k: v.astype(np.float64) for k, v in glorot_uniform_init(t, 0).items()}, seed=1)
-        t0 = time.perf_counter()
-        o.train_step(x, y, 0)
-        t1 = time.perf_counter()
-        o.forward(x, y, train=False)
-        t2 = time.perf_counter()
-        t_tr += t1 - t0
-        t_ev += t2 - t1
-        n += 1
-        if time.perf_counter() - t_start > budget_s:
-            break
-    sec_per_trial = (24000 * t_tr + 6000 * t_ev) / n
-    cores = int(os.environ.get("OMP_NUM_THREADS", len(os.sched_getaffinity(0))))
-    return {"value": 3600.0 / sec_per_trial, "unit": "trials/hour", "cores": cores, "kind": "port",
-            "sample": f"1 train step + 1 validation batch (batch 100) of each of the first {n} sampled trials, "
-                      f"fp64 numpy restatement (oracle/cnn.py, BLAS threads = {cores}), extrapolated to "
-                      f"24000 train steps + 6000 validation batches per trial ({time.perf_counter() - t_start:.1f} s)"}
+    cores = host_cores()
+    t0 = time.perf_counter()
+    times, threads = CT.time_trials([(t.nb_filters, t.kernel_size, t.pool_size, t.dense) for t in trials],
+                                    concurrent=concurrent, cores=cores, steps=steps, val=val, warmup=1)
+    return times, cores, threads, time.perf_counter() - t0
+
+
+def cpu_baseline_train(trials, n_sample=32, concurrent=4):
+    """torch-CPU fp32 single-trial training (BASELINE.md:45-52), 4 trials at once
+    with cores//4 threads each, timed on a bounded sample of steps of the first
+    ``n_sample`` trials and extrapolated to whole trials (5-fold, 10 epochs, 60k
+    samples: 24 000 train steps + 6 000 validation batches)."""
+    sample = trials[:n_sample]
+    times, cores, threads, wall = torch_cpu_trial_seconds(sample, concurrent)
+    sec = [24000 * ts + 6000 * tv for ts, tv in times]
+    value = concurrent * 3600.0 / float(np.mean(sec))
+    return {"value": value, "unit": "trials/hour", "cores": cores, "kind": "port",
+            "sample": f"torch-CPU fp32 restatement (oracle/cnn_torch.py): {len(sample)} of the trials, {concurrent} "
+                      f"at once x {threads} threads, 3 train steps + 1 validation batch each (batch 100), "
+                      f"extrapolated to 24000 train steps + 6000 validation batches per trial ({wall:.1f} s)"}
 
 
 def bench_train(args, torch, dist, ws, rank, dev):
@@ -360,40 +374,23 @@ def bench_train(args, torch, dist, ws, rank, dev):
     }
 
 
-def cpu_baseline_densenet(budget_s=10.0, B=20):
-    """fp64 numpy restatement (oracle/densenet.py) of one DenseNet trial on the
-    host: one train step + one validation batch at batch B, scaled linearly to
-    batch 100 and extrapolated to a whole trial (10 epochs x (350 train + 150
-    validation batches))."""
-    from oracle import densenet as od
+def cpu_baseline_densenet(n_sample=4, concurrent=4):
+    """torch-CPU fp32 DenseNet (oracle/densenet_torch.py, the reference grid
+    architecture) at batch 100, 4 trials at once with cores//4 threads each:
+    2 train steps + 1 validation batch per trial, extrapolated to a whole trial
+    (10 epochs x (350 train + 150 validation batches))."""
+    from oracle import densenet_torch as DT
 
-    layers = od.arch_layers()
-    rng = np.random.RandomState(0)
-    x = rng.uniform(size=(B, 32, 32, 3))
-    y = rng.randint(0, 10, size=B)
-    t_start = time.perf_counter()
-    t_tr = t_ev = 0.0
-    n = 0
-    while True:
-        p, s = od.he_uniform_init(layers, n)
-        o = od.DenseNetOracle(layers, p, s)
-        t0 = time.perf_counter()
-        o.train_step(x, y)
-        t1 = time.perf_counter()
-        o.eval_batch(x, y)
-        t2 = time.perf_counter()
-        t_tr += t1 - t0
-        t_ev += t2 - t1
-        n += 1
-        if time.perf_counter() - t_start > budget_s:
-            break
-    scale = 100.0 / B
-    sec_per_trial = 10 * (350 * t_tr * scale + 150 * t_ev * scale) / n
-    cores = int(os.environ.get("OMP_NUM_THREADS", len(os.sched_getaffinity(0))))
-    return {"value": 3600.0 / sec_per_trial, "unit": "trials/hour", "cores": cores, "kind": "port",
-            "sample": f"{n} x (1 train step + 1 validation batch) at batch {B}, fp64 numpy restatement "
-                      f"(oracle/densenet.py, BLAS threads = {cores}), scaled to batch 100 and extrapolated to "
-                      f"3500 train steps + 1500 validation batches per trial ({time.perf_counter() - t_start:.1f} s)"}
+    cores = host_cores()
+    t0 = time.perf_counter()
+    times, threads = DT.time_trials(n_sample, concurrent=concurrent, cores=cores, steps=2, val=1, warmup=1)
+    wall = time.perf_counter() - t0
+    sec = [10 * (350 * ts + 150 * tv) for ts, tv in times]
+    return {"value": concurrent * 3600.0 / float(np.mean(sec)), "unit": "trials/hour", "cores": cores,
+            "kind": "port",
+            "sample": f"torch-CPU fp32 restatement (oracle/densenet_torch.py): {n_sample} trials, {concurrent} at once "
+                      f"x {threads} threads, 2 train steps + 1 validation batch at batch 100 each, extrapolated to "
+                      f"3500 train steps + 1500 validation batches per trial ({wall:.1f} s)"}
 
 
 def bench_densenet(args, torch, dist, ws, rank, dev):
@@ -468,12 +465,82 @@ def bench_densenet(args, torch, dist, ws, rank, dev):
     }
 
 
+SEARCH_ARGV = ["--world-size", "21", "--block-size", "5", "--epochs", "10", "--num-iterations", "10",
+               "--n-fold", "5", "--n-samples", "60000"]
+
+
+def bench_search(args, torch, dist, ws, rank, dev):
+    """BASELINE configs[0], measured end to end: the option3 search
+    ``-n 21 --block-size 5 --epochs 10 --num-iterations 10 --n-fold 5`` on 60k
+    synthetic MNIST-shape samples, through the build's scheduler, the device
+    Optimizer and the population engine (the in-flight tail is trained too, as
+    the reference's blocks finish theirs).  Reports the measured trials/hour and
+    the wall time split into optimizer (ask/tell) and training."""
+    import tempfile
+
+    from mpi_opt_amd import search
+
+    a = search.make_parser().parse_args(SEARCH_ARGV + list(args.search_args or []))
+    with tempfile.TemporaryDirectory() as tmp:
+        a.checkpoint = os.path.join(tmp, "coordinator.pkl")
+        if ws > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        rep = search.run_search(a, log=lambda *m: print(*m, file=sys.stderr, flush=True))
+        torch.cuda.synchronize(dev)
+        if ws > 1:
+            dist.barrier()
+        wall = time.perf_counter() - t0
+    if rank != 0:
+        return None
+    out = {"metric": "MNIST-CNN trials/hour, measured search (BASELINE configs[0])",
+           "value": rep["trials_trained"] * 3600.0 / wall, "unit": "trials/hour", "n_gpus": ws,
+           "wall_s": wall, "scaling": "strong", "dtype": "f32",
+           "config": {"workload": "option3 search " + " ".join(SEARCH_ARGV + list(args.search_args or [])),
+                      "num_blocks": rep["num_blocks"], "populations": rep["populations"],
+                      "parallelism": f"(trial, fold) units LPT-sharded over {ws} GPU(s)"},
+           "trials_trained": rep["trials_trained"], "trials_told": rep["trials_told"],
+           "split_s": {"optimizer_ask": rep["ask_s"], "optimizer_tell": rep["tell_s"], "training": rep["train_s"],
+                       "other": wall - rep["ask_s"] - rep["tell_s"] - rep["train_s"]},
+           "asks": rep["asks"], "tells": rep["tells"], "best_fom": rep["best_fom"],
+           "_trained_params": rep["trained_params"], "_num_blocks": rep["num_blocks"]}
+    return out
+
+
+def cpu_baseline_search(search_out, concurrent=4):
+    """The same trials on the host the way the reference runs them: torch-CPU fp32
+    single-trial training, ``num_blocks`` trials at once (cores // num_blocks
+    threads each), launched in the search's order onto the first free block;
+    per-trial time from a bounded sample of steps (3 train + 1 validation)."""
+    from mpi_opt_amd.population import TrialSpec
+
+    params = search_out.pop("_trained_params")
+    nb = search_out.pop("_num_blocks")
+    trials = [TrialSpec(nb_filters=int(p[0]), pool_size=int(p[1]), kernel_size=int(p[2]), dense=int(p[3]))
+              for p in params]
+    times, cores, threads, wall = torch_cpu_trial_seconds(trials, concurrent=nb)
+    sec = [24000 * ts + 6000 * tv for ts, tv in times]
+    free = [0.0] * nb
+    for t in sec:                            # list schedule in launch order
+        j = int(np.argmin(free))
+        free[j] += t
+    makespan = max(free)
+    return {"value": len(trials) * 3600.0 / makespan, "unit": "trials/hour", "cores": cores, "kind": "port",
+            "sample": f"the search's {len(trials)} trials, torch-CPU fp32 (oracle/cnn_torch.py), {nb} at once x "
+                      f"{threads} threads, 3 train steps + 1 validation batch each, extrapolated to 24000 + 6000 "
+                      f"per trial and list-scheduled onto {nb} blocks: makespan {makespan / 3600:.2f} h "
+                      f"({wall:.1f} s); the GP is not reached (n_initial_points = 10)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="all", choices=["ei", "fit", "train", "densenet", "all"])
+    ap.add_argument("--workload", default="all", choices=["ei", "fit", "train", "densenet", "search", "all"])
+    ap.add_argument("--search-args", nargs="*", default=None,
+                    help="extra search CLI flags appended to configs[0]'s (e.g. --n-samples 6000)")
     ap.add_argument("--candidates", type=int, default=1_000_000)
     ap.add_argument("--train-trials", type=int, default=64)
     ap.add_argument("--train-steps", type=int, default=5)
@@ -501,8 +568,16 @@ def main():
         fit = bench_gp_fit(args, torch, dev, ws == 1 and not args.no_cpu_baseline)
     train = bench_train(args, torch, dist, ws, rank, dev) if args.workload in ("train", "all") else None
     dn = bench_densenet(args, torch, dist, ws, rank, dev) if args.workload in ("densenet", "all") else None
+    srch = bench_search(args, torch, dist, ws, rank, dev) if args.workload in ("search", "all") else None
     if rank == 0:
         cpu = ws == 1 and not args.no_cpu_baseline
+        if srch is not None:
+            if cpu:
+                srch["cpu_baseline"] = cpu_baseline_search(srch)
+            else:
+                srch.pop("_trained_params")
+                srch.pop("_num_blocks")
+                srch["cpu_baseline"] = None
         if train is not None:
             trials = train.pop("_trials")
             train["cpu_baseline"] = cpu_baseline_train(trials) if cpu else None
@@ -516,8 +591,10 @@ def main():
                 res["train"] = train
             if dn is not None:
                 res["densenet"] = dn
+            if srch is not None:
+                res["search"] = srch
         else:
-            res = train if train is not None else (dn if dn is not None else fit)
+            res = next(r for r in (train, dn, srch, fit) if r is not None)
         print(json.dumps(res), flush=True)
     if ws > 1:
         dist.barrier()

@@ -206,6 +206,7 @@ class PopulationComm:
         self.exited = set()
         self.busy = set()        # launched blocks whose result has not been collected
         self.batches = []        # sizes of the populations trained
+        self.trained_params = [] # parameters of every trial trained, in training order
         self.tail = []           # (params, fom) of trials trained after the exit broadcast (never told)
 
     def Get_size(self):
@@ -241,6 +242,7 @@ class PopulationComm:
         params = [self.pending.pop(b) for b in blocks]
         foms = self.evaluator.evaluate(params)
         self.batches.append(len(params))
+        self.trained_params.extend(params)
         for b, f in zip(blocks, foms):
             self.results[b] = f
 

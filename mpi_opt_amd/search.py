@@ -121,6 +121,7 @@ def run_search(args, x=None, y=None, log=print):
         "trials_trained": comm.trials_trained,
         "trials_told": len(state.fom_list),
         "populations": list(comm.batches),
+        "trained_params": [list(p) for p in comm.trained_params],
         "num_blocks": num_blocks,
         "optimizer_s": tm["ask_s"] + tm["tell_s"],
         "ask_s": tm["ask_s"], "tell_s": tm["tell_s"], "asks": tm["asks"], "tells": tm["tells"],

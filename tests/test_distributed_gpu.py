@@ -1,0 +1,72 @@
+"""DistributedEvaluator with the REAL device TrialEvaluator on the GPU box: two
+ranks share cuda:0 over a gloo group (the node's 8-GPU launch is the driver's;
+RCCL is the same code path with backend "nccl").  Rank 0 broadcasts each batch,
+both ranks train their LPT shard of (trial, fold) units as device populations,
+the histories are all-gathered -- and the FOMs are bit-identical to one process
+training everything (unit seeds depend only on the unit; population isolation).
+Reference: /root/reference/hyperparameter_search_option3.py:172-205,
+coordinator.py:140-150."""
+import os
+import socket
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+BATCHES = [[[10, 2, 2, 50, 0.1], [50, 5, 3, 200, 0.2], [30, 3, 4, 100, 0.5]], [[12, 2, 3, 60, 0.0], [40, 9, 2, 70, 0.3]]]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _evaluator():
+    from mpi_opt_amd.blocks import TrialEvaluator
+    from mpi_opt_amd.models import BuilderFromFunction, mnist_space
+    from mpi_opt_amd.models import test_mnist as mnist_fn
+    from mpi_opt_amd.population import synthetic_mnist
+
+    x, y = synthetic_mnist(1000, seed=1, device="cuda:0")
+    return TrialEvaluator(BuilderFromFunction(mnist_fn, mnist_space()), x, y, n_fold=2, epochs=1, device="cuda:0")
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from mpi_opt_amd.blocks import DistributedEvaluator
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ev = DistributedEvaluator(_evaluator())
+    if rank == 0:
+        out = [ev.evaluate(b) for b in BATCHES]
+        ev.shutdown()
+        q.put((out, ev.local.n_evaluated))
+    else:
+        ev.serve()
+        q.put(("served", len(ev.local.units(BATCHES[0]))))
+    dist.destroy_process_group()
+
+
+def test_two_ranks_on_one_gpu_match_single_process():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    dist_out = next(g for g in got if g[0] != "served")
+    single = _evaluator()
+    want = [single.evaluate(b) for b in BATCHES]
+    assert dist_out[0] == want
+    assert dist_out[1] == sum(len(b) for b in BATCHES)

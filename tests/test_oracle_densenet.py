@@ -95,3 +95,31 @@ def test_bn_moving_stats_and_eval_mode():
     np.testing.assert_allclose(o.state[f"mv{i}"], 0.99 + 0.01 * c[i][1]["var"])
     s, correct = o.eval_batch(x, y)
     assert np.isfinite(s) and 0 <= correct <= 4
+
+
+def test_torch_cpu_baseline_trajectory_matches_oracle():
+    """oracle/densenet_torch.py (the timed CPU baseline) trains the same network:
+    fp64 to 1e-10 of the oracle over 3 Adam steps, fp32 within 1e-3."""
+    from oracle import densenet_torch as dt
+
+    layers = od.arch_layers(img_dim=(12, 10, 3), nb_classes=5, depth=10, nb_dense_block=2, growth_rate=4,
+                            nb_filter=6)
+    params, state = od.he_uniform_init(layers, seed=2)
+    rng = np.random.RandomState(4)
+    x = rng.rand(4, 12, 10, 3)
+    y = rng.randint(0, 5, size=4)
+    o = od.DenseNetOracle(layers, params, state, lr=1e-2)
+    n64 = dt.TorchDenseNet(layers, params, state, lr=1e-2, dtype=torch.float64)
+    n32 = dt.TorchDenseNet(layers, params, state, lr=1e-2)
+    for _ in range(3):
+        ref = o.train_step(x, y)
+        l64 = n64.train_step(torch.tensor(x), torch.tensor(y))
+        l32 = n32.train_step(torch.tensor(x, dtype=torch.float32), torch.tensor(y))
+        assert abs(l64 - ref) <= 1e-10 * abs(ref)
+        assert abs(l32 - ref) <= 1e-3 * abs(ref)
+    for i, ly in enumerate(layers):
+        if ly["kind"] != "conv0":
+            np.testing.assert_allclose(n64.S[f"mm{i}"].numpy(), o.state[f"mm{i}"], rtol=1e-9, atol=1e-12)
+    s64, c64 = n64.eval_batch(torch.tensor(x), torch.tensor(y))
+    s_ref, c_ref = o.eval_batch(x, y)
+    assert abs(s64 - s_ref) <= 1e-9 * abs(s_ref) and c64 == c_ref

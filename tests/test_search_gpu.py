@@ -41,3 +41,29 @@ def test_evaluator_is_deterministic():
     b = ev.foms(params, res)
     assert a == b
     assert all(0.0 < f < 1.0 for f in a)
+
+
+def test_configs0_search_shape(tmp_path, monkeypatch):
+    """BASELINE configs[0]'s layout -- `-n 21 --block-size 5 --n-fold 5
+    --num-iterations 10` -- end to end on reduced data (3000 samples, 2 epochs;
+    the full 60k x 10-epoch run is bench.py's `search` leg).  4 blocks train as
+    populations of 4, 4 and the 2-trial tail; 6 results are told (the reference
+    leaves the last num_blocks trials untold); every trained trial writes its
+    history JSON."""
+    from mpi_opt_amd import search
+
+    monkeypatch.chdir(tmp_path)
+    random.seed(0)
+    args = search.make_parser().parse_args(
+        ["--world-size", "21", "--block-size", "5", "--epochs", "2", "--num-iterations", "10", "--n-fold", "5",
+         "--n-samples", "3000", "--history-dir", str(tmp_path / "hist")])
+    rep = search.run_search(args)
+    assert rep["num_blocks"] == 4
+    assert rep["populations"] == [4, 4, 2]
+    assert rep["trials_trained"] == 10 and rep["trials_told"] == 6
+    assert rep["train_s"] > 0 and rep["optimizer_s"] >= 0
+    files = list((tmp_path / "hist").iterdir())
+    assert len(files) == 10
+    doc = json.loads(files[0].read_text())
+    assert len(doc["history"]) == 5 and len(doc["history"]["0"]["val_loss"]) == 2
+    assert doc["history"]["0"]["dropped_train_samples"] == 0

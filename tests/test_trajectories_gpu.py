@@ -1,0 +1,123 @@
+"""Long-trajectory parity of the device populations against the fp64 oracles
+(fixture tests/golden/trajectories.npz, made by make_trajectory_golden.py from
+oracle/cnn.py and oracle/densenet.py on identical init, data order and dropout
+masks).  Bar: the north_star's per-step training loss within 1e-3 relative.
+
+* configs[2]: the whole 64-trial x 5-fold = 320-member ragged population (per-
+  trial widths, lr 10**U(-4,-2), dropout U(0, .5)) is built and stepped on one
+  GPU -- every (NT, MT) bucket of that plan runs -- and 8 sampled members are
+  checked for 20 steps plus a validation pass; two of them are also trained
+  alone and must end bit-identical (population isolation);
+* one full 5-fold fold-epoch (480 steps on 48 000 samples) + the fold's whole
+  validation pass, 2 members;
+* DenseNet at the configs[4] geometry and batch 100, 20 steps + an
+  inference-mode validation batch.
+
+The observed max relative drifts are printed (recorded in DESIGN.md §4)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests import trajectory_cases as T
+from tests.conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+G = np.load(os.path.join(GOLDEN, "trajectories.npz"))
+
+
+def _engine(members):
+    from mpi_opt_amd.population import PopulationEngine, TrialSpec, glorot_uniform_init
+
+    specs = [TrialSpec(F, k, p, d, lr, dr, seed=ds) for (F, k, p, d, lr, dr, _, ds, _) in members]
+    init = [glorot_uniform_init(s, m[8]) for s, m in zip(specs, members)]
+    return PopulationEngine(specs, batch=T.BATCH, init=init)
+
+
+def _orders(members, n, k):
+    from mpi_opt_amd.population import kfold_split
+
+    tr = np.stack([kfold_split(n, k, m[6])[0] for m in members])
+    va = np.stack([kfold_split(n, k, m[6])[1] for m in members])
+    return torch.from_numpy(tr).cuda(), torch.from_numpy(va).cuda()
+
+
+def test_population_320_members_configs2():
+    members = T.pop_members()
+    picks = list(G["pop_picks"])
+    assert picks == T.pop_sampled()
+    x, y = T.pop_data()
+    xd, yd = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    eng = _engine(members)
+    otr, ova = _orders(members, T.POP_SAMPLES, T.POP_FOLDS)
+    spe = otr.shape[1] // T.BATCH
+    got = []
+    for st in range(T.POP_STEPS):
+        got.append(eng.train_step(xd, yd, otr, (st % spe) * T.BATCH).cpu().numpy()[picks])
+    got = np.array(got).T
+    ref = G["pop_train_loss"]
+    rel = np.abs(got - ref) / np.abs(ref)
+    print("configs[2] 320 members: max rel train-loss drift over 20 steps per sampled member",
+          np.array2string(rel.max(1), precision=2))
+    assert np.isfinite(got).all() and rel.max() < 1e-3, rel.max(1)
+    eng.eval_reset()
+    for vb in range(2):
+        eng.eval_step(xd, yd, ova, vb * T.BATCH)
+    val = eng.val_loss_sum.cpu().numpy()[picks] / (2 * T.BATCH)
+    relv = np.abs(val - G["pop_val_loss"]) / np.abs(G["pop_val_loss"])
+    print("configs[2] validation rel drift", np.array2string(relv, precision=2))
+    assert relv.max() < 1e-3
+    # isolation: sampled members trained alone end bit-identical
+    full = eng.params.cpu()
+    for i in (picks[2], picks[6]):
+        solo = _engine([members[i]])
+        o1, _ = _orders([members[i]], T.POP_SAMPLES, T.POP_FOLDS)
+        for st in range(T.POP_STEPS):
+            solo.train_step(xd, yd, o1, (st % spe) * T.BATCH)
+        solo_p = solo.params.cpu()
+        for name, (off, shape) in eng._slices(i).items():
+            cnt = int(np.prod(shape))
+            so, _ = solo._slices(0)[name]
+            assert torch.equal(full[off:off + cnt], solo_p[so:so + cnt]), (i, name)
+
+
+def test_full_fold_epoch_trajectory():
+    members = T.EPOCH_MEMBERS
+    x, y = T.epoch_data()
+    xd, yd = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    eng = _engine(members)
+    h = eng.fit_folds(xd, yd, [m[6] for m in members], T.EPOCH_FOLDS, 1, record_train_loss=True)
+    assert h["steps_per_epoch"] == 480 and h["val_batches"] == 120
+    ref = G["epoch_train_loss"]
+    rel = np.abs(h["train_loss"] - ref) / np.abs(ref)
+    relv = np.abs(h["val_loss"][:, 0] - G["epoch_val_loss"]) / np.abs(G["epoch_val_loss"])
+    print("fold-epoch (480 steps): max rel train-loss drift", np.array2string(rel.max(1), precision=2),
+          "validation", np.array2string(relv, precision=2))
+    assert rel.max() < 1e-3 and relv.max() < 1e-3
+
+
+def test_densenet_batch100_trajectory():
+    from mpi_opt_amd.densenet import DenseNetArch, DenseNetPopulation, he_uniform_init
+    from oracle import densenet as OD
+
+    layers = OD.arch_layers()
+    init = [he_uniform_init(layers, 300 + i) for i in range(len(T.DN_LRS))]
+    pop = DenseNetPopulation(DenseNetArch(), T.DN_LRS, batch=T.BATCH, init=init)
+    x, y, order = T.dn_data()
+    xd, yd, od_ = (torch.from_numpy(a).cuda() for a in (x, y, order))
+    got = np.array([pop.train_step(xd, yd, od_, st * T.BATCH).cpu().numpy() for st in range(T.DN_STEPS)]).T
+    ref = G["dn_train_loss"]
+    rel = np.abs(got - ref) / np.abs(ref)
+    pop.eval_reset()
+    pop.eval_step(xd, yd, od_, 1500)
+    vs = pop.val_loss_sum.cpu().numpy()
+    vc = pop.val_correct.cpu().numpy()
+    relv = np.abs(vs - G["dn_val_sum"]) / np.abs(G["dn_val_sum"])
+    print("DenseNet batch 100, 20 steps: max rel train-loss drift", np.array2string(rel.max(1), precision=2),
+          "validation", np.array2string(relv, precision=2), "hits", vc, G["dn_val_correct"])
+    assert rel.max() < 1e-3 and relv.max() < 1e-3
+    assert np.abs(vc - G["dn_val_correct"]).max() <= 1   # an argmax near-tie may flip in f32
+    for i in range(len(T.DN_LRS)):
+        np.testing.assert_allclose(pop.get_state(i)["mm1"], G["dn_mm1"][i], rtol=1e-3, atol=1e-5)
