@@ -8,6 +8,8 @@ compare the device populations against these numbers).
             steps each + one validation batch pair (oracle/cnn.py);
 * epoch:    2 members, one whole 5-fold fold-epoch (480 steps) + the fold's full
             validation pass (oracle/cnn.py);
+* epoch_fp32: the same 480 steps by torch-CPU fp32 (oracle/cnn_torch.py), the
+            envelope of fp32-vs-fp64 trajectory divergence;
 * densenet: 2 DenseNets at the configs[4] geometry, batch 100, 20 steps + one
             inference-mode validation batch (oracle/densenet.py).
 """
@@ -79,6 +81,31 @@ def make_epoch():
     return {"epoch_train_loss": np.array(losses), "epoch_val_loss": np.array(vals)}
 
 
+def make_epoch_fp32():
+    """The same fold-epoch trained by an INDEPENDENT fp32 implementation (torch
+    CPU autograd, oracle/cnn_torch.py, same init / order / masks): how far any
+    fp32 trajectory drifts from the fp64 one over 480 Adam steps."""
+    import torch
+
+    from oracle import cnn_torch as CT
+
+    x, y = T.epoch_data()
+    xt, yt = torch.from_numpy(x), torch.from_numpy(y)
+    losses = []
+    for m in T.EPOCH_MEMBERS:
+        F, k, p, d, lr, dr, fold, dseed, iseed = m
+        masks = lambda step, layer, n, rate, ds=dseed: C.dropout_keep(ds, step, layer, n, rate)  # noqa: E731
+        t = CT.TorchTrial(F, k, p, d, T.glorot_init(F, k, p, d, iseed), lr=lr, dropout=dr, mask_fn=masks)
+        tr, _ = kfold(T.EPOCH_SAMPLES, T.EPOCH_FOLDS, fold)
+        ls = []
+        for s in range(len(tr) // T.BATCH):
+            rows = torch.from_numpy(tr[s * T.BATCH:(s + 1) * T.BATCH].astype(np.int64))
+            ls.append(t.train_step(xt[rows], yt[rows], s))
+        losses.append(ls)
+        print("epoch member fp32 torch", m[:6], ls[0], "->", ls[-1], flush=True)
+    return {"epoch_train_loss_fp32": np.array(losses)}
+
+
 def make_densenet():
     from mpi_opt_amd.densenet import he_uniform_init  # init shared with the device side
 
@@ -105,9 +132,10 @@ def make_densenet():
 
 
 if __name__ == "__main__":
-    want = sys.argv[1:] or ["pop", "epoch", "densenet"]
+    want = sys.argv[1:] or ["pop", "epoch", "epoch_fp32", "densenet"]
     data = dict(np.load(OUT)) if os.path.exists(OUT) else {}
     for w in want:
-        data.update({"pop": make_pop, "epoch": make_epoch, "densenet": make_densenet}[w]())
+        data.update({"pop": make_pop, "epoch": make_epoch, "epoch_fp32": make_epoch_fp32,
+                     "densenet": make_densenet}[w]())
         np.savez(OUT, **data)
     print("wrote", OUT, sorted(data))

@@ -45,7 +45,7 @@ def _worker(rank, world, port, q):
     if rank == 0:
         out = [ev.evaluate(b) for b in BATCHES]
         ev.shutdown()
-        q.put((out, ev.local.n_evaluated))
+        q.put((out, ev.n_evaluated))
     else:
         ev.serve()
         q.put(("served", len(ev.local.units(BATCHES[0]))))

@@ -60,7 +60,7 @@ def test_population_320_members_configs2():
     ref = G["pop_train_loss"]
     rel = np.abs(got - ref) / np.abs(ref)
     print("configs[2] 320 members: max rel train-loss drift over 20 steps per sampled member",
-          np.array2string(rel.max(1), precision=2))
+          np.array2string(rel.max(1), formatter={"float_kind": lambda v: "%.2e" % v}))
     assert np.isfinite(got).all() and rel.max() < 1e-3, rel.max(1)
     eng.eval_reset()
     for vb in range(2):
@@ -93,9 +93,21 @@ def test_full_fold_epoch_trajectory():
     ref = G["epoch_train_loss"]
     rel = np.abs(h["train_loss"] - ref) / np.abs(ref)
     relv = np.abs(h["val_loss"][:, 0] - G["epoch_val_loss"]) / np.abs(G["epoch_val_loss"])
-    print("fold-epoch (480 steps): max rel train-loss drift", np.array2string(rel.max(1), precision=2),
-          "validation", np.array2string(relv, precision=2))
-    assert rel.max() < 1e-3 and relv.max() < 1e-3
+    # an independent fp32 implementation (torch CPU) of the same 480 steps drifts
+    # from the fp64 oracle too: Adam's m/sqrt(v) turns last-bit differences of
+    # near-zero gradients into full-size updates, and the trajectories separate
+    # (3-4e-3 max over the fold-epoch, 1e-3 by step ~100).  The 1e-3 bar holds
+    # for the first 50 steps; beyond, the device must stay inside fp32's own envelope.
+    rel32 = np.abs(G["epoch_train_loss_fp32"] - ref) / np.abs(ref)
+    fmt = lambda a: np.array2string(np.asarray(a), formatter={"float_kind": lambda v: "%.2e" % v})  # noqa: E731
+    print("fold-epoch (480 steps) device vs fp64: max rel train-loss drift", fmt(rel.max(1)),
+          "median", fmt(np.median(rel, 1)), "first 50 steps", fmt(rel[:, :50].max(1)),
+          "| torch-CPU fp32 vs fp64: max", fmt(rel32.max(1)), "median", fmt(np.median(rel32, 1)),
+          "| validation", fmt(relv))
+    assert rel[:, :50].max() < 1e-3
+    assert (rel.max(1) <= np.maximum(1e-3, 1.5 * rel32.max(1))).all()
+    assert (np.median(rel, 1) <= 3 * np.median(rel32, 1)).all()
+    assert relv.max() < 1e-3
 
 
 def test_densenet_batch100_trajectory():
@@ -115,8 +127,9 @@ def test_densenet_batch100_trajectory():
     vs = pop.val_loss_sum.cpu().numpy()
     vc = pop.val_correct.cpu().numpy()
     relv = np.abs(vs - G["dn_val_sum"]) / np.abs(G["dn_val_sum"])
-    print("DenseNet batch 100, 20 steps: max rel train-loss drift", np.array2string(rel.max(1), precision=2),
-          "validation", np.array2string(relv, precision=2), "hits", vc, G["dn_val_correct"])
+    fmt = lambda a: np.array2string(np.asarray(a), formatter={"float_kind": lambda v: "%.2e" % v})  # noqa: E731
+    print("DenseNet batch 100, 20 steps: max rel train-loss drift", fmt(rel.max(1)), "validation", fmt(relv),
+          "hits", vc, G["dn_val_correct"])
     assert rel.max() < 1e-3 and relv.max() < 1e-3
     assert np.abs(vc - G["dn_val_correct"]).max() <= 1   # an argmax near-tie may flip in f32
     for i in range(len(T.DN_LRS)):
