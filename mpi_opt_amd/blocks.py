@@ -257,8 +257,54 @@ class PopulationComm:
         return sum(self.batches)
 
 
+def local_topk(payload, s0, s1, device=None):
+    """Score candidates [s0, s1) of a sharded acquisition request on this rank's
+    GPU; returns {acq: (values, global indices)} of the shard's lowest-index-first
+    top-k (skopt's ``np.argsort(values)[:k]`` restricted to the shard)."""
+    from .optimizer import GPModel
+
+    p = payload
+    k = min(int(p["k"]), s1 - s0)
+    est = GPModel(p["Xt"], p["y"], p["amp"], p["ls"], p["noise"], device=device)
+    top = _device_topk(est, p["cand"][s0:s1], p["y_opt"], tuple(p["acqs"]), p["xi"], p["kappa"], k)
+    return {a: (v, i + s0) for a, (v, i) in top.items()}
+
+
+def _device_topk(est, X, y_opt, acqs, xi, kappa, k):
+    import torch
+
+    from . import _lib
+
+    if k <= _lib.MPO_TOPK_MAX:
+        sc = est.dev.score(X, y_opt, acqs=acqs, xi=xi, kappa=kappa, k=k, want_mu_sd=False, want_values=False)
+        return {a: (sc["topk"][a][1].cpu().numpy(), sc["topk"][a][0].cpu().numpy()) for a in acqs}
+    sc = est.dev.score(X, y_opt, acqs=acqs, xi=xi, kappa=kappa, k=0, want_mu_sd=False, want_values=True)
+    out = {}
+    for a in acqs:
+        v, i = torch.sort(sc["values"][a], stable=True)
+        out[a] = (v[:k].cpu().numpy(), i[:k].cpu().numpy())
+    return out
+
+
+def merge_topk(parts, k):
+    """Global lowest-index-first top-k from per-shard lists [(values, indices)]:
+    lexicographic (value, index), exactly the single-device order."""
+    vals = np.concatenate([np.asarray(v, dtype=np.float64) for v, _ in parts])
+    idx = np.concatenate([np.asarray(i, dtype=np.int64) for _, i in parts])
+    order = np.lexsort((idx, vals))[:k]
+    return vals[order], idx[order]
+
+
 class DistributedEvaluator:
-    """Shards (trial, fold) units over torch.distributed ranks; rank 0 drives."""
+    """Shards work over torch.distributed ranks (one process per GPU); rank 0 drives.
+
+    Two kinds of rounds, announced by a broadcast from rank 0:
+    * ``("train", params)`` -- (trial, fold) units LPT-sharded by FLOPs, histories
+      all-gathered (SURVEY §8e);
+    * ``("score", request)`` -- the acquisition's candidates split M/W per rank,
+      each rank's (value, index) top-k all-gathered and merged lowest-index-first
+      (SURVEY §8e "EI"), used by :class:`ShardedScorer`.
+    """
 
     def __init__(self, local, group=None):
         import torch.distributed as dist
@@ -270,36 +316,78 @@ class DistributedEvaluator:
         self.world = dist.get_world_size(group)
         self.n_evaluated = 0
 
-    def _round(self, params_list):
-        dist = self.dist
-        box = [params_list]
-        dist.broadcast_object_list(box, src=0, group=self.group)
-        params_list = box[0]
-        if params_list is None:
-            return None
+    def _announce(self, msg):
+        box = [msg]
+        self.dist.broadcast_object_list(box, src=0, group=self.group)
+        return box[0]
+
+    def _gather(self, obj):
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj, group=self.group)
+        return out
+
+    def _train(self, params_list):
         units = self.local.units(params_list)
         owner = lpt_assign([u[3] for u in units], self.world)
         mine = [u for u, o in zip(units, owner) if o == self.rank]
         res = self.local.train_units(mine, seed_base=self.n_evaluated)
         self.n_evaluated += len(params_list)
-        gathered = [None] * self.world
-        dist.all_gather_object(gathered, {k: v for k, v in res.items()}, group=self.group)
         merged = {}
-        for g in gathered:
+        for g in self._gather({k: v for k, v in res.items()}):
             merged.update(g)
-        return params_list, merged
+        return merged
+
+    def _score(self, req):
+        m = len(req["cand"])
+        s0, s1 = self.rank * m // self.world, (self.rank + 1) * m // self.world
+        part = local_topk(req, s0, s1, device=self.local.device) if s1 > s0 else {}
+        parts = self._gather(part)
+        return {a: merge_topk([p[a] for p in parts if a in p], int(req["k"])) for a in req["acqs"]}
+
+    def _serve_one(self):
+        msg = self._announce(None)
+        if msg is None:
+            return False
+        kind, body = msg
+        if kind == "train":
+            self._train(body)
+        elif kind == "score":
+            self._score(body)
+        else:
+            raise ValueError(f"unknown round {kind!r}")
+        return True
 
     def evaluate(self, params_list):
         """Rank 0: evaluate a batch over all ranks."""
-        out = self._round(list(params_list))
-        params_list, merged = out
-        return self.local.foms(params_list, merged)
+        params_list = [list(p) for p in params_list]
+        self._announce(("train", params_list))
+        return self.local.foms(params_list, self._train(params_list))
+
+    def score(self, req):
+        """Rank 0: a sharded acquisition request -> {acq: (values, indices)} top-k."""
+        self._announce(("score", req))
+        return self._score(req)
 
     def serve(self):
-        """Ranks > 0: train shards until rank 0 sends None."""
-        while self._round(None) is not None:
+        """Ranks > 0: serve rounds until rank 0 sends None."""
+        while self._serve_one():
             pass
 
     def shutdown(self):
         if self.rank == 0:
-            self._round(None)
+            self._announce(None)
+
+
+class ShardedScorer:
+    """Optimizer acquisition scoring split over the ranks of a
+    :class:`DistributedEvaluator` (the candidate batch M/W per GPU, then a global
+    lowest-index top-k); plugs into ``Optimizer(scorer=...)``.  Not pickled."""
+
+    def __init__(self, dist_eval):
+        self.dist_eval = dist_eval
+
+    def __call__(self, est, X, y_opt, acqs, xi, kappa, k):
+        req = {"Xt": est.Xt, "y": est.y, "amp": est.amp, "ls": est.length_scale, "noise": est.noise,
+               "cand": np.ascontiguousarray(X, dtype=np.float64), "y_opt": float(y_opt), "acqs": list(acqs),
+               "xi": float(xi), "kappa": float(kappa), "k": int(k)}
+        return {a: idx for a, (vals, idx) in self.dist_eval.score(req).items()}

@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <string>
 
 namespace {
 
@@ -74,15 +75,25 @@ __device__ __forceinline__ void wave_lex_min(double& v, long long& i) {
 }
 
 // ---------------------------------------------------------------------------
-__global__ void scale_rows_kernel(const double* __restrict__ X, int n, int d, int dp,
+// Rows [n, rows) are padding: a point 1e30 away in every real dimension, whose
+// Matern value underflows to exactly 0 (and alpha is 0 there), so the wave-tile
+// scoring kernel evaluates whole 32-observation groups without bounds checks.
+constexpr double kFarAway = 1e30;
+
+__global__ void scale_rows_kernel(const double* __restrict__ X, int n, int rows, int d, int dp,
                                   const double* __restrict__ ls, double* __restrict__ xs,
                                   double* __restrict__ ls_pad) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < n * dp) {
+    if (t < rows * dp) {
         const int i = t / dp, c = t % dp;
-        xs[t] = c < d ? X[(size_t)i * d + c] / ls[c] : 0.0;
+        xs[t] = c < d ? (i < n ? X[(size_t)i * d + c] / ls[c] : kFarAway) : 0.0;
     }
     if (ls_pad && t < dp) ls_pad[t] = t < d ? ls[t] : 1.0;
+}
+
+__global__ void zero_kernel(double* __restrict__ p, int n) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) p[t] = 0.0;
 }
 
 __global__ void kernel_matrix_kernel(const double* __restrict__ xs, int n, int dp, double amp,
@@ -193,7 +204,7 @@ __global__ void copy_kernel(const double* __restrict__ src, double* __restrict__
 // B-fragment stream of W^T (W = L^-1 lower): column tile jt of 16 columns needs
 // the k-steps ks < 4(jt+1) (rows i <= 16 jt + 15); lane l of k-step ks holds
 // W^T[4 ks + (l>>4)][16 jt + (l&15)] = W[16 jt + (l&15)][4 ks + (l>>4)].
-__host__ __device__ inline size_t wfrag_tile_base(int jt) { return (size_t)128 * jt * (jt + 1); }
+__host__ __device__ constexpr size_t wfrag_tile_base(int jt) { return (size_t)128 * jt * (jt + 1); }
 inline size_t wfrag_elems(int np16) { return wfrag_tile_base(np16 / 16) + 16 * 64; }  // + prefetch slack
 
 __global__ void pack_wfrag_kernel(const double* __restrict__ W, int n, int ldw, int T,
@@ -229,6 +240,58 @@ struct ScoreArgs {
     long long* part_idx;  // [nblocks][3][k]
     double* part_val;
 };
+
+// Posterior, acquisitions and the tile's top-k from mu_n = K* alpha and
+// q = ||L^-1 k*||^2 of one candidate per lane (``live`` lanes own a row).
+__device__ __forceinline__ void score_epilogue(const ScoreArgs& a, bool live, long long gm, double mu_n, double q,
+                                               long long part, int lane) {
+    const bool valid = live && gm < a.m;
+    double mu = 0.0, sd = 0.0, vei = 0.0, vpi = 0.0, vlcb = 0.0;
+    if (live) {
+        double var = a.amp - q;
+        if (var < 0.0) var = 0.0;
+        sd = sqrt(var) * a.y_std;
+        mu = a.y_std * mu_n + a.y_mean;
+        if (sd > 0.0) {
+            const double improve = a.y_opt - a.xi - mu;
+            const double scaled = improve / sd;
+            const double cdf = ndtr(scaled);
+            vei = -(improve * cdf + sd * norm_pdf(scaled));
+            vpi = -cdf;
+        } else {
+            vei = -0.0;
+            vpi = -0.0;
+        }
+        vlcb = mu - a.kappa * sd;
+    }
+    if (valid) {
+        if (a.mu) a.mu[gm] = mu;
+        if (a.sd) a.sd[gm] = sd;
+        if (a.vals) {
+            if (a.flags & MPO_ACQ_EI) a.vals[gm] = a.ei_positive ? -vei : vei;
+            if (a.flags & MPO_ACQ_PI) a.vals[a.m + gm] = vpi;
+            if (a.flags & MPO_ACQ_LCB) a.vals[2 * a.m + gm] = vlcb;
+        }
+    }
+    if (a.k > 0) {
+        const double inf = __builtin_huge_val();
+#pragma unroll
+        for (int acq = 0; acq < 3; ++acq) {
+            if (!(a.flags & (1u << acq))) continue;
+            double v = valid ? (acq == 0 ? vei : (acq == 1 ? vpi : vlcb)) : inf;
+            long long idx = valid ? gm : 0x7fffffffffffffffLL;
+            long long* pi = a.part_idx + ((size_t)part * 3 + acq) * a.k;
+            double* pv = a.part_val + ((size_t)part * 3 + acq) * a.k;
+            for (int r = 0; r < a.k; ++r) {
+                double bv = v;
+                long long bi = idx;
+                wave_lex_min(bv, bi);
+                if (lane == 0) { pv[r] = bv; pi[r] = bi; }
+                if (idx == bi) { v = inf; idx = 0x7fffffffffffffffLL; }
+            }
+        }
+    }
+}
 
 template <int BM, int DP, int OCC>
 __global__ __launch_bounds__(256, OCC) void gp_score_kernel(ScoreArgs a) {
@@ -364,53 +427,122 @@ __global__ __launch_bounds__(256, OCC) void gp_score_kernel(ScoreArgs a) {
     // ---- phase 3: posterior, acquisitions, block top-k (wave 0)
     if (wave != 0) return;
     const int row = lane;
-    const long long gm = m0 + row;
-    const bool valid = row < BM && gm < a.m;
-    double mu = 0.0, sd = 0.0, vei = 0.0, vpi = 0.0, vlcb = 0.0;
-    if (row < BM) {
-        const double q = red[0 * BM + row] + red[1 * BM + row] + red[2 * BM + row] + red[3 * BM + row];
-        double var = a.amp - q;
-        if (var < 0.0) var = 0.0;
-        sd = sqrt(var) * a.y_std;
-        mu = a.y_std * mu_n + a.y_mean;
-        if (sd > 0.0) {
-            const double improve = a.y_opt - a.xi - mu;
-            const double scaled = improve / sd;
-            const double cdf = ndtr(scaled);
-            vei = -(improve * cdf + sd * norm_pdf(scaled));
-            vpi = -cdf;
-        } else {
-            vei = -0.0;
-            vpi = -0.0;
-        }
-        vlcb = mu - a.kappa * sd;
-    }
-    if (valid) {
-        if (a.mu) a.mu[gm] = mu;
-        if (a.sd) a.sd[gm] = sd;
-        if (a.vals) {
-            if (a.flags & MPO_ACQ_EI) a.vals[gm] = a.ei_positive ? -vei : vei;
-            if (a.flags & MPO_ACQ_PI) a.vals[a.m + gm] = vpi;
-            if (a.flags & MPO_ACQ_LCB) a.vals[2 * a.m + gm] = vlcb;
-        }
-    }
-    if (a.k > 0) {
-        const double inf = __builtin_huge_val();
+    const double q = row < BM ? red[0 * BM + row] + red[1 * BM + row] + red[2 * BM + row] + red[3 * BM + row] : 0.0;
+    score_epilogue(a, row < BM, m0 + row, mu_n, q, blockIdx.x, lane);
+}
+
+// ---------------------------------------------------------------------------
+// gp_score_wave_kernel: one WAVE owns a 16-candidate tile end to end.
+//
+//   * the L^-1 B-fragment stream of the first TL column tiles is staged ONCE per
+//     workgroup into LDS (persistent grid: one 512-thread workgroup per CU, 8 waves =
+//     2 per SIMD); the remaining tiles stream from L2;
+//   * the loop runs over 4-k-step groups g: the Matern values of group g + 1 are
+//     computed (VALU) while group g's MFMAs run -- every column tile jt >= g takes
+//     4 MFMAs of group g into its own accumulator, so consecutive MFMAs are
+//     independent -- and column tile g is complete (its ||V_row||^2 added) after
+//     group g.  K* never leaves registers: lane l holds candidate l & 15 at
+//     observation 4 ks + (l >> 4), the v_mfma_f64_16x16x4 A-fragment layout.
+// T (column tiles = np16 / 16) is a template parameter, so every LDS offset is an
+// immediate and the T accumulators stay in registers.
+template <int T>
+__host__ __device__ constexpr int wave_lds_tiles_ct() {
+    int tl = 0;
+    while (tl < T && wfrag_tile_base(tl + 1) * sizeof(double) <= 160 * 1024) ++tl;
+    return tl;
+}
+
+template <int DP>
+__device__ __forceinline__ void matern_group(const ScoreArgs& a, const double* xb, const double* ab, const double (&c)[DP],
+                                             int g, double (&A)[4], double& mu_p) {
 #pragma unroll
-        for (int acq = 0; acq < 3; ++acq) {
-            if (!(a.flags & (1u << acq))) continue;
-            double v = valid ? (acq == 0 ? vei : (acq == 1 ? vpi : vlcb)) : inf;
-            long long idx = valid ? gm : 0x7fffffffffffffffLL;
-            long long* pi = a.part_idx + ((size_t)blockIdx.x * 3 + acq) * a.k;
-            double* pv = a.part_val + ((size_t)blockIdx.x * 3 + acq) * a.k;
-            for (int r = 0; r < a.k; ++r) {
-                double bv = v;
-                long long bi = idx;
-                wave_lex_min(bv, bi);
-                if (lane == 0) { pv[r] = bv; pi[r] = bi; }
-                if (idx == bi) { v = inf; idx = 0x7fffffffffffffffLL; }
-            }
+    for (int u = 0; u < 4; ++u) {
+        const int ks = 4 * g + u;
+        const double* xr = xb + 4 * ks * DP;
+        double r2 = 0.0;
+#pragma unroll
+        for (int q = 0; q < DP; ++q) {
+            const double d_ = c[q] - xr[q];
+            r2 += d_ * d_;
         }
+        const double kv = matern52(sqrt(r2), a.amp);
+        mu_p += kv * ab[4 * ks];
+        A[u] = kv;
+    }
+}
+
+template <int DP, int T>
+__global__ __launch_bounds__(512, 2) void gp_score_wave_kernel(ScoreArgs a, long long ntiles) {
+    constexpr int TL = wave_lds_tiles_ct<T>();
+    extern __shared__ __attribute__((aligned(16))) double bl[];   // wfrag tiles [0, TL)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    {
+        constexpr int nst = (int)wfrag_tile_base(TL);             // doubles, even
+        const double2* src = reinterpret_cast<const double2*>(a.wfrag);
+        double2* dst = reinterpret_cast<double2*>(bl);
+        for (int e = tid; e < nst / 2; e += 512) dst[e] = src[e];
+    }
+    __syncthreads();
+
+    const int row = lane & 15, grp = lane >> 4;
+    for (long long t = (long long)blockIdx.x * 8 + wave; t < ntiles; t += (long long)gridDim.x * 8) {
+        const long long m0 = t * 16;
+        const long long gm = m0 + row;
+        double c[DP];
+#pragma unroll
+        for (int q = 0; q < DP; ++q) c[q] = (gm < a.m && q < a.d) ? a.cand[gm * a.d + q] / a.ls[q] : 0.0;
+        // xs / alpha are padded to 32 rows (padding rows give K* = 0 exactly): no
+        // bounds checks.  Bases opaque per tile: no hoisting of per-k-step addresses.
+        const double* xb = a.xs + grp * DP;
+        const double* ab = a.alpha + grp;
+        const double* wb = a.wfrag + lane;
+        asm volatile("" : "+v"(xb), "+v"(ab), "+v"(wb));
+
+        f64x4 acc[T];
+#pragma unroll
+        for (int jt = 0; jt < T; ++jt) acc[jt] = f64x4{0.0, 0.0, 0.0, 0.0};
+        double sq[4] = {0.0, 0.0, 0.0, 0.0};
+        double mu_p = 0.0;
+        double A[4], An[4];
+        matern_group<DP>(a, xb, ab, c, 0, A, mu_p);
+#pragma unroll
+        for (int g = 0; g < T; ++g) {
+            if (g + 1 < T) matern_group<DP>(a, xb, ab, c, g + 1, An, mu_p);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                for (int jt = g; jt < T; ++jt) {
+                    const size_t off = wfrag_tile_base(jt) + (size_t)(4 * g + u) * 64;
+                    const double b = jt < TL ? bl[off + lane] : wb[off];
+                    acc[jt] = __builtin_amdgcn_mfma_f64_16x16x4f64(A[u], b, acc[jt], 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sq[r] += acc[g][r] * acc[g][r];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) A[u] = An[u];
+        }
+
+        // ---- reductions: ||V_row||^2 over the 16 column lanes, mu over the 4 k-groups
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            double v = sq[r];
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 4);
+            v += __shfl_xor(v, 8);
+            sq[r] = v;                       // row grp + 4 r, every lane of the group
+        }
+        mu_p += __shfl_xor(mu_p, 16);
+        mu_p += __shfl_xor(mu_p, 32);
+        // row R (< 16) lives in lane 16 (R & 3), register R >> 2
+        double q = 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const double v = __shfl(sq[r], 16 * (lane & 3));
+            if ((lane >> 2) == r) q = v;
+        }
+        score_epilogue(a, lane < 16, gm, mu_p, q, t, lane);
     }
 }
 
@@ -568,6 +700,73 @@ hipError_t launch_score_dp(int dp, int bm, const ScoreArgs& a, int nblocks, size
     return hipErrorInvalidValue;
 }
 
+// ---- wave-tile kernel dispatch ------------------------------------------------
+constexpr int kWaveTile = 16;
+
+bool wave_kernel_ok(int dp, int np16) {
+    const char* env = getenv("MPO_GP_KERNEL");
+    if (env && std::string(env) == "block") return false;
+    return dp <= 16 && np16 <= 256;
+}
+
+int device_cus() {
+    static thread_local int dev_cached = -1, cus = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (dev != dev_cached) {
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        dev_cached = dev;
+    }
+    return cus;
+}
+
+template <int DP, int T>
+hipError_t launch_wave(const ScoreArgs& a, long long ntiles, hipStream_t s) {
+    constexpr int TL = wave_lds_tiles_ct<T>();
+    const size_t lds = std::max<size_t>(wfrag_tile_base(TL) * sizeof(double), 16);
+    auto kern = gp_score_wave_kernel<DP, T>;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    const long long want = (ntiles + 7) / 8;
+    const int grid = (int)std::max<long long>(1, std::min<long long>(want, device_cus()));
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, a, ntiles);
+    return hipGetLastError();
+}
+
+template <int DP>
+hipError_t launch_wave_n(const ScoreArgs& a, long long ntiles, hipStream_t s) {
+    switch (a.T) {
+        case 1: return launch_wave<DP, 1>(a, ntiles, s);
+        case 2: return launch_wave<DP, 2>(a, ntiles, s);
+        case 3: return launch_wave<DP, 3>(a, ntiles, s);
+        case 4: return launch_wave<DP, 4>(a, ntiles, s);
+        case 5: return launch_wave<DP, 5>(a, ntiles, s);
+        case 6: return launch_wave<DP, 6>(a, ntiles, s);
+        case 7: return launch_wave<DP, 7>(a, ntiles, s);
+        case 8: return launch_wave<DP, 8>(a, ntiles, s);
+        case 9: return launch_wave<DP, 9>(a, ntiles, s);
+        case 10: return launch_wave<DP, 10>(a, ntiles, s);
+        case 11: return launch_wave<DP, 11>(a, ntiles, s);
+        case 12: return launch_wave<DP, 12>(a, ntiles, s);
+        case 13: return launch_wave<DP, 13>(a, ntiles, s);
+        case 14: return launch_wave<DP, 14>(a, ntiles, s);
+        case 15: return launch_wave<DP, 15>(a, ntiles, s);
+        case 16: return launch_wave<DP, 16>(a, ntiles, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_wave_dp(int dp, const ScoreArgs& a, long long ntiles, hipStream_t s) {
+    switch (dp) {
+        case 4: return launch_wave_n<4>(a, ntiles, s);
+        case 8: return launch_wave_n<8>(a, ntiles, s);
+        case 12: return launch_wave_n<12>(a, ntiles, s);
+        case 16: return launch_wave_n<16>(a, ntiles, s);
+    }
+    return hipErrorInvalidValue;
+}
+
 int trsm_cols_per_block(int n) {
     size_t cb = 64;
     while (cb > 1 && (size_t)n * cb * sizeof(double) > kMaxLds - 1024) cb >>= 1;
@@ -630,12 +829,13 @@ size_t mpo_gp_prepare_ws_bytes(int n, int d) {
     const int dp = pad_dims(d);
     if (n <= 0 || dp < 0) return 0;
     const int np16 = (n + 15) / 16 * 16;
+    const int np32 = (n + 31) / 32 * 32;
     mpo::WsCarver c(nullptr);
-    c.take<double>((size_t)n * dp);        // xs
+    c.take<double>((size_t)np32 * dp);     // xs (+ far-away padding rows)
     c.take<double>(dp);                    // ls_pad
     c.take<double>((size_t)n * n);         // L
     c.take<double>((size_t)n * n);         // W
-    c.take<double>(n);                     // alpha
+    c.take<double>(np32);                  // alpha (+ zero padding)
     c.take<double>(wfrag_elems(np16));     // wfrag
     c.take<int32_t>(4);                    // info
     return c.used + 256;
@@ -652,18 +852,22 @@ int mpo_gp_prepare(const double* X, const double* y_norm, int n, int d, const do
     MPO_CHECK_ARG(ws_bytes >= mpo_gp_prepare_ws_bytes(n, d), "mpo_gp_prepare: workspace too small (%zu < %zu)",
                   ws_bytes, mpo_gp_prepare_ws_bytes(n, d));
     const int np16 = (n + 15) / 16 * 16;
+    const int np32 = (n + 31) / 32 * 32;
     if (choose_bm(dp, np16) < 0) { mpo::set_error("mpo_gp_prepare: n=%d exceeds the LDS-resident scoring limit", n); return MPO_ENOTSUP; }
     hipStream_t s = static_cast<hipStream_t>(stream);
     mpo::WsCarver c(ws);
-    double* xs = c.take<double>((size_t)n * dp);
+    double* xs = c.take<double>((size_t)np32 * dp);
     double* ls_pad = c.take<double>(dp);
     double* L = c.take<double>((size_t)n * n);
     double* W = c.take<double>((size_t)n * n);
-    double* alpha = c.take<double>(n);
+    double* alpha = c.take<double>(np32);
     double* wfrag = c.take<double>(wfrag_elems(np16));
     int32_t* info = c.take<int32_t>(4);
 
-    hipLaunchKernelGGL(scale_rows_kernel, dim3((n * dp + 255) / 256), dim3(256), 0, s, X, n, d, dp, ls, xs, ls_pad);
+    hipLaunchKernelGGL(scale_rows_kernel, dim3((np32 * dp + 255) / 256), dim3(256), 0, s, X, n, np32, d, dp, ls, xs,
+                       ls_pad);
+    MPO_LAUNCH_CHECK();
+    hipLaunchKernelGGL(zero_kernel, dim3((np32 + 255) / 256), dim3(256), 0, s, alpha, np32);
     MPO_LAUNCH_CHECK();
     hipLaunchKernelGGL(kernel_matrix_kernel, dim3((n + 63) / 64, n), dim3(64), 0, s, xs, n, dp, amp,
                        noise + kJitter, L, n);
@@ -704,9 +908,8 @@ int mpo_gp_prepare(const double* X, const double* y_norm, int n, int d, const do
 
 size_t mpo_gp_score_ws_bytes(const MpoGpModel* model, int64_t m, int k) {
     if (!model || m <= 0 || k < 0 || k > MPO_TOPK_MAX) return 0;
-    const int bm = choose_bm(model->dp, model->np16);
-    if (bm < 0) return 0;
-    const int64_t nblocks = (m + bm - 1) / bm;
+    if (choose_bm(model->dp, model->np16) < 0) return 0;
+    const int64_t nblocks = (m + kWaveTile - 1) / kWaveTile;   // partial lists per 16-candidate tile (upper bound)
     const int kk = std::max(k, 1);
     mpo::WsCarver c(nullptr);
     c.take<long long>((size_t)nblocks * 3 * kk);
@@ -731,7 +934,8 @@ static int gp_score_impl(const MpoGpModel* model, const double* cand, int64_t m,
     MPO_CHECK_ARG(ws && ws_bytes >= mpo_gp_score_ws_bytes(model, m, k), "mpo_gp_acq_score: workspace too small");
     const int bm = choose_bm(model->dp, model->np16);
     if (bm < 0) { mpo::set_error("mpo_gp_acq_score: model too large"); return MPO_ENOTSUP; }
-    const int64_t nblocks64 = (m + bm - 1) / bm;
+    const bool wave = wave_kernel_ok(model->dp, model->np16);
+    const int64_t nblocks64 = wave ? (m + kWaveTile - 1) / kWaveTile : (m + bm - 1) / bm;
     MPO_CHECK_ARG(nblocks64 < (1LL << 31), "mpo_gp_acq_score: too many candidates");
     const int nblocks = (int)nblocks64;
     mpo::WsCarver c(ws);
@@ -766,8 +970,12 @@ static int gp_score_impl(const MpoGpModel* model, const double* cand, int64_t m,
     a.k = k;
     a.part_idx = part_idx;
     a.part_val = part_val;
-    const size_t lds = score_lds_bytes(bm, model->dp, model->np16);
-    MPO_HIP(launch_score_dp(model->dp, bm, a, nblocks, lds, s));
+    if (wave) {
+        MPO_HIP(launch_wave_dp(model->dp, a, nblocks64, s));
+    } else {
+        const size_t lds = score_lds_bytes(bm, model->dp, model->np16);
+        MPO_HIP(launch_score_dp(model->dp, bm, a, nblocks, lds, s));
+    }
     if (k > 0) {
         // stage 1: G groups of ~64 block-lists each; stage 2: one list
         const int chunk = std::max(64, (nblocks + kMergeGroups - 1) / kMergeGroups);
@@ -799,8 +1007,8 @@ int mpo_gp_ei_score(const MpoGpModel* model, const double* cand, int64_t m, doub
     MPO_CHECK_ARG(ws_bytes >= mpo_gp_score_ws_bytes(model, m, 1), "mpo_gp_ei_score: workspace too small");
     // top-1 of -EI lands in the tail of the workspace the score call does not use
     mpo::WsCarver c(ws);
-    const int bm = choose_bm(model->dp, model->np16);
-    const int64_t nblocks = (m + bm - 1) / bm;
+    if (choose_bm(model->dp, model->np16) < 0) { mpo::set_error("mpo_gp_ei_score: model too large"); return MPO_ENOTSUP; }
+    const int64_t nblocks = (m + kWaveTile - 1) / kWaveTile;   // the carve of mpo_gp_score_ws_bytes
     c.take<long long>((size_t)nblocks * 3);
     c.take<double>((size_t)nblocks * 3);
     c.take<long long>((size_t)kMergeGroups * 3);

@@ -148,7 +148,7 @@ class Optimizer:
     def __init__(self, dimensions, base_estimator="gp", n_random_starts=None, n_initial_points=10,
                  initial_point_generator="random", acq_func="gp_hedge", acq_optimizer="auto",
                  random_state=None, model_queue_size=None, acq_func_kwargs=None, acq_optimizer_kwargs=None,
-                 device=None, _gp_seed=None):
+                 device=None, _gp_seed=None, scorer=None):
         self.rng = check_random_state(random_state)
         self.space = Space(dimensions)
         if n_random_starts is not None:
@@ -181,6 +181,7 @@ class Optimizer:
         self._initial_samples = None
         self.model_queue_size = model_queue_size
         self.device = device
+        self.scorer = scorer
         self.cand_acq_funcs_ = ["EI", "LCB", "PI"] if acq_func == "gp_hedge" else [acq_func]
         if acq_func == "gp_hedge":
             self.gains_ = np.zeros(3)
@@ -194,7 +195,7 @@ class Optimizer:
                         initial_point_generator=self._initial_point_generator, acq_func=self.acq_func,
                         acq_optimizer=self.acq_optimizer, acq_func_kwargs=self.acq_func_kwargs,
                         acq_optimizer_kwargs=self.acq_optimizer_kwargs, random_state=random_state,
-                        device=self.device, _gp_seed=self._gp_seed)
+                        device=self.device, _gp_seed=self._gp_seed, scorer=self.scorer)
         opt._initial_samples = self._initial_samples
         if hasattr(self, "gains_"):
             opt.gains_ = np.copy(self.gains_)
@@ -300,16 +301,14 @@ class Optimizer:
     def _score_topk(self, est, X, y_opt, xi, kappa, k):
         """skopt's ``np.argsort(values)[:k]`` per acquisition (lowest index first on
         ties).  The device top-k holds up to MPO_TOPK_MAX entries; a larger
-        ``n_restarts_optimizer`` takes the full value rows and a stable sort."""
+        ``n_restarts_optimizer`` takes the full value rows and a stable sort.  With
+        a ``scorer`` (e.g. blocks.ShardedScorer) the candidates are split over GPUs."""
         acqs = tuple(self.cand_acq_funcs_)
-        if k <= _lib.MPO_TOPK_MAX:
-            scored = est.dev.score(X, y_opt, acqs=acqs, xi=xi, kappa=kappa, k=k, want_mu_sd=False,
-                                   want_values=False)
-            return {a: scored["topk"][a][0].cpu().numpy() for a in acqs}
-        import torch
+        if self.scorer is not None:
+            return self.scorer(est, X, y_opt, acqs, xi, kappa, k)
+        from .blocks import _device_topk
 
-        scored = est.dev.score(X, y_opt, acqs=acqs, xi=xi, kappa=kappa, k=0, want_mu_sd=False, want_values=True)
-        return {a: torch.sort(scored["values"][a], stable=True)[1][:k].cpu().numpy() for a in acqs}
+        return {a: idx for a, (vals, idx) in _device_topk(est, X, y_opt, acqs, xi, kappa, k).items()}
 
     def _result(self):
         if not self.yi:
@@ -327,4 +326,6 @@ class Optimizer:
         return self._result()
 
     def __getstate__(self):
-        return _copy.copy(self.__dict__)
+        d = _copy.copy(self.__dict__)
+        d["scorer"] = None          # a process-group handle is not checkpoint state
+        return d

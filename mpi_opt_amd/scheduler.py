@@ -37,10 +37,10 @@ PARAMS_TAG = tag_lookup("params")
 RESULT_TAG = tag_lookup("result")
 
 
-def default_optimizer(dimensions, random_state):
+def default_optimizer(dimensions, random_state, **kwargs):
     from .optimizer import Optimizer
 
-    return Optimizer(dimensions=dimensions, random_state=random_state)
+    return Optimizer(dimensions=dimensions, random_state=random_state, **kwargs)
 
 
 @dataclass
@@ -77,14 +77,14 @@ class AskTellScheduler:
     random_state = 13579            # coordinator.py:33
 
     def __init__(self, comm, num_blocks, dimensions, checkpoint="coordinator.pkl", target_fom=None,
-                 verbose=False):
+                 verbose=False, optimizer_kwargs=None):
         self.comm = comm
         self.num_blocks = int(num_blocks)
         self.dimensions = dimensions
         self.checkpoint = checkpoint
         self.target_fom = target_fom
         self.verbose = verbose
-        self.optimizer = type(self).optimizer_factory(dimensions, self.random_state)
+        self.optimizer = type(self).optimizer_factory(dimensions, self.random_state, **(optimizer_kwargs or {}))
         self.state = SearchState()
         self.inflight = {}          # block -> _Launch
         self.timings = {"ask_s": 0.0, "tell_s": 0.0, "poll_s": 0.0, "asks": 0, "tells": 0}

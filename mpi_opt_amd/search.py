@@ -55,6 +55,8 @@ def make_parser():
     p.add_argument("--lr", type=float, default=1e-3, help="Adam learning rate (mpi_learn default)")
     p.add_argument("--history-dir", default=None, help="write per-trial history JSON here")
     p.add_argument("--checkpoint", default="coordinator.pkl")
+    p.add_argument("--ei-candidates", type=int, default=10000,
+                   help="acquisition candidates per ask (skopt n_points); split over the GPUs when distributed")
     return p
 
 
@@ -78,7 +80,7 @@ def run_search(args, x=None, y=None, log=print):
 
     import torch
 
-    from .blocks import DistributedEvaluator, PopulationComm, TrialEvaluator
+    from .blocks import DistributedEvaluator, PopulationComm, ShardedScorer, TrialEvaluator
     from .models import BuilderFromFunction, mnist_space, test_mnist
     from .population import synthetic_mnist
     from .scheduler import AskTellScheduler
@@ -106,8 +108,11 @@ def run_search(args, x=None, y=None, log=print):
             evaluator.serve()
             return None
     comm = PopulationComm(num_blocks, args.block_size, evaluator)
+    opt_kw = {"device": dev, "acq_optimizer_kwargs": {"n_points": args.ei_candidates}}
+    if dist is not None:
+        opt_kw["scorer"] = ShardedScorer(evaluator)       # candidates split M/W over the GPUs
     sched = AskTellScheduler(comm, num_blocks, provider.parameters, checkpoint=args.checkpoint,
-                             target_fom=args.target_objective, verbose=args.verbose)
+                             target_fom=args.target_objective, verbose=args.verbose, optimizer_kwargs=opt_kw)
     if args.previous_state:
         sched.load(args.previous_state)
     t0 = time.perf_counter()

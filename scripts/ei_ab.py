@@ -1,4 +1,4 @@
-"""A/B the GP scoring variants (candidates per workgroup) in one process, interleaved."""
+"""A/B the GP scoring kernels (block-per-16-candidates vs wave-tile) in one process, interleaved."""
 import os
 import sys
 
@@ -13,10 +13,12 @@ X, y = synthetic.gp_problem(200, 10, 0)
 ls = np.array([16.2, 1.91, 1.65, 9.84, 1.84, 2.94, 2.45, 9.09, 8.13, 1.94])
 g = DeviceGP(X, y, 17.4955, ls, 0.0465)
 cand = torch.from_numpy(synthetic.gp_candidates(1_000_000, 10, seed=1)).cuda()
-res = {b: [] for b in ("32/1", "16/5", "16/6")}
+VARIANTS = {"block16/5": {"MPO_GP_KERNEL": "block", "MPO_GP_BM": "16", "MPO_GP_OCC": "5"},
+            "wave": {"MPO_GP_KERNEL": "wave"}}
+res = {b: [] for b in VARIANTS}
 for rnd in range(4):
     for b in res:
-        os.environ["MPO_GP_BM"], os.environ["MPO_GP_OCC"] = b.split("/")
+        os.environ.update(VARIANTS[b])
         g.score(cand, float(y.min()), k=0)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -27,4 +29,5 @@ for rnd in range(4):
         torch.cuda.synchronize()
         res[b].append(e0.elapsed_time(e1) / 5)
 for b, v in res.items():
-    print("BM/occ=%s  median %.3f ms  min %.3f ms" % (b, np.median(v), np.min(v)))
+    print("%-10s median %.3f ms  min %.3f ms  (%.1f%% of FP64 peak)" % (b, np.median(v), np.min(v),
+          100 * (200 * 201 + 200 * 42 + 30) * 1e6 / (np.median(v) * 1e-3) / 78.6e12))

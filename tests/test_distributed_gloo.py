@@ -44,6 +44,68 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _fake_local_topk(payload, s0, s1, device=None):
+    """Stands in for the device scoring: deterministic per-candidate values with ties."""
+    import numpy as np
+
+    out = {}
+    for j, acq in enumerate(payload["acqs"]):
+        v = np.round(payload["cand"][s0:s1].sum(1) * 4) / 4 - j      # coarse: many ties
+        order = np.lexsort((np.arange(s0, s1), v))[: min(payload["k"], s1 - s0)]
+        out[acq] = (v[order], order + s0)
+    return out
+
+
+def _score_worker(rank, world, port, q):
+    import numpy as np
+
+    from mpi_opt_amd import blocks
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    blocks.local_topk = _fake_local_topk
+    ev = DistributedEvaluator(CpuEval(BuilderFromFunction(mnist_model_fn, mnist_space()), None, None, n_fold=1))
+    if rank == 0:
+        cand = np.random.RandomState(0).uniform(size=(1001, 3))
+        req = {"cand": cand, "acqs": ["EI", "LCB"], "k": 6}
+        got = ev.score(req)
+        ev.evaluate(BATCHES[1])       # a training round after a scoring round
+        ev.shutdown()
+        q.put((cand, {a: (v.tolist(), i.tolist()) for a, (v, i) in got.items()}))
+    else:
+        ev.serve()
+    dist.destroy_process_group()
+
+
+def test_sharded_scoring_merges_to_the_global_topk():
+    """candidates split M/W per rank, per-rank (value, index) top-k
+    all-gathered, merged lowest-index-first = the single-device top-k, ties too."""
+    import numpy as np
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_score_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    cand, got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = _fake_local_topk({"cand": cand, "acqs": ["EI", "LCB"], "k": 6}, 0, len(cand))
+    for a in ("EI", "LCB"):
+        assert got[a][1] == want[a][1].tolist() and got[a][0] == want[a][0].tolist()
+
+
+def test_merge_topk_lexicographic():
+    import numpy as np
+
+    from mpi_opt_amd.blocks import merge_topk
+
+    v, i = merge_topk([(np.array([0.5, 1.0]), np.array([7, 2])), (np.array([0.5, 0.25]), np.array([3, 9]))], 3)
+    assert v.tolist() == [0.25, 0.5, 0.5] and i.tolist() == [9, 3, 7]
+
+
 def test_two_rank_gloo_matches_single_process():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -70,3 +70,70 @@ def test_two_ranks_on_one_gpu_match_single_process():
     want = [single.evaluate(b) for b in BATCHES]
     assert dist_out[0] == want
     assert dist_out[1] == sum(len(b) for b in BATCHES)
+
+
+TOLD = 12       # past n_initial_points = 10: the GP is fitted and the acquisition scored
+
+
+def _told_points():
+    import numpy as np
+
+    rng = np.random.RandomState(4)
+    X = [[int(rng.randint(10, 51)), int(rng.randint(2, 11)), int(rng.randint(2, 11)), int(rng.randint(50, 201)),
+          float(rng.uniform())] for _ in range(TOLD)]
+    y = [float(0.3 + 0.05 * np.sin(i)) for i in range(TOLD)]
+    return X, y
+
+
+def _opt(scorer=None):
+    from mpi_opt_amd.models import mnist_space
+    from mpi_opt_amd.optimizer import Optimizer
+
+    return Optimizer(mnist_space(), random_state=13579, device="cuda:0", scorer=scorer,
+                     acq_optimizer_kwargs={"n_points": 20000})
+
+
+def _opt_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from mpi_opt_amd.blocks import DistributedEvaluator, ShardedScorer
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ev = DistributedEvaluator(_evaluator())
+    if rank == 0:
+        opt = _opt(ShardedScorer(ev))
+        X, y = _told_points()
+        opt.tell(X, y)
+        nxt = opt.ask()
+        batch = opt.ask(3)
+        ev.shutdown()
+        q.put((list(nxt), [list(b) for b in batch]))
+    else:
+        ev.serve()
+        q.put("served")
+    dist.destroy_process_group()
+
+
+def test_sharded_optimizer_scoring_matches_single_gpu():
+    """The Optimizer's acquisition split over 2 ranks (ShardedScorer)
+    proposes exactly the single-GPU points: same tell history, same next point,
+    same cl_min batch."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_opt_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    dist_out = next(g for g in got if g != "served")
+    opt = _opt()
+    X, y = _told_points()
+    opt.tell(X, y)
+    assert dist_out[0] == list(opt.ask())
+    assert dist_out[1] == [list(b) for b in opt.ask(3)]
