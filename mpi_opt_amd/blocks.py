@@ -58,13 +58,14 @@ class TrialEvaluator:
     """Trains trials (parameter lists of ``model_provider``'s space) on one GPU."""
 
     def __init__(self, model_provider, x, y, n_fold=1, epochs=10, batch=100, lr=1e-3, device=None,
-                 history_dir=None, init_seed=0):
+                 history_dir=None, init_seed=0, holdout=None):
         self.model_provider = model_provider
         self.x, self.y = x, y
         self.n_fold, self.epochs, self.batch, self.lr = n_fold, epochs, batch, lr
         self.device = device
         self.history_dir = history_dir
         self.init_seed = init_seed
+        self.holdout = holdout      # training samples of the train_list files (None: 70 % of x)
         self.n_evaluated = 0
         self.train_s = 0.0          # wall seconds spent training populations (synchronised)
 
@@ -124,7 +125,8 @@ class TrialEvaluator:
             folds.append(f)
             init.append(glorot_uniform_init(s, uid))
         eng = PopulationEngine(specs, batch=self.batch, device=self.device, init=init)
-        return self._histories(units, eng.fit_folds(self.x, self.y, folds, self.n_fold, self.epochs))
+        return self._histories(units, eng.fit_folds(self.x, self.y, folds, self.n_fold, self.epochs,
+                                                      holdout=self.holdout))
 
     def _train_densenet(self, units, seed_base):
         from .densenet import DenseNetPopulation, he_uniform_init
@@ -135,7 +137,8 @@ class TrialEvaluator:
         folds = [u[1] for u in units]
         init = [he_uniform_init(layers, self._uid(seed_base, t, f)) for (t, f, _, _) in units]
         pop = DenseNetPopulation(arch, lrs, batch=self.batch, device=self.device, init=init)
-        return self._histories(units, pop.fit_folds(self.x, self.y, folds, self.n_fold, self.epochs))
+        return self._histories(units, pop.fit_folds(self.x, self.y, folds, self.n_fold, self.epochs,
+                                                      holdout=self.holdout))
 
     @staticmethod
     def _histories(units, hist):

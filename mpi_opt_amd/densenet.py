@@ -268,14 +268,14 @@ class DenseNetPopulation:
         return self._pen
 
     # -- full k-fold training -----------------------------------------------------
-    def fit_folds(self, x, labels, folds, n_fold, epochs, record_train_loss=False):
+    def fit_folds(self, x, labels, folds, n_fold, epochs, record_train_loss=False, holdout=None):
         """Train every member for ``epochs`` on its fold (in order, no shuffle),
         validating once per epoch; val_loss = mean CE + l2 penalty (Keras)."""
         n_samples = x.shape[0]
         B = self.batch
         tr, va = [], []
         for i in range(self.n):
-            t, v = kfold_split(n_samples, n_fold, int(folds[i]))
+            t, v = kfold_split(n_samples, n_fold, int(folds[i]), holdout)
             tr.append(t)
             va.append(v)
         n_tr = min(len(t) for t in tr)

@@ -88,16 +88,22 @@ def glorot_uniform_init(spec: TrialSpec, seed: int):
     return out
 
 
-def kfold_split(n_samples: int, n_fold: int, fold: int):
+def kfold_split(n_samples: int, n_fold: int, fold: int, holdout=None):
     """Fold split as an index gather.
 
-    n_fold == 1 mirrors option3's file split (first 70 % train, rest validation,
-    hyperparameter_search_option3.py:136-139); n_fold > 1 is a contiguous KFold
-    without shuffle: fold sizes n//k (+1 for the first n%k folds)."""
+    n_fold == 1 mirrors option3's file split: training on the first 70 % (of the
+    files, hyperparameter_search_option3.py:136-139; of the samples when the data
+    is synthetic), validation on the rest -- ``holdout`` = the number of training
+    samples when they come from the train_list files.  n_fold > 1 is a contiguous
+    KFold without shuffle over the training samples (the first ``holdout``, all
+    if None): fold sizes n//k (+1 for the first n%k folds)."""
     idx = np.arange(n_samples, dtype=np.int32)
     if n_fold <= 1:
-        cut = int(n_samples * 0.70)
+        cut = int(n_samples * 0.70) if holdout is None else int(holdout)
         return idx[:cut], idx[cut:]
+    if holdout is not None:
+        idx = idx[:int(holdout)]
+        n_samples = len(idx)
     sizes = np.full(n_fold, n_samples // n_fold, dtype=np.int64)
     sizes[: n_samples % n_fold] += 1
     starts = np.concatenate([[0], np.cumsum(sizes)])
@@ -238,7 +244,7 @@ class PopulationEngine:
                                           _lib.stream_handle(self.device)), "mpo_pop_eval_step")
 
     # -- full k-fold training -----------------------------------------------------
-    def fit_folds(self, x, labels, folds, n_fold, epochs, record_train_loss=False):
+    def fit_folds(self, x, labels, folds, n_fold, epochs, record_train_loss=False, holdout=None):
         """Train every member for ``epochs`` on its fold's training indices (in
         order, no shuffle), validating once per epoch (validate_every =
         count/batch, option3:260).  ``folds[i]`` is member i's fold index.
@@ -247,7 +253,7 @@ class PopulationEngine:
         B = self.batch
         tr, va = [], []
         for i in range(self.n):
-            t, v = kfold_split(n_samples, n_fold, int(folds[i]))
+            t, v = kfold_split(n_samples, n_fold, int(folds[i]), holdout)
             tr.append(t)
             va.append(v)
         # members step in lock-step on full batches: every member trains on the

@@ -52,6 +52,9 @@ def make_parser():
     p.add_argument("--world-size", type=int, default=21,
                    help="rank count of the reference's `mpirun -n` (sets concurrent trials)")
     p.add_argument("--n-samples", type=int, default=60000, help="synthetic MNIST-shape samples")
+    p.add_argument("--data-dir", default=None,
+                   help="directory of *.h5 files with `features` / `labels` (option3's mnist data, "
+                        "/bigdata/shared/mnist/*.h5); first 70%% of the files train, the rest validate")
     p.add_argument("--lr", type=float, default=1e-3, help="Adam learning rate (mpi_learn default)")
     p.add_argument("--history-dir", default=None, help="write per-trial history JSON here")
     p.add_argument("--checkpoint", default="coordinator.pkl")
@@ -97,10 +100,23 @@ def run_search(args, x=None, y=None, log=print):
             dist.init_process_group("nccl")
     dev = torch.device("cuda", local)
     provider = BuilderFromFunction(model_fn=test_mnist, parameters=mnist_space())
+    holdout = None
+    if x is None and args.data_dir:
+        from .h5 import load_xy, split_files
+
+        import numpy as np
+
+        train_list, val_list = split_files(args.data_dir)
+        (xt, yt), (xv, yv) = load_xy(train_list), load_xy(val_list)
+        holdout = len(yt)
+        xh, yh = np.concatenate([xt, xv]), np.concatenate([yt, yv])
+        x, y = torch.from_numpy(xh).to(dev), torch.from_numpy(yh).to(dev)
+        log(f"data: {len(train_list)} train / {len(val_list)} validation files, {holdout} / "
+            f"{len(yh) - holdout} samples")
     if x is None:
         x, y = synthetic_mnist(args.n_samples, seed=0, device=dev)
     evaluator = TrialEvaluator(provider, x, y, n_fold=args.n_fold, epochs=args.epochs, batch=args.batch,
-                               lr=args.lr, device=dev, history_dir=args.history_dir)
+                               lr=args.lr, device=dev, history_dir=args.history_dir, holdout=holdout)
     local_eval = evaluator
     if dist is not None:
         evaluator = DistributedEvaluator(evaluator)

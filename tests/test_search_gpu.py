@@ -67,3 +67,28 @@ def test_configs0_search_shape(tmp_path, monkeypatch):
     doc = json.loads(files[0].read_text())
     assert len(doc["history"]) == 5 and len(doc["history"]["0"]["val_loss"]) == 2
     assert doc["history"]["0"]["dropped_train_samples"] == 0
+
+
+def test_search_reads_hdf5_data_dir(tmp_path, monkeypatch):
+    """--data-dir: option3's mnist data layout (*.h5 with features / labels, 70 %
+    of the files train, the rest validate), read by mpi_opt_amd.h5."""
+    import shutil
+
+    from mpi_opt_amd import search
+    from tests.conftest import GOLDEN
+
+    data = tmp_path / "mnist"
+    data.mkdir()
+    for fn in ("mnist_a.h5", "mnist_b.h5", "mnist_c.h5"):
+        shutil.copy(os.path.join(GOLDEN, "h5", fn), data / fn)
+    monkeypatch.chdir(tmp_path)
+    random.seed(0)
+    args = search.make_parser().parse_args(
+        ["--world-size", "5", "--block-size", "2", "--epochs", "1", "--num-iterations", "3", "--batch", "10",
+         "--data-dir", str(data), "--history-dir", str(tmp_path / "hist")])
+    rep = search.run_search(args)
+    assert rep["trials_trained"] == 3
+    doc = json.loads(next((tmp_path / "hist").iterdir()).read_text())
+    h = doc["history"]["0"]
+    # 77 train samples (a + b) -> 7 steps of 10, 50 validation samples (c) -> 5 batches
+    assert h["dropped_train_samples"] == 7 and h["dropped_val_samples"] == 0
