@@ -49,6 +49,58 @@ __device__ __forceinline__ double matern52(double r, double amp) {
     return amp * ((1.0 + k + k * k * (1.0 / 3.0)) * exp(-k));
 }
 
+// exp(-k) for k >= 0 without the generic exp's special-case handling (k is a
+// scaled distance: never negative, never NaN): Cody-Waite reduction
+// k = n ln2 + r, |r| <= ln2/2, degree-13 Taylor polynomial of exp(-r) (truncation
+// < 4e-18 relative), 2^-n by ldexp.  k is clamped at 800 (exp(-800) underflows to
+// exactly 0, as the padding rows need).  Within 2 ulp of exp(-k).
+__device__ __forceinline__ double exp_neg(double k) {
+    k = fmin(k, 800.0);
+    const double t = rint(k * 1.44269504088896340736);
+    const double r = fma(-t, 1.90821492927058770002e-10, fma(-t, 6.93147180369123816490e-01, k));
+    const double x = -r;
+    double p = 1.0 / 6227020800.0;                  // 1/13!
+    p = fma(p, x, 1.0 / 479001600.0);
+    p = fma(p, x, 1.0 / 39916800.0);
+    p = fma(p, x, 1.0 / 3628800.0);
+    p = fma(p, x, 1.0 / 362880.0);
+    p = fma(p, x, 1.0 / 40320.0);
+    p = fma(p, x, 1.0 / 5040.0);
+    p = fma(p, x, 1.0 / 720.0);
+    p = fma(p, x, 1.0 / 120.0);
+    p = fma(p, x, 1.0 / 24.0);
+    p = fma(p, x, 1.0 / 6.0);
+    p = fma(p, x, 0.5);
+    p = fma(p, x, 1.0);
+    p = fma(p, x, 1.0);
+    return ldexp(p, -(int)t);
+}
+
+// sqrt of a non-negative finite r2 by v_rsq_f64, a Goldschmidt step and one
+// Newton correction (ocml's sequence without its denormal scaling and 0/inf
+// fix-ups: r2 is clamped below at 1e-300, whose square root 1e-150 gives the same
+// Matern value as 0).  Within 2 ulp; an ulp of r moves K* by <= 1e-14 relative.
+__device__ __forceinline__ double sqrt_pos(double r2) {
+    r2 = fmax(r2, 1e-300);
+    const double y = __builtin_amdgcn_rsq(r2);
+    double s = r2 * y, h = 0.5 * y;
+    const double e0 = fma(-h, s, 0.5);
+    s = fma(s, e0, s);
+    h = fma(h, e0, h);
+    const double e1 = fma(-s, s, r2);
+    return fma(e1, h, s);
+}
+
+// The scoring kernel's Matern WITHOUT the ConstantKernel amplitude:
+// (1 + k + k^2/3) exp(-k), k = sqrt(5 r2), k^2/3 = r2 * 5/3.  The kernel folds amp
+// into mu (amp * K'.alpha) and into q (amp^2 ||L^-1 K'||^2): one multiply fewer per
+// candidate-observation pair -- fp64 VALU and fp64 MFMA work do not overlap on
+// gfx950 (scripts/probes/coexec.hip), so every VALU op per pair is kernel time.
+__device__ __forceinline__ double matern52_unit(double r2) {
+    const double k = sqrt_pos(r2) * kSqrt5;
+    return fma(r2, 5.0 / 3.0, 1.0 + k) * exp_neg(k);
+}
+
 // scipy.special.ndtr (cephes ndtr.c), the kernel of scipy.stats.norm.cdf.
 __device__ __forceinline__ double ndtr(double a) {
     const double x = a * kSqrt1_2;
@@ -74,10 +126,9 @@ __device__ __forceinline__ void wave_lex_min(double& v, long long& i) {
     }
 }
 
-// ---------------------------------------------------------------------------
 // Rows [n, rows) are padding: a point 1e30 away in every real dimension, whose
-// Matern value underflows to exactly 0 (and alpha is 0 there), so the wave-tile
-// scoring kernel evaluates whole 32-observation groups without bounds checks.
+// Matern value underflows to exactly 0 (and alpha is 0 there): a scoring loop may
+// run over whole 32-observation groups without bounds checks.
 constexpr double kFarAway = 1e30;
 
 __global__ void scale_rows_kernel(const double* __restrict__ X, int n, int rows, int d, int dp,
@@ -293,7 +344,7 @@ __device__ __forceinline__ void score_epilogue(const ScoreArgs& a, bool live, lo
     }
 }
 
-template <int BM, int DP, int OCC>
+template <int BM, int DP, int D, int OCC>
 __global__ __launch_bounds__(256, OCC) void gp_score_kernel(ScoreArgs a) {
     constexpr int MT = BM / 16;      // 16-row m-tiles per block
     constexpr int G = 64 / BM;       // lanes groups per wave in phase 1
@@ -330,11 +381,11 @@ __global__ __launch_bounds__(256, OCC) void gp_score_kernel(ScoreArgs a) {
                 const double* xi_ = a.xs + (size_t)i * DP;
                 double r2 = 0.0;
 #pragma unroll
-                for (int q = 0; q < DP; ++q) {
+                for (int q = 0; q < D; ++q) {      // D real dims of the DP-padded rows
                     const double t = c[q] - xi_[q];
                     r2 += t * t;
                 }
-                kv = matern52(sqrt(r2), a.amp);
+                kv = matern52_unit(r2);             // amp folded into mu and q below
                 mu_acc += kv * a.alpha[i];
             }
             kc[(size_t)((i >> 2) * MT) * 64 + kc_row + (i & 3) * 16] = kv;
@@ -346,6 +397,7 @@ __global__ __launch_bounds__(256, OCC) void gp_score_kernel(ScoreArgs a) {
     if (tid < BM) {
 #pragma unroll
         for (int s = 0; s < S; ++s) mu_n += red[s * BM + tid];
+        mu_n *= a.amp;
     }
     __syncthreads();  // red is reused for the q partials below
 
@@ -427,123 +479,9 @@ __global__ __launch_bounds__(256, OCC) void gp_score_kernel(ScoreArgs a) {
     // ---- phase 3: posterior, acquisitions, block top-k (wave 0)
     if (wave != 0) return;
     const int row = lane;
-    const double q = row < BM ? red[0 * BM + row] + red[1 * BM + row] + red[2 * BM + row] + red[3 * BM + row] : 0.0;
+    const double q = row < BM ? (red[0 * BM + row] + red[1 * BM + row] + red[2 * BM + row] + red[3 * BM + row]) *
+                                    (a.amp * a.amp) : 0.0;
     score_epilogue(a, row < BM, m0 + row, mu_n, q, blockIdx.x, lane);
-}
-
-// ---------------------------------------------------------------------------
-// gp_score_wave_kernel: one WAVE owns a 16-candidate tile end to end.
-//
-//   * the L^-1 B-fragment stream of the first TL column tiles is staged ONCE per
-//     workgroup into LDS (persistent grid: one 512-thread workgroup per CU, 8 waves =
-//     2 per SIMD); the remaining tiles stream from L2;
-//   * the loop runs over 4-k-step groups g: the Matern values of group g + 1 are
-//     computed (VALU) while group g's MFMAs run -- every column tile jt >= g takes
-//     4 MFMAs of group g into its own accumulator, so consecutive MFMAs are
-//     independent -- and column tile g is complete (its ||V_row||^2 added) after
-//     group g.  K* never leaves registers: lane l holds candidate l & 15 at
-//     observation 4 ks + (l >> 4), the v_mfma_f64_16x16x4 A-fragment layout.
-// T (column tiles = np16 / 16) is a template parameter, so every LDS offset is an
-// immediate and the T accumulators stay in registers.
-template <int T>
-__host__ __device__ constexpr int wave_lds_tiles_ct() {
-    int tl = 0;
-    while (tl < T && wfrag_tile_base(tl + 1) * sizeof(double) <= 160 * 1024) ++tl;
-    return tl;
-}
-
-template <int DP>
-__device__ __forceinline__ void matern_group(const ScoreArgs& a, const double* xb, const double* ab, const double (&c)[DP],
-                                             int g, double (&A)[4], double& mu_p) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int ks = 4 * g + u;
-        const double* xr = xb + 4 * ks * DP;
-        double r2 = 0.0;
-#pragma unroll
-        for (int q = 0; q < DP; ++q) {
-            const double d_ = c[q] - xr[q];
-            r2 += d_ * d_;
-        }
-        const double kv = matern52(sqrt(r2), a.amp);
-        mu_p += kv * ab[4 * ks];
-        A[u] = kv;
-    }
-}
-
-template <int DP, int T>
-__global__ __launch_bounds__(512, 2) void gp_score_wave_kernel(ScoreArgs a, long long ntiles) {
-    constexpr int TL = wave_lds_tiles_ct<T>();
-    extern __shared__ __attribute__((aligned(16))) double bl[];   // wfrag tiles [0, TL)
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    {
-        constexpr int nst = (int)wfrag_tile_base(TL);             // doubles, even
-        const double2* src = reinterpret_cast<const double2*>(a.wfrag);
-        double2* dst = reinterpret_cast<double2*>(bl);
-        for (int e = tid; e < nst / 2; e += 512) dst[e] = src[e];
-    }
-    __syncthreads();
-
-    const int row = lane & 15, grp = lane >> 4;
-    for (long long t = (long long)blockIdx.x * 8 + wave; t < ntiles; t += (long long)gridDim.x * 8) {
-        const long long m0 = t * 16;
-        const long long gm = m0 + row;
-        double c[DP];
-#pragma unroll
-        for (int q = 0; q < DP; ++q) c[q] = (gm < a.m && q < a.d) ? a.cand[gm * a.d + q] / a.ls[q] : 0.0;
-        // xs / alpha are padded to 32 rows (padding rows give K* = 0 exactly): no
-        // bounds checks.  Bases opaque per tile: no hoisting of per-k-step addresses.
-        const double* xb = a.xs + grp * DP;
-        const double* ab = a.alpha + grp;
-        const double* wb = a.wfrag + lane;
-        asm volatile("" : "+v"(xb), "+v"(ab), "+v"(wb));
-
-        f64x4 acc[T];
-#pragma unroll
-        for (int jt = 0; jt < T; ++jt) acc[jt] = f64x4{0.0, 0.0, 0.0, 0.0};
-        double sq[4] = {0.0, 0.0, 0.0, 0.0};
-        double mu_p = 0.0;
-        double A[4], An[4];
-        matern_group<DP>(a, xb, ab, c, 0, A, mu_p);
-#pragma unroll
-        for (int g = 0; g < T; ++g) {
-            if (g + 1 < T) matern_group<DP>(a, xb, ab, c, g + 1, An, mu_p);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-#pragma unroll
-                for (int jt = g; jt < T; ++jt) {
-                    const size_t off = wfrag_tile_base(jt) + (size_t)(4 * g + u) * 64;
-                    const double b = jt < TL ? bl[off + lane] : wb[off];
-                    acc[jt] = __builtin_amdgcn_mfma_f64_16x16x4f64(A[u], b, acc[jt], 0, 0, 0);
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) sq[r] += acc[g][r] * acc[g][r];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) A[u] = An[u];
-        }
-
-        // ---- reductions: ||V_row||^2 over the 16 column lanes, mu over the 4 k-groups
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            double v = sq[r];
-            v += __shfl_xor(v, 1);
-            v += __shfl_xor(v, 2);
-            v += __shfl_xor(v, 4);
-            v += __shfl_xor(v, 8);
-            sq[r] = v;                       // row grp + 4 r, every lane of the group
-        }
-        mu_p += __shfl_xor(mu_p, 16);
-        mu_p += __shfl_xor(mu_p, 32);
-        // row R (< 16) lives in lane 16 (R & 3), register R >> 2
-        double q = 0.0;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const double v = __shfl(sq[r], 16 * (lane & 3));
-            if ((lane >> 2) == r) q = v;
-        }
-        score_epilogue(a, lane < 16, gm, mu_p, q, t, lane);
-    }
 }
 
 // Merge per-block top-k lists.  grid = (G, 3): block g of acquisition y merges
@@ -656,9 +594,9 @@ int choose_bm(int dp, int np16) {
     return -1;
 }
 
-template <int BM, int DP, int OCC>
+template <int BM, int DP, int D, int OCC>
 hipError_t launch_score(const ScoreArgs& a, int nblocks, size_t lds, hipStream_t s) {
-    auto kern = gp_score_kernel<BM, DP, OCC>;
+    auto kern = gp_score_kernel<BM, DP, D, OCC>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)lds);
     hipLaunchKernelGGL(kern, dim3(nblocks), dim3(256), lds, s, a);
@@ -669,103 +607,42 @@ hipError_t launch_score(const ScoreArgs& a, int nblocks, size_t lds, hipStream_t
 // MPO_GP_OCC overrides for experiments
 inline int gp_occ16() {
     const char* e = getenv("MPO_GP_OCC");
-    const int v = e ? atoi(e) : 5;
-    return (v == 1 || v == 5 || v == 6) ? v : 5;
+    const int v = e ? atoi(e) : 6;
+    return (v == 1 || v == 5 || v == 6 || v == 8) ? v : 6;
 }
 
-template <int DP>
+template <int DP, int D>
 hipError_t launch_score_bm(int bm, const ScoreArgs& a, int nblocks, size_t lds, hipStream_t s) {
     switch (bm) {
-        case 64: return launch_score<64, DP, 1>(a, nblocks, lds, s);
-        case 32: return launch_score<32, DP, 1>(a, nblocks, lds, s);
+        case 64: return launch_score<64, DP, D, 1>(a, nblocks, lds, s);
+        case 32: return launch_score<32, DP, D, 1>(a, nblocks, lds, s);
         case 16:
             switch (gp_occ16()) {
-                case 1: return launch_score<16, DP, 1>(a, nblocks, lds, s);
-                case 5: return launch_score<16, DP, 5>(a, nblocks, lds, s);
-                case 6: return launch_score<16, DP, 6>(a, nblocks, lds, s);
-                default: return launch_score<16, DP, 5>(a, nblocks, lds, s);
+                case 1: return launch_score<16, DP, D, 1>(a, nblocks, lds, s);
+                case 5: return launch_score<16, DP, D, 5>(a, nblocks, lds, s);
+                case 8: return launch_score<16, DP, D, 8>(a, nblocks, lds, s);
+                default: return launch_score<16, DP, D, 6>(a, nblocks, lds, s);
             }
     }
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_score_dp(int dp, int bm, const ScoreArgs& a, int nblocks, size_t lds, hipStream_t s) {
+// (padded row width DP, distance dims D): d = 5 and d = 10 (the reference's mnist
+// space and the BASELINE config) get exact-width distance loops
+hipError_t launch_score_dp(int dp, int d, int bm, const ScoreArgs& a, int nblocks, size_t lds, hipStream_t s) {
     switch (dp) {
-        case 4: return launch_score_bm<4>(bm, a, nblocks, lds, s);
-        case 8: return launch_score_bm<8>(bm, a, nblocks, lds, s);
-        case 12: return launch_score_bm<12>(bm, a, nblocks, lds, s);
-        case 16: return launch_score_bm<16>(bm, a, nblocks, lds, s);
-        case 32: return launch_score_bm<32>(bm, a, nblocks, lds, s);
+        case 4: return launch_score_bm<4, 4>(bm, a, nblocks, lds, s);
+        case 8: return d == 5 ? launch_score_bm<8, 5>(bm, a, nblocks, lds, s)
+                              : launch_score_bm<8, 8>(bm, a, nblocks, lds, s);
+        case 12: return d == 10 ? launch_score_bm<12, 10>(bm, a, nblocks, lds, s)
+                                : launch_score_bm<12, 12>(bm, a, nblocks, lds, s);
+        case 16: return launch_score_bm<16, 16>(bm, a, nblocks, lds, s);
+        case 32: return launch_score_bm<32, 32>(bm, a, nblocks, lds, s);
     }
     return hipErrorInvalidValue;
 }
 
-// ---- wave-tile kernel dispatch ------------------------------------------------
-constexpr int kWaveTile = 16;
-
-bool wave_kernel_ok(int dp, int np16) {
-    const char* env = getenv("MPO_GP_KERNEL");
-    if (env && std::string(env) == "block") return false;
-    return dp <= 16 && np16 <= 256;
-}
-
-int device_cus() {
-    static thread_local int dev_cached = -1, cus = 0;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 256;
-    if (dev != dev_cached) {
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-        dev_cached = dev;
-    }
-    return cus;
-}
-
-template <int DP, int T>
-hipError_t launch_wave(const ScoreArgs& a, long long ntiles, hipStream_t s) {
-    constexpr int TL = wave_lds_tiles_ct<T>();
-    const size_t lds = std::max<size_t>(wfrag_tile_base(TL) * sizeof(double), 16);
-    auto kern = gp_score_wave_kernel<DP, T>;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    const long long want = (ntiles + 7) / 8;
-    const int grid = (int)std::max<long long>(1, std::min<long long>(want, device_cus()));
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, a, ntiles);
-    return hipGetLastError();
-}
-
-template <int DP>
-hipError_t launch_wave_n(const ScoreArgs& a, long long ntiles, hipStream_t s) {
-    switch (a.T) {
-        case 1: return launch_wave<DP, 1>(a, ntiles, s);
-        case 2: return launch_wave<DP, 2>(a, ntiles, s);
-        case 3: return launch_wave<DP, 3>(a, ntiles, s);
-        case 4: return launch_wave<DP, 4>(a, ntiles, s);
-        case 5: return launch_wave<DP, 5>(a, ntiles, s);
-        case 6: return launch_wave<DP, 6>(a, ntiles, s);
-        case 7: return launch_wave<DP, 7>(a, ntiles, s);
-        case 8: return launch_wave<DP, 8>(a, ntiles, s);
-        case 9: return launch_wave<DP, 9>(a, ntiles, s);
-        case 10: return launch_wave<DP, 10>(a, ntiles, s);
-        case 11: return launch_wave<DP, 11>(a, ntiles, s);
-        case 12: return launch_wave<DP, 12>(a, ntiles, s);
-        case 13: return launch_wave<DP, 13>(a, ntiles, s);
-        case 14: return launch_wave<DP, 14>(a, ntiles, s);
-        case 15: return launch_wave<DP, 15>(a, ntiles, s);
-        case 16: return launch_wave<DP, 16>(a, ntiles, s);
-    }
-    return hipErrorInvalidValue;
-}
-
-hipError_t launch_wave_dp(int dp, const ScoreArgs& a, long long ntiles, hipStream_t s) {
-    switch (dp) {
-        case 4: return launch_wave_n<4>(a, ntiles, s);
-        case 8: return launch_wave_n<8>(a, ntiles, s);
-        case 12: return launch_wave_n<12>(a, ntiles, s);
-        case 16: return launch_wave_n<16>(a, ntiles, s);
-    }
-    return hipErrorInvalidValue;
-}
+constexpr int kWaveTile = 16;   // candidates per partial top-k list (the smallest block)
 
 int trsm_cols_per_block(int n) {
     size_t cb = 64;
@@ -934,8 +811,7 @@ static int gp_score_impl(const MpoGpModel* model, const double* cand, int64_t m,
     MPO_CHECK_ARG(ws && ws_bytes >= mpo_gp_score_ws_bytes(model, m, k), "mpo_gp_acq_score: workspace too small");
     const int bm = choose_bm(model->dp, model->np16);
     if (bm < 0) { mpo::set_error("mpo_gp_acq_score: model too large"); return MPO_ENOTSUP; }
-    const bool wave = wave_kernel_ok(model->dp, model->np16);
-    const int64_t nblocks64 = wave ? (m + kWaveTile - 1) / kWaveTile : (m + bm - 1) / bm;
+    const int64_t nblocks64 = (m + bm - 1) / bm;
     MPO_CHECK_ARG(nblocks64 < (1LL << 31), "mpo_gp_acq_score: too many candidates");
     const int nblocks = (int)nblocks64;
     mpo::WsCarver c(ws);
@@ -970,12 +846,8 @@ static int gp_score_impl(const MpoGpModel* model, const double* cand, int64_t m,
     a.k = k;
     a.part_idx = part_idx;
     a.part_val = part_val;
-    if (wave) {
-        MPO_HIP(launch_wave_dp(model->dp, a, nblocks64, s));
-    } else {
-        const size_t lds = score_lds_bytes(bm, model->dp, model->np16);
-        MPO_HIP(launch_score_dp(model->dp, bm, a, nblocks, lds, s));
-    }
+    const size_t lds = score_lds_bytes(bm, model->dp, model->np16);
+    MPO_HIP(launch_score_dp(model->dp, model->d, bm, a, nblocks, lds, s));
     if (k > 0) {
         // stage 1: G groups of ~64 block-lists each; stage 2: one list
         const int chunk = std::max(64, (nblocks + kMergeGroups - 1) / kMergeGroups);

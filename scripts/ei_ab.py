@@ -1,4 +1,4 @@
-"""A/B the GP scoring kernels (block-per-16-candidates vs wave-tile) in one process, interleaved."""
+"""A/B the GP scoring kernel variants (candidates per workgroup / occupancy) in one process, interleaved."""
 import os
 import sys
 
@@ -13,8 +13,9 @@ X, y = synthetic.gp_problem(200, 10, 0)
 ls = np.array([16.2, 1.91, 1.65, 9.84, 1.84, 2.94, 2.45, 9.09, 8.13, 1.94])
 g = DeviceGP(X, y, 17.4955, ls, 0.0465)
 cand = torch.from_numpy(synthetic.gp_candidates(1_000_000, 10, seed=1)).cuda()
-VARIANTS = {"block16/5": {"MPO_GP_KERNEL": "block", "MPO_GP_BM": "16", "MPO_GP_OCC": "5"},
-            "wave": {"MPO_GP_KERNEL": "wave"}}
+VARIANTS = {"bm16/occ5": {"MPO_GP_BM": "16", "MPO_GP_OCC": "5"},
+            "bm16/occ6": {"MPO_GP_BM": "16", "MPO_GP_OCC": "6"},
+            "bm16/occ8": {"MPO_GP_BM": "16", "MPO_GP_OCC": "8"}}
 res = {b: [] for b in VARIANTS}
 for rnd in range(4):
     for b in res:
