@@ -32,8 +32,10 @@
 
 #include "mpo_internal.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <string>
 
 namespace {
 
@@ -508,12 +510,355 @@ __global__ __launch_bounds__(kFitThreads) void lml_grad_kernel(LmlArgs a) {
     }
 }
 
+// ===========================================================================
+// Block-sweep variant (n <= kSwMaxN): K^-1 and log det K by the symmetric sweep
+// operator over 32-wide pivot blocks, trailing updates on v_mfma_f64_16x16x4.
+//
+// Sweeping pivot block k of a symmetric A (Goodnight's sweep, block form):
+//     A_kk <- -A_kk^-1,   A_ik <- A_ik A_kk^-1,   A_ij <- A_ij - A_ik A_kk^-1 A_kj
+// for i, j != k; after every block is swept A = -K^-1, and log det K is the sum of
+// the log determinants of the pivot blocks at their sweep (the Schur complements
+// a Cholesky factorisation meets).  Work: n^3 flops, all in rank-32 MFMA updates
+// of the lower triangle (L2-resident, one XCD's L2 per theta); no L^-1, and the
+// pair phase reads K^-1 directly instead of forming L^-T L^-1 entry by entry.
+// Per step (3 barriers):
+//   a. the old block column C = A[:, k] -> LDS (stride 33: conflict-free B reads)
+//   b. wave 0 sweeps the 32x32 pivot block in registers (lane = row, the pivot row
+//      broadcast through LDS), accumulating log det and flagging a non-positive
+//      pivot (sklearn's Cholesky LinAlgError);
+//   c. G = C P^-1 for every 16-row tile outside the block (MFMA) -> workspace;
+//   d. every lower 16x16 tile outside block k: A_IJ -= G_I C_J^T (8 MFMAs, K = 32);
+//      block column k <- G, the pivot block <- -P^-1.
+// Padding rows/columns n..np carry the identity, so they never couple to K.
+constexpr int kSwNb = 32;
+constexpr int kSwLd = kSwNb + 1;
+constexpr int kSwMaxN = 576;   // LDS: np * 33 + 2 * 32 * 33 doubles <= 160 KiB
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+__host__ __device__ inline long long sw_np(int n) { return (n + kSwNb - 1) / kSwNb * kSwNb; }
+
+// per-theta workspace (doubles): xs [n][d] | alpha [np] | A [np][np] | G [np][32]
+__host__ __device__ inline long long sw_ws_doubles(int n, int d) {
+    auto al = [](long long x) { return (x + 31) & ~31LL; };
+    const long long np = sw_np(n);
+    return al((long long)n * d) + al(np) + np * np + np * kSwNb;
+}
+
+template <int DP>
+__global__ __launch_bounds__(kFitThreads) void lml_sweep_kernel(LmlArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double fsm[];
+    const int b = blockIdx.x;
+    const int n = a.n, d = a.d;
+    const int np = (int)sw_np(n);
+    const int nbk = np / kSwNb, ntile = np / 16;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const double* th = a.theta + (long long)b * (d + 2);
+    auto al = [](long long x) { return (x + 31) & ~31LL; };
+    double* ws = a.ws + (long long)b * a.ws_stride;
+    double* xs = ws;
+    double* alpha = xs + al((long long)n * d);
+    double* A = alpha + al(np);                    // [np][np], lower triangle + full diagonal tiles
+    double* G = A + (long long)np * np;            // [np][32]
+    double* Cp = fsm;                              // [np][33] old block column
+    double* Pi = Cp + np * kSwLd;                  // [32][33] P^-1
+    double* Pr = Pi + kSwNb * kSwLd;               // [32][33] pivot-row broadcast / reductions
+    __shared__ int fail_s;
+    __shared__ double logdet_s;
+
+    const double amp = exp(th[0]);
+    const double noise = exp(th[d + 1]);
+    double ls[DP];
+#pragma unroll
+    for (int c = 0; c < DP; ++c) ls[c] = c < d ? exp(th[1 + c]) : 1.0;
+
+    // ---- 1. xs = X / ls; K into A (lower triangle and the full diagonal 16x16 tiles)
+    for (int e = tid; e < n * d; e += kFitThreads) {
+        const int c = e % d;
+        double lc = 1.0;
+#pragma unroll
+        for (int q = 0; q < DP; ++q)
+            if (q == c) lc = ls[q];
+        xs[e] = a.X[e] / lc;
+    }
+    if (tid == 0) { fail_s = 0; logdet_s = 0.0; }
+    __syncthreads();
+    for (int i = wave; i < np; i += kFitWaves) {
+        double xi[DP];
+#pragma unroll
+        for (int c = 0; c < DP; ++c) xi[c] = (c < d && i < n) ? xs[i * d + c] : 0.0;
+        const int jend = (i | 15) + 1;             // through the end of i's diagonal tile
+        for (int j = lane; j < jend && j < np; j += 64) {
+            double v;
+            if (i >= n || j >= n) {
+                v = i == j ? 1.0 : 0.0;
+            } else if (i == j) {
+                v = amp * 1.0 + noise + kFitJitter;
+            } else {
+                double r2 = 0.0;
+#pragma unroll
+                for (int c = 0; c < DP; ++c)
+                    if (c < d) {
+                        const double t = xi[c] - xs[j * d + c];
+                        r2 += t * t;
+                    }
+                const double k = sqrt(r2) * kSqrt5;
+                v = amp * ((1.0 + k + k * k / 3.0) * exp(-k));
+            }
+            A[(long long)i * np + j] = v;
+        }
+    }
+    __threadfence_block();
+    __syncthreads();
+    if (a.stop == 1) return;
+
+    // ---- 2. block sweeps
+    for (int k = 0; k < nbk; ++k) {
+        const int k0 = k * kSwNb;
+        // a. old block column (symmetric read from the lower storage)
+        for (int e = tid; e < np * kSwNb; e += kFitThreads) {
+            const int i = e >> 5, c = e & 31, j = k0 + c;
+            Cp[i * kSwLd + c] = i >= j ? A[(long long)i * np + j] : A[(long long)j * np + i];
+        }
+        __syncthreads();
+        // b. wave 0: sweep the pivot block in registers: lane l < 32 holds row l;
+        //    the pivot row is broadcast by v_readlane (wave-uniform SGPR operands),
+        //    so a step has no LDS round trip; log det accumulates as a product of
+        //    pivots (each in [noise, amp + noise]: no over/underflow in 32 steps)
+        if (wave == 0 && a.stop != 6) {   // stop 6: diagnostics only, pivot sweep skipped
+            const int l = lane & 31;
+            double r[kSwNb];
+#pragma unroll
+            for (int j = 0; j < kSwNb; ++j) r[j] = Cp[(k0 + l) * kSwLd + j];
+            double prod = 1.0;
+            int bad = 0;
+#pragma unroll
+            for (int c = 0; c < kSwNb; ++c) {
+                const double p = readlane_f64(r[c], c);
+                if (!(p > 0.0) || !isfinite(p)) bad = bad ? bad : c + 1;
+                prod *= p;
+                const double ip = 1.0 / p;
+                const bool piv = l == c;
+                const double t = r[c] * ip;
+#pragma unroll
+                for (int j = 0; j < kSwNb; ++j) {
+                    if (j == c) continue;
+                    const double pj = readlane_f64(r[j], c);
+                    r[j] = piv ? r[j] * ip : fma(-t, pj, r[j]);
+                }
+                r[c] = piv ? -ip : t;
+            }
+            // r = -P^-1 (row l)
+            if (lane < kSwNb) {
+#pragma unroll
+                for (int j = 0; j < kSwNb; ++j) Pi[l * kSwLd + j] = -r[j];
+            }
+            if (lane == 0) {
+                logdet_s += log(prod);
+                if (bad && !fail_s) fail_s = k0 + bad;
+            }
+        }
+        __syncthreads();
+        // c. G = C P^-1 for the 16-row tiles outside block k (2 column tiles x 8 k-steps)
+        for (int R = wave; R < ntile; R += kFitWaves) {
+            if ((R >> 1) == k) continue;
+            f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+            const int ar = (16 * R + (lane & 15)) * kSwLd + (lane >> 4);
+            const int br = (lane >> 4) * kSwLd + (lane & 15);
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) {
+                const double av = Cp[ar + 4 * ks];
+                acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, Pi[br + 4 * ks * kSwLd], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, Pi[br + 4 * ks * kSwLd + 16], acc1, 0, 0, 0);
+            }
+            // stored in A-fragment order for the trailing update: element (row, col)
+            // of row tile R -> Gf[(R*8 + col/4)*64 + row%16 + 16*(col%4)]
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int rr = (lane >> 4) + 4 * q, c0 = lane & 15, c1 = 16 + c0;
+                G[((long long)R * 8 + (c0 >> 2)) * 64 + rr + 16 * (c0 & 3)] = acc0[q];
+                G[((long long)R * 8 + (c1 >> 2)) * 64 + rr + 16 * (c1 & 3)] = acc1[q];
+            }
+        }
+        __threadfence_block();
+        __syncthreads();
+        // d. trailing update of the lower tiles outside block k; block column k <- G,
+        //    pivot block <- -P^-1
+        const int nt_low = ntile * (ntile + 1) / 2;
+        // tiles of this wave, in order; the next tile's C and G fragments are
+        // loaded before the current tile's MFMAs (latency of L2 hides under them)
+        auto tile_of = [&](int t, int& I, int& J) {
+            I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+            while (I * (I + 1) / 2 > t) --I;
+            while ((I + 1) * (I + 2) / 2 <= t) ++I;
+            J = t - I * (I + 1) / 2;
+        };
+        auto live = [&](int t) {
+            int I, J;
+            tile_of(t, I, J);
+            return (I >> 1) != k && (J >> 1) != k;
+        };
+        auto next_live = [&](int t) {
+            for (; t < nt_low; t += kFitWaves)
+                if (live(t)) return t;
+            return nt_low;
+        };
+        int t = a.stop == 7 ? nt_low : next_live(wave);
+        f64x4 cc;
+        double ga[8];
+        auto fetch = [&](int tt) {
+            int I, J;
+            tile_of(tt, I, J);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cc[q] = A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)];
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) ga[ks] = G[((long long)I * 8 + ks) * 64 + lane];
+        };
+        if (t < nt_low) fetch(t);
+        while (t < nt_low) {
+            int I, J;
+            tile_of(t, I, J);
+            f64x4 acc = cc;
+            double av[8];
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) av[ks] = ga[ks];
+            const int tn = next_live(t + kFitWaves);
+            if (tn < nt_low) fetch(tn);
+            const int cb = (16 * J + (lane & 15)) * kSwLd + (lane >> 4);
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks)
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[ks], Cp[cb + 4 * ks], acc, 0, 0, 0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)] = acc[q];
+            t = tn;
+        }
+        for (int e = tid; e < np * kSwNb; e += kFitThreads) {
+            const int i = e >> 5, c = e & 31, j = k0 + c;
+            if ((i >> 5) == k) {
+                A[(long long)i * np + j] = -Pi[(i - k0) * kSwLd + c];
+            } else {
+                const double gv = G[((long long)(i >> 4) * 8 + (c >> 2)) * 64 + (i & 15) + 16 * (c & 3)];
+                if (i > j) A[(long long)i * np + j] = gv;
+                else A[(long long)j * np + i] = gv;
+            }
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
+    if (a.stop == 2) return;
+    if (fail_s) {  // sklearn: LinAlgError -> (-inf, zeros)
+        if (tid == 0) { a.lml[b] = -INFINITY; a.info[b] = fail_s; }
+        for (int c = tid; c < d + 2; c += kFitThreads) a.grad[(long long)b * (d + 2) + c] = 0.0;
+        return;
+    }
+    auto kinv = [&](int i, int j) -> double {   // (K^-1)_ij = -A (symmetric, lower storage)
+        return i >= j ? -A[(long long)i * np + j] : -A[(long long)j * np + i];
+    };
+
+    // ---- 3. alpha = K^-1 y
+    for (int i = tid; i < n; i += kFitThreads) {
+        double s0 = 0.0, s1 = 0.0;
+        int j = 0;
+        for (; j + 1 < n; j += 2) {
+            s0 += kinv(i, j) * a.y[j];
+            s1 += kinv(i, j + 1) * a.y[j + 1];
+        }
+        if (j < n) s0 += kinv(i, j) * a.y[j];
+        alpha[i] = s0 + s1;
+    }
+    __syncthreads();
+    if (a.stop == 4) return;
+
+    // ---- 4. pairs (i >= j): W_ij dK_ij / dtheta, W = alpha alpha^T - K^-1
+    double g[DP + 2];
+#pragma unroll
+    for (int c = 0; c < DP + 2; ++c) g[c] = 0.0;
+    for (int i = wave; i < n; i += kFitWaves) {
+        const double ai = alpha[i];
+        double xi[DP];
+#pragma unroll
+        for (int c = 0; c < DP; ++c) xi[c] = c < d ? xs[i * d + c] : 0.0;
+        for (int j = lane; j <= i; j += 64) {
+            const double W = (ai * alpha[j] + A[(long long)i * np + j]) * (i == j ? 1.0 : 2.0);
+            // two passes over the dims (distance, then gradient terms) instead of a
+            // D[DP] array: fewer live registers at 1024 threads per workgroup
+            const double* xj = xs + j * d;
+            double r2 = 0.0;
+#pragma unroll
+            for (int c = 0; c < DP; ++c)
+                if (c < d) {
+                    const double t = xi[c] - xj[c];
+                    r2 += t * t;
+                }
+            const double sq = sqrt(5.0 * r2);
+            const double e = exp(-sq);
+            const double Mij = i == j ? 1.0 : (1.0 + sq + sq * sq / 3.0) * e;
+            g[0] += W * (amp * Mij);
+            const double f = W * amp * (5.0 / 3.0) * (sq + 1.0) * e;
+#pragma unroll
+            for (int c = 0; c < DP; ++c)
+                if (c < d) {
+                    const double t = xi[c] - xj[c];
+                    g[1 + c] += f * (t * t);
+                }
+            if (i == j) g[DP + 1] += W * noise;
+        }
+    }
+
+    // ---- 5. fixed-order reduction: lanes (butterfly) -> waves (LDS, in order)
+    __syncthreads();
+    double* red = fsm;  // [kFitWaves][DP + 2]
+#pragma unroll
+    for (int c = 0; c < DP + 2; ++c) {
+        const double v = wave_sum_bcast(g[c]);
+        if (lane == 0) red[wave * (DP + 2) + c] = v;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double ya = 0.0;
+        for (int i = 0; i < n; ++i) ya += a.y[i] * alpha[i];
+        a.lml[b] = -0.5 * ya - 0.5 * logdet_s - 0.5 * n * kLog2Pi;
+        a.info[b] = 0;
+        double* out = a.grad + (long long)b * (d + 2);
+        for (int c = 0; c < d + 2; ++c) {
+            const int src = c == 0 ? 0 : (c == d + 1 ? DP + 1 : c);
+            double s = 0.0;
+            for (int w = 0; w < kFitWaves; ++w) s += red[w * (DP + 2) + src];
+            out[c] = 0.5 * s;
+        }
+    }
+}
+
 inline int fit_dp(int d) {
     if (d <= 4) return 4;
     if (d <= 8) return 8;
+    if (d <= 12) return 12;
     if (d <= 16) return 16;
     if (d <= 32) return 32;
     return -1;
+}
+
+template <int DP>
+int launch_sweep(const LmlArgs& a, int B, hipStream_t s) {
+    auto kern = lml_sweep_kernel<DP>;
+    const size_t lds = ((size_t)sw_np(a.n) * kSwLd + 2 * kSwNb * kSwLd) * sizeof(double);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(B), dim3(kFitThreads), lds, s, a);
+    MPO_LAUNCH_CHECK();
+    return MPO_OK;
+}
+
+// which LML kernel: the LDS-packed Cholesky kernel for n <= kSwMinN (small,
+// latency-bound factors), the block sweep for kSwMinN < n <= kSwMaxN (0.44 vs
+// 0.68 ms per launch at n = 200, 0.60 at 256, 2.45 at 500: scripts/fit_probe.py),
+// the global-memory Cholesky past that.  MPO_FIT_KERNEL=sweep / panel force one.
+constexpr int kSwMinN = 192;
+inline bool use_sweep(int n) {
+    const char* e = getenv("MPO_FIT_KERNEL");
+    if (e && std::string(e) == "panel" && n <= kFitLdsMaxN) return false;
+    if (e && std::string(e) == "sweep" && n <= kSwMaxN) return true;
+    return n > kSwMinN && n <= kSwMaxN;
 }
 
 template <bool kLds, int DP>
@@ -532,7 +877,8 @@ extern "C" {
 
 size_t mpo_gp_lml_ws_bytes(int n, int d, int batch) {
     if (n <= 0 || n > kFitMaxN || fit_dp(d) < 0 || batch <= 0) return 0;
-    return (size_t)fit_ws_doubles(n, d, n <= kFitLdsMaxN) * sizeof(double) * batch + 256;
+    const long long per = std::max(fit_ws_doubles(n, d, n <= kFitLdsMaxN), n <= kSwMaxN ? sw_ws_doubles(n, d) : 0LL);
+    return (size_t)per * sizeof(double) * batch + 256;
 }
 
 int mpo_gp_lml_grad(const double* X, const double* y_norm, int n, int d, const double* theta, int batch,
@@ -548,15 +894,26 @@ int mpo_gp_lml_grad(const double* X, const double* y_norm, int n, int d, const d
     MPO_CHECK_ARG(ws_bytes >= mpo_gp_lml_ws_bytes(n, d, batch), "mpo_gp_lml_grad: workspace too small (%zu < %zu)",
                   ws_bytes, mpo_gp_lml_ws_bytes(n, d, batch));
     const bool use_lds = n <= kFitLdsMaxN;
+    const bool sweep = use_sweep(n);
     LmlArgs a{X, y_norm, n, d, theta, lml, grad, info,
               reinterpret_cast<double*>(mpo::align_up(reinterpret_cast<uintptr_t>(ws), 256)),
-              fit_ws_doubles(n, d, use_lds), 0};
+              sweep ? sw_ws_doubles(n, d) : fit_ws_doubles(n, d, use_lds), 0};
     if (const char* e = getenv("MPO_FIT_DEBUG")) a.stop = atoi(e);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    if (sweep) {
+        switch (dp) {
+            case 4: return launch_sweep<4>(a, batch, s);
+            case 8: return launch_sweep<8>(a, batch, s);
+            case 12: return launch_sweep<12>(a, batch, s);
+            case 16: return launch_sweep<16>(a, batch, s);
+            default: return launch_sweep<32>(a, batch, s);
+        }
+    }
     if (use_lds) {
         switch (dp) {
             case 4: return launch_lml<true, 4>(a, batch, s);
             case 8: return launch_lml<true, 8>(a, batch, s);
+            case 12: return launch_lml<true, 12>(a, batch, s);
             case 16: return launch_lml<true, 16>(a, batch, s);
             default: return launch_lml<true, 32>(a, batch, s);
         }
@@ -564,6 +921,7 @@ int mpo_gp_lml_grad(const double* X, const double* y_norm, int n, int d, const d
     switch (dp) {
         case 4: return launch_lml<false, 4>(a, batch, s);
         case 8: return launch_lml<false, 8>(a, batch, s);
+        case 12: return launch_lml<false, 12>(a, batch, s);
         case 16: return launch_lml<false, 16>(a, batch, s);
         default: return launch_lml<false, 32>(a, batch, s);
     }

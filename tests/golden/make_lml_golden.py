@@ -20,7 +20,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 
 from oracle import gp_ei as O  # noqa: E402
 
-CASES = [("n200_d10", 200, 10, 0), ("n12_d5", 12, 5, 3), ("n57_d3", 57, 3, 5), ("n230_d4", 230, 4, 7), ("n130_d6", 130, 6, 11)]
+CASES = [("n200_d10", 200, 10, 0), ("n12_d5", 12, 5, 3), ("n57_d3", 57, 3, 5), ("n230_d4", 230, 4, 7), ("n130_d6", 130, 6, 11),
+         ("n256_d10", 256, 10, 13), ("n500_d10", 500, 10, 17)]
 
 
 def main():

@@ -1,7 +1,9 @@
 """Device GP refit (``mpo_gp_lml_grad`` + the lockstep L-BFGS-B driver) against
 scikit-learn's own outputs (golden ``gp_lml.npz``, made by
-``tests/golden/make_lml_golden.py``).  n=230 exercises the global-memory
-variant (the factor no longer fits the LDS)."""
+``tests/golden/make_lml_golden.py``).  n up to 576 runs the block-sweep kernel;
+n = 256 and 500 are the sizes a 256-trial search reaches (real points plus the
+cl_min lies of a batch ask); MPO_FIT_KERNEL=panel re-checks the LDS Cholesky
+kernel at n <= 200."""
 import os
 import time
 
@@ -14,18 +16,29 @@ from tests.conftest import ROOT
 
 pytestmark = pytest.mark.gpu
 G = np.load(os.path.join(ROOT, "tests", "golden", "gp_lml.npz"))
-CASES = ["n200_d10", "n12_d5", "n57_d3", "n230_d4", "n130_d6"]
+CASES = ["n200_d10", "n12_d5", "n57_d3", "n230_d4", "n130_d6", "n256_d10", "n500_d10"]
+
+
+SWEEP_MIN_N, SWEEP_MAX_N = 192, 576     # csrc/gp_fit.hip kSwMinN / kSwMaxN
+
+
+def _sweep(n):
+    k = os.environ.get("MPO_FIT_KERNEL")
+    return k == "sweep" or (k != "panel" and SWEEP_MIN_N < n <= SWEEP_MAX_N)
 
 
 def _rel_tol(X, theta):
     """fp64 rounding of the LML pieces grows with cond(K); sklearn's LAPACK
-    solves and the device's explicit L^-1 round differently by up to ~cond*eps."""
+    solves and the device's explicit L^-1 round differently by up to ~cond*eps.
+    The block-sweep kernel (n > 192) inverts K by Gauss-Jordan sweeps instead of
+    a Cholesky factor: the same ~cond*eps order with a 10x larger constant."""
     n, d = X.shape
+    c = 500.0 if _sweep(n) else 50.0
     amp, ls, noise = np.exp(theta[0]), np.exp(theta[1:d + 1]), np.exp(theta[d + 1])
     M = O.matern52(X, X, ls, 1.0)
     np.fill_diagonal(M, 1.0)
     K = amp * M + (noise + 1e-10) * np.eye(n)
-    return max(1e-9, 50 * np.finfo(float).eps * np.linalg.cond(K))
+    return max(1e-9, c * np.finfo(float).eps * np.linalg.cond(K))
 
 
 def _lml(name):
@@ -49,7 +62,7 @@ def test_lml_and_gradient_match_sklearn(name):
         assert err <= tol, (b, err, tol)
 
 
-@pytest.mark.parametrize("name", ["n200_d10", "n230_d4"])
+@pytest.mark.parametrize("name", ["n200_d10", "n230_d4", "n500_d10"])
 def test_batching_does_not_change_results(name):
     dev, _ = _lml(name)
     T = G[name + "_theta"]
@@ -57,6 +70,15 @@ def test_batching_does_not_change_results(name):
     for b in range(len(T)):
         l1, g1, _ = dev.evaluate(T[b:b + 1])
         assert l1[0] == lml[b] and np.array_equal(g1[0], grad[b])
+
+
+@pytest.mark.parametrize("name,kernel", [("n200_d10", "panel"), ("n130_d6", "panel"), ("n57_d3", "sweep"),
+                                         ("n12_d5", "sweep")])
+def test_other_kernel_still_matches_sklearn(name, kernel, monkeypatch):
+    """Each LML kernel outside its default range: the Cholesky kernel at n <= 200,
+    the block sweep at small n (one pivot block with identity padding)."""
+    monkeypatch.setenv("MPO_FIT_KERNEL", kernel)
+    test_lml_and_gradient_match_sklearn(name)
 
 
 def test_non_finite_theta_reports_cholesky_failure():
