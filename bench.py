@@ -203,50 +203,57 @@ def bench_ei(args, torch, dist, ws, rank, dev):
 def bench_gp_fit(args, torch, dev, cpu):
     """GP refit: skopt's L-BFGS-B hyper-parameter search with the
     LML + gradient on the device (all restarts batched per iteration), at the
-    configs[1] problem (200 observations, D=10).  Rank 0 only: the optimizer runs
-    on the coordinator rank.  CPU baseline: sklearn's own fit on the host cores."""
-    from mpi_opt_amd import synthetic
+    configs[1] problem (200 observations, D=10) -- and at n = 256 / 500, the sizes
+    a 256-trial search reaches (real points + the cl_min lies of a batch ask).
+    Rank 0 only: the optimizer runs on the coordinator rank.  CPU baseline:
+    sklearn's own fit on the host cores (n = 200)."""
+    from mpi_opt_amd import _lib, synthetic
     from mpi_opt_amd.gp_fit import DeviceLML, fit_lml, normalize_targets
 
-    n, d = 200, 10
-    X, y = synthetic.gp_problem(n, d, 0)
-    fit_lml(X, y, random_state=0, device=dev)                        # warm (allocation, first launch)
-    reps = 3
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        _, det = fit_lml(X, y, random_state=0, device=dev, return_details=True)
-    dt = (time.perf_counter() - t0) / reps
-    lml = DeviceLML(X, normalize_targets(y)[0], device=dev)
-    T = np.zeros((3, d + 2))
-    lml.evaluate(T)
-    stream = torch.cuda.current_stream(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    from mpi_opt_amd import _lib
-
-    for _ in range(10):
-        _lib.check(_lib.lib().mpo_gp_lml_grad(
-            _lib.ptr(lml.X), _lib.ptr(lml.y), n, d, _lib.ptr(lml.theta_d), 3, _lib.ptr(lml.lml_d),
-            _lib.ptr(lml.grad_d), _lib.ptr(lml.info_d), _lib.ptr(lml.ws), lml.ws_bytes, stream.cuda_stream))
-    e1.record(stream)
-    torch.cuda.synchronize(dev)
-    t_k = e0.elapsed_time(e1) / 1e3 / 10
+    d = 10
+    sizes = {}
+    for n in (200, 256, 500):
+        X, y = synthetic.gp_problem(n, d, 0)
+        fit_lml(X, y, random_state=0, device=dev)                    # warm (allocation, first launch)
+        reps = 2 if n > 256 else 3
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            _, det = fit_lml(X, y, random_state=0, device=dev, return_details=True)
+        dt = (time.perf_counter() - t0) / reps
+        lml = DeviceLML(X, normalize_targets(y)[0], device=dev)
+        T = np.zeros((3, d + 2))
+        lml.evaluate(T)
+        stream = torch.cuda.current_stream(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(10):
+            _lib.check(_lib.lib().mpo_gp_lml_grad(
+                _lib.ptr(lml.X), _lib.ptr(lml.y), n, d, _lib.ptr(lml.theta_d), 3, _lib.ptr(lml.lml_d),
+                _lib.ptr(lml.grad_d), _lib.ptr(lml.info_d), _lib.ptr(lml.ws), lml.ws_bytes, stream.cuda_stream))
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        sizes[n] = {"fits_per_s": 1.0 / dt, "ms_per_fit": dt * 1e3, "launches_per_fit": det["launches"],
+                    "kernel_ms_per_launch": e0.elapsed_time(e1) / 10, "lml": det["lml"],
+                    "kernel": "lml_sweep_kernel" if n > 192 else "lml_grad_kernel (LDS Cholesky)"}
+    s200 = sizes[200]
     out = {"metric": "GP refits/sec (skopt LML L-BFGS-B, 3 starts, N=200 obs, D=10, fp64)",
-           "value": 1.0 / dt, "unit": "fits/s", "ms_per_fit": dt * 1e3, "launches_per_fit": det["launches"],
-           "lml": det["lml"], "dtype": "f64",
-           "kernel": {"name": "lml_grad_kernel", "ms_per_launch": t_k * 1e3, "thetas_per_launch": 3,
-                      "note": "one 1024-thread workgroup per theta: latency-bound (Cholesky/L^-1 column "
-                              "recurrences), not a roofline kernel"}}
+           "value": s200["fits_per_s"], "unit": "fits/s", "ms_per_fit": s200["ms_per_fit"],
+           "launches_per_fit": s200["launches_per_fit"], "lml": s200["lml"], "dtype": "f64",
+           "by_n": {str(k): v for k, v in sizes.items()},
+           "kernel": {"name": "lml_grad_kernel", "ms_per_launch": s200["kernel_ms_per_launch"],
+                      "thetas_per_launch": 3,
+                      "note": "one 1024-thread workgroup per theta: latency-bound (factorisation recurrences), "
+                              "not a roofline kernel; n > 192 runs the block-sweep kernel"}}
     if cpu:
         from oracle import gp_ei as O
 
+        X, y = synthetic.gp_problem(200, d, 0)
         t0 = time.perf_counter()
         st, gpr = O.fit_skopt_gp(X, y, random_state=0)
         t_cpu = time.perf_counter() - t0
-        cores = int(os.environ.get("OMP_NUM_THREADS", len(os.sched_getaffinity(0))))
-        out["cpu_baseline"] = {"value": 1.0 / t_cpu, "unit": "fits/s", "cores": cores, "kind": "port",
-                               "sample": f"one sklearn GaussianProcessRegressor.fit (the skopt refit), "
+        out["cpu_baseline"] = {"value": 1.0 / t_cpu, "unit": "fits/s", "cores": host_cores(), "kind": "port",
+                               "sample": f"one sklearn GaussianProcessRegressor.fit (the skopt refit) at n=200, "
                                          f"lml {gpr.log_marginal_likelihood_value_:.9f}, {t_cpu:.2f} s"}
     return out
 

@@ -68,9 +68,15 @@ class DeviceLML:
             raise _lib.MpoError(f"mpo_gp_lml_grad: n={self.n} d={self.d} unsupported")
         self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
         self.theta_d = torch.empty((batch, self.d + 2), dtype=torch.float64, device=self.device)
-        self.lml_d = torch.empty(batch, dtype=torch.float64, device=self.device)
-        self.grad_d = torch.empty((batch, self.d + 2), dtype=torch.float64, device=self.device)
-        self.info_d = torch.empty(batch, dtype=torch.int32, device=self.device)
+        # lml | grad | info in ONE device buffer: one device-to-host copy (one sync)
+        # per L-BFGS iteration instead of three
+        k = self.d + 2
+        self.out_d = torch.empty(batch * (k + 2), dtype=torch.float64, device=self.device)
+        self.lml_d = self.out_d[:batch]
+        self.grad_d = self.out_d[batch:batch * (k + 1)].view(batch, k)
+        self.info_d = self.out_d[batch * (k + 1):].view(torch.int32)[:batch]
+        self.theta_h = torch.empty((batch, k), dtype=torch.float64).pin_memory()
+        self.out_h = torch.empty(batch * (k + 2), dtype=torch.float64).pin_memory()
         self._cap = batch
 
     def evaluate(self, thetas):
@@ -83,13 +89,17 @@ class DeviceLML:
         # thread-local default: pin this objective's device for the launch
         with torch.cuda.device(self.device):
             self._ensure(B)
-            self.theta_d[:B].copy_(torch.from_numpy(thetas))
+            k, cap = self.d + 2, self._cap
+            self.theta_h[:B].numpy()[:] = thetas
+            self.theta_d[:B].copy_(self.theta_h[:B], non_blocking=True)
             _lib.check(_lib.lib().mpo_gp_lml_grad(
                 _lib.ptr(self.X), _lib.ptr(self.y), self.n, self.d, _lib.ptr(self.theta_d), B,
                 _lib.ptr(self.lml_d), _lib.ptr(self.grad_d), _lib.ptr(self.info_d),
                 _lib.ptr(self.ws), self.ws_bytes, _lib.stream_handle(self.device)), "mpo_gp_lml_grad")
-            return (self.lml_d[:B].cpu().numpy().copy(), self.grad_d[:B].cpu().numpy().copy(),
-                    self.info_d[:B].cpu().numpy().copy())
+            self.out_h.copy_(self.out_d)          # synchronising copy of all outputs
+            h = self.out_h.numpy()
+            return (h[:B].copy(), h[cap:cap + B * k].reshape(B, k).copy(),
+                    h[cap * (k + 1):].view(np.int32)[:B].copy())
 
 
 class _Lockstep:

@@ -8,9 +8,9 @@ export TMPDIR=/tmp
 PROG="python $R/scripts/train_probe.py --steps 1 ${PROBE_ARGS}"
 pass() {
   local tag=$1 ctr=$2
-  ( cd /tmp && timeout -s KILL ${PMC_TIMEOUT:-150} rocprofv3 --pmc $ctr -d "$R/gpurun_out/pmc_$tag" -o pmc \
+  ( cd /tmp && rm -rf /tmp/pmc_$tag && timeout -s KILL ${PMC_TIMEOUT:-150} rocprofv3 --pmc $ctr -d /tmp/pmc_$tag -o pmc \
       --output-format csv -- $PROG > "$R/gpurun_out/pmc_$tag.log" 2>&1 ) && \
-  python "$R/scripts/pmc_dump.py" "$R/gpurun_out/pmc_$tag" > "$R/gpurun_out/pmc_$tag.txt" && echo "PMC $tag OK"
+  python "$R/scripts/pmc_dump.py" /tmp/pmc_$tag > "$R/gpurun_out/pmc_$tag.txt" && echo "PMC $tag OK"
 }
 pass A "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" && \
 pass B "SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_MFMA SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_VALU SQ_LEVEL_WAVES SQ_INST_LEVEL_VMEM SQ_WAVES GRBM_GUI_ACTIVE" && \
