@@ -16,8 +16,10 @@ one rank per GPU, barrier + synchronize around the timed region, max over ranks.
 from __future__ import annotations
 
 import argparse
+import collections
 import json
 import os
+import shutil
 import sys
 import time
 
@@ -50,30 +52,88 @@ def dist_env():
     return ws, rank, local
 
 
-def load_traffic(kernel, config_key):
-    """HBM bytes per launch from the committed PMC summary (profiles/), if present
-    for exactly this kernel + workload; else None."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    try:
-        d = json.load(open(path))
-        e = d.get(kernel, {}).get(config_key)
-        return None if e is None else float(e["hbm_bytes_per_launch"])
-    except (OSError, ValueError, KeyError):
-        return None
+PMC_FAMILIES = (("conv_img_kernel<0", "conv1_fwd"), ("conv_img_kernel<1", "conv2_fwd"), ("conv_dgrad", "conv2_dgrad"),
+                ("conv_wgrad_kernel<1", "conv2_wgrad"), ("conv_wgrad_kernel<0", "conv1_wgrad"),
+                ("dense_kernel", "dense_kernel"))
 
 
-def load_population_pmc():
-    """rocprofv3 counters of the 320-member population step (committed summary,
-    scripts/pmc_train_summary.py): MFMA-busy fraction of the MFMA training kernels
-    (SQ_VALU_MFMA_BUSY_CYCLES over SIMD cycles, GUI-time weighted) and HBM bytes per
-    train batch.  None if absent."""
+def pmc_pass(counters, prog, timeout=150):
+    """One ``rocprofv3 --pmc`` pass (its own process, counters of one pass only)
+    over ``python <prog>``; returns the counter_collection rows, or raises."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+
+    d = tempfile.mkdtemp(prefix="mpo_pmc_", dir="/tmp")
     try:
-        e = json.load(open(os.path.join(ROOT, "profiles", "pmc_summary.json")))["population_step"]
-        return {"mfma_busy": e["mfma_busy"], "hbm_bytes_per_train_batch": e["hbm_bytes_per_train_step"],
-                "per_kernel_mfma_busy": {k: v["mfma_busy"] for k, v in e["per_kernel"].items()},
-                "source": e["source"]}
-    except (OSError, ValueError, KeyError):
-        return None
+        cmd = ["rocprofv3", "--pmc", *counters, "-d", d, "-o", "pmc", "--output-format", "csv", "--",
+               sys.executable, *prog]
+        r = subprocess.run(cmd, cwd="/tmp", env={**os.environ, "TMPDIR": "/tmp"}, stdout=subprocess.DEVNULL,
+                           stderr=subprocess.PIPE, timeout=timeout)
+        if r.returncode != 0:
+            raise RuntimeError(f"rocprofv3 exit {r.returncode}: {r.stderr.decode(errors='replace')[-300:]}")
+        paths = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        if not paths:
+            raise RuntimeError("rocprofv3 wrote no counter_collection.csv")
+        return list(csv.DictReader(open(paths[0])))
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def _per_dispatch(rows, counter, match):
+    vals = collections.defaultdict(float)
+    for r in rows:
+        if r["Counter_Name"] == counter and match(r["Kernel_Name"]):
+            vals[r.get("Dispatch_Id", r.get("Correlation_Id"))] += float(r["Counter_Value"])
+    return vals
+
+
+def live_pmc(train_trials):
+    """HBM traffic measured in this run (MI355X_MICROARCH.md HBM section): separate
+    FETCH_SIZE and WRITE_SIZE passes (KiB; FETCH_SIZE doubled -- gfx950 reports half
+    of a wide streaming read), per launch of gp_score_kernel over scripts/ei_probe.py
+    (the bench's EI step, 3 launches) and per train step over scripts/train_probe.py
+    (the bench's 320-member population, 3 train steps), plus one SQ pass for the
+    training kernels' MFMA-busy fraction (SQ_VALU_MFMA_BUSY_CYCLES over
+    GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs).  Runs before this process touches the
+    GPU.  Returns {"ei": ..., "train": ...}; a failed pass leaves its entry None
+    with the reason."""
+    out = {"ei": None, "train": None, "errors": []}
+    ei_prog = [os.path.join(ROOT, "scripts", "ei_probe.py"), "3"]
+    try:
+        f = _per_dispatch(pmc_pass(["FETCH_SIZE"], ei_prog), "FETCH_SIZE", lambda k: "gp_score_kernel" in k)
+        w = _per_dispatch(pmc_pass(["WRITE_SIZE"], ei_prog), "WRITE_SIZE", lambda k: "gp_score_kernel" in k)
+        fetch = 1024.0 * sum(f.values()) / len(f)
+        write = 1024.0 * sum(w.values()) / len(w)
+        out["ei"] = {"hbm_bytes_per_launch": 2.0 * fetch + write, "fetch_size_bytes_raw": fetch,
+                     "write_size_bytes": write, "launches": len(f)}
+    except Exception as e:  # noqa: BLE001 -- reported, the bench line carries traffic null
+        out["errors"].append(f"ei: {e}")
+    steps = 3
+    tr_prog = [os.path.join(ROOT, "scripts", "train_probe.py"), "--steps", "1", "--trials", str(train_trials)]
+    try:
+        ours = lambda k: "anonymous namespace" in k     # noqa: E731 -- libmpo's kernels, not torch's setup
+        f = _per_dispatch(pmc_pass(["FETCH_SIZE"], tr_prog), "FETCH_SIZE", ours)
+        w = _per_dispatch(pmc_pass(["WRITE_SIZE"], tr_prog), "WRITE_SIZE", ours)
+        fetch = 1024.0 * sum(f.values()) / steps
+        write = 1024.0 * sum(w.values()) / steps
+        rows = pmc_pass(["SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"], tr_prog)
+        per, num, den = {}, 0.0, 0.0
+        for needle, fam in PMC_FAMILIES:
+            busy = sum(_per_dispatch(rows, "SQ_VALU_MFMA_BUSY_CYCLES", lambda k: needle in k).values())
+            gui = sum(_per_dispatch(rows, "GRBM_GUI_ACTIVE", lambda k: needle in k).values())
+            if gui:
+                per[fam] = busy / (gui / 8 * 1024)
+                num += busy
+                den += gui / 8 * 1024
+        out["train"] = {"hbm_bytes_per_train_batch": 2.0 * fetch + write, "fetch_size_bytes_raw": fetch,
+                        "write_size_bytes": write, "mfma_busy": num / den if den else None,
+                        "per_kernel_mfma_busy": per}
+    except Exception as e:  # noqa: BLE001
+        out["errors"].append(f"train: {e}")
+    return out
 
 
 def host_cores():
@@ -191,7 +251,8 @@ def bench_ei(args, torch, dist, ws, rank, dev):
                    "parallelism": f"candidates sharded, {ws} GPU(s), all-gather of (value,index)"},
         "roofline": {"kernel": "gp_score_kernel", "bound": "mfma", "achieved": achieved,
                      "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
-                     "traffic": load_traffic("gp_score_kernel", f"n{n}_d{d}_m{m}"),
+                     "traffic": ((args.pmc or {}).get("ei") or {}).get("hbm_bytes_per_launch"),
+                     "traffic_detail": (args.pmc or {}).get("ei"),
                      "kernel_ms": t_kernel * 1e3,
                      "algorithmic_flops_per_launch": flops,
                      "algorithmic_hbm_bytes_per_launch": algo_bytes,
@@ -362,6 +423,8 @@ def bench_train(args, torch, dist, ws, rank, dev):
     flops = (ratio * B * sum(m.flops_per_sample_train() for m in members)
              + B * sum(m.flops_per_sample_fwd() for m in members))
     achieved = flops / (t_gpu / args.train_steps) / 1e12
+    algo_bytes = sum(m.hbm_bytes_train(B) for m in members)          # per train batch
+    pmc = (args.pmc or {}).get("train") if n_trials == 64 else None
     return {
         "metric": "MNIST-CNN trials/hour (5-fold CV, 10 epochs, 60k samples/trial-fold split)",
         "value": trials_per_hour, "unit": "trials/hour", "n_gpus": ws, "steps": args.train_steps,
@@ -374,9 +437,12 @@ def bench_train(args, torch, dist, ws, rank, dev):
                    "parallelism": f"trials sharded, {ws} GPU(s), all-gather of fold losses"},
         "roofline": {"kernel": "population step (all conv/dense MFMA kernels)", "bound": "mfma",
                      "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None,
+                     "frac": achieved / FP32_PEAK_TFLOPS,
+                     "traffic": pmc["hbm_bytes_per_train_batch"] if pmc else None,
+                     "traffic_unit": "HBM bytes per train batch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, this run)",
+                     "algorithmic_hbm_bytes_per_train_batch": algo_bytes,
                      "algorithmic_flops_per_step": flops,
-                     "pmc": load_population_pmc() if n_trials == 64 else None},
+                     "pmc": pmc},
         "_trials": trials,
     }
 
@@ -554,11 +620,20 @@ def main():
     ap.add_argument("--train-warmup", type=int, default=1)
     ap.add_argument("--dn-trials", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 traffic passes")
     args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    args.pmc = None
+    if ws == 1 and not args.no_pmc and args.workload in ("ei", "train", "all") and shutil.which("rocprofv3"):
+        t0 = time.perf_counter()
+        args.pmc = live_pmc(args.train_trials)      # child processes, before this one touches the GPU
+        args.pmc["wall_s"] = time.perf_counter() - t0
+        for e in args.pmc["errors"]:
+            print(f"warning: PMC pass failed: {e}", file=sys.stderr)
 
     import torch
 
-    ws, rank, local = dist_env()
     dist = None
     if ws > 1:
         import torch.distributed as dist

@@ -140,6 +140,16 @@ int mpo_gp_ei_score(const MpoGpModel* model, const double* cand, int64_t m,
                     double y_opt, double xi, double* mu, double* sd, double* ei,
                     int64_t* argmax, void* ws, size_t ws_bytes, void* stream);
 
+/* Acquisition value and gradient at `batch` points x [batch][d] (transformed
+ * space, device): f[b] = the minimised value of acquisition acq[b] (device int32,
+ * one of MPO_ACQ_EI / MPO_ACQ_PI / MPO_ACQ_LCB), g[b][d] its gradient.  The
+ * objective of skopt's L-BFGS-B polish of the best candidates (skopt
+ * gaussian_acquisition_1D with predict(return_mean_grad, return_std_grad)),
+ * reached from Coordinator.ask (coordinator.py:46-50); one point per live
+ * polish, all of an ask step's polishes in lockstep. */
+int mpo_gp_acq_grad(const MpoGpModel* model, const double* x, int batch, const int32_t* acq,
+                    double y_opt, double xi, double kappa, double* f, double* g, void* stream);
+
 /* ------------------------------------------------------------------------
  * Population training of ragged MNIST-CNN trials.
  * Replaces ProcessBlock.train_model -> mpi_learn MPIKFoldManager.train()

@@ -666,6 +666,154 @@ int trsm_launch(const double* L, int n, int lda, double* B, int nrhs, int ldb, i
     return MPO_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Acquisition value + gradient at a few points: the objective of skopt's
+// L-BFGS-B polish of the best n_restarts_optimizer candidates per acquisition
+// (skopt optimizer.py _tell -> fmin_l_bfgs_b(gaussian_acquisition_1D, ...,
+// maxiter=20); gaussian_acquisition_1D / gaussian_ei/pi/lcb(return_grad=True) and
+// GaussianProcessRegressor.predict(return_mean_grad, return_std_grad)).  All
+// polishes of one ask step run in lockstep, so one launch carries one point per
+// live L-BFGS-B run: one workgroup per point, the posterior as in the scoring
+// kernel but with the explicit derivative of k* (skopt gpr.py):
+//   dk_i/dx_j  = c_i (x_j - X_ij) / ls_j^2,  c_i = -(5/3) amp (1 + t_i) e^-t_i
+//   dmu/dx     = y_std dk^T alpha
+//   dsd/dx     = -y_std dk^T (W^T W k*) / sd_n,  W = L^-1
+// LDS: k*, c (n each), v = W k* (n), four per-wave partials of W^T v (4 n).
+constexpr int kGradThreads = 256;
+
+__global__ __launch_bounds__(kGradThreads) void acq_grad_kernel(
+        int n, int d, int dp, double amp, double y_mean, double y_std, const double* __restrict__ xs,
+        const double* __restrict__ ls, const double* __restrict__ alpha, const double* __restrict__ W,
+        const double* __restrict__ x, const int32_t* __restrict__ acq, double y_opt, double xi, double kappa,
+        double* __restrict__ f, double* __restrict__ g) {
+    extern __shared__ double sm[];
+    double* kk = sm;              // [n]
+    double* cc = kk + n;          // [n]
+    double* vv = cc + n;          // [n]
+    double* up = vv + n;          // [4][n]
+    __shared__ double xp[32];     // x / ls
+    __shared__ double red[kGradThreads];
+    __shared__ double ga[8][32], gu[8][32];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < 32) xp[tid] = tid < d ? x[(size_t)b * d + tid] / ls[tid] : 0.0;
+    __syncthreads();
+
+    // k*, c and mu_n partials
+    double mu_part = 0.0;
+    for (int i = tid; i < n; i += kGradThreads) {
+        double r2 = 0.0;
+        for (int j = 0; j < d; ++j) {
+            const double t = xp[j] - xs[(size_t)i * dp + j];
+            r2 = fma(t, t, r2);
+        }
+        const double t = kSqrt5 * sqrt(r2);
+        const double e = exp(-t);
+        const double k = amp * ((1.0 + t + t * t * (1.0 / 3.0)) * e);
+        kk[i] = k;
+        cc[i] = (-5.0 / 3.0) * amp * (1.0 + t) * e;
+        mu_part = fma(k, alpha[i], mu_part);
+    }
+    for (int i = tid; i < 4 * n; i += kGradThreads) up[i] = 0.0;
+    __syncthreads();
+
+    // v = W k* (rows per wave, lanes across the row), q = ||v||^2
+    double q_part = 0.0;
+    for (int r = wave; r < n; r += 4) {
+        double s = 0.0;
+        for (int c = lane; c <= r; c += 64) s = fma(W[(size_t)r * n + c], kk[c], s);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+        if (lane == 0) vv[r] = s;
+        q_part = fma(s, s, q_part);     // identical in every lane: count lane 0 only
+    }
+    if (lane != 0) q_part = 0.0;
+    __syncthreads();
+
+    // u = W^T v: wave w accumulates rows r = w (mod 4) into its own partial
+    double* uw = up + (size_t)wave * n;
+    for (int r = wave; r < n; r += 4) {
+        const double vr = vv[r];
+        for (int c = lane; c <= r; c += 64) uw[c] = fma(W[(size_t)r * n + c], vr, uw[c]);
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += kGradThreads) up[i] = (up[i] + up[n + i]) + (up[2 * n + i] + up[3 * n + i]);
+
+    // block sums of mu_n and q
+    red[tid] = mu_part;
+    __syncthreads();
+    for (int s = kGradThreads / 2; s > 0; s >>= 1) {
+        if (tid < s) red[tid] += red[tid + s];
+        __syncthreads();
+    }
+    const double mu_n = red[0];
+    __syncthreads();
+    red[tid] = q_part;
+    __syncthreads();
+    for (int s = kGradThreads / 2; s > 0; s >>= 1) {
+        if (tid < s) red[tid] += red[tid + s];
+        __syncthreads();
+    }
+    const double q = red[0];
+
+    // dk^T alpha and dk^T u per dimension: thread (grp, j) sums observations grp (mod 8)
+    {
+        const int j = tid & 31, grp = tid >> 5;
+        double sa = 0.0, su = 0.0;
+        if (j < d) {
+            for (int i = grp; i < n; i += 8) {
+                const double t = cc[i] * (xp[j] - xs[(size_t)i * dp + j]);
+                sa = fma(t, alpha[i], sa);
+                su = fma(t, up[i], su);
+            }
+        }
+        ga[grp][j] = sa;
+        gu[grp][j] = su;
+    }
+    __syncthreads();
+
+    if (tid < d) {
+        const int j = tid;
+        double sa = 0.0, su = 0.0;
+        for (int grp = 0; grp < 8; ++grp) {
+            sa += ga[grp][j];
+            su += gu[grp][j];
+        }
+        const double inv_ls = 1.0 / ls[j];
+        double var = amp - q;
+        if (var < 0.0) var = 0.0;
+        const double sd_n = sqrt(var);
+        const double mu = y_std * mu_n + y_mean;
+        const double sd = sd_n * y_std;
+        const double mu_g = y_std * sa * inv_ls;
+        const double sd_g = sd_n > 0.0 ? -y_std * su * inv_ls / sd_n : 0.0;
+        const int a = acq[b];
+        double fv, gv;
+        if (a == (int)MPO_ACQ_LCB) {
+            fv = mu - kappa * sd;
+            gv = mu_g - kappa * sd_g;
+        } else if (sd <= 0.0) {
+            fv = 0.0;
+            gv = 0.0;
+        } else {
+            const double improve = y_opt - xi - mu;
+            const double z = improve / sd;
+            const double cdf = ndtr(z), pdf = norm_pdf(z);
+            const double improve_g = (-mu_g * sd - sd_g * improve) / (sd * sd);
+            if (a == (int)MPO_ACQ_PI) {
+                fv = -cdf;
+                gv = -(improve_g * pdf);
+            } else {
+                const double cdf_g = improve_g * pdf;
+                const double pdf_g = -improve * cdf_g;
+                fv = -(improve * cdf + sd * pdf);
+                gv = -((-mu_g * cdf - pdf_g) + (sd_g * pdf + pdf_g));
+            }
+        }
+        g[(size_t)b * d + j] = gv;
+        if (j == 0) f[b] = fv;
+    }
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -892,6 +1040,24 @@ int mpo_gp_ei_score(const MpoGpModel* model, const double* cand, int64_t m, doub
                            reinterpret_cast<int64_t*>(tidx), tval, ws, ws_bytes, s);
     if (rc) return rc;
     hipLaunchKernelGGL(argmax_from_topk_kernel, dim3(1), dim3(1), 0, s, tidx, reinterpret_cast<long long*>(argmax));
+    MPO_LAUNCH_CHECK();
+    return MPO_OK;
+    MPO_GUARD_END
+}
+
+int mpo_gp_acq_grad(const MpoGpModel* model, const double* x, int batch, const int32_t* acq, double y_opt,
+                    double xi, double kappa, double* f, double* g, void* stream) {
+    MPO_GUARD_BEGIN
+    MPO_CHECK_ARG(model && x && acq && f && g, "mpo_gp_acq_grad: null pointer");
+    MPO_CHECK_ARG(batch > 0 && batch <= 65535, "mpo_gp_acq_grad: batch=%d outside [1, 65535]", batch);
+    MPO_CHECK_ARG(model->n > 0 && model->d > 0 && model->d <= 32 && model->W, "mpo_gp_acq_grad: model not prepared");
+    const size_t lds = (size_t)7 * model->n * sizeof(double);
+    if (lds > kMaxLds - 8192) { mpo::set_error("mpo_gp_acq_grad: n=%d too large", model->n); return MPO_ENOTSUP; }
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(acq_grad_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(acq_grad_kernel, dim3(batch), dim3(kGradThreads), lds, static_cast<hipStream_t>(stream),
+                       model->n, model->d, model->dp, model->amp, model->y_mean, model->y_std, model->xs, model->ls,
+                       model->alpha, model->W, x, acq, y_opt, xi, kappa, f, g);
     MPO_LAUNCH_CHECK();
     return MPO_OK;
     MPO_GUARD_END

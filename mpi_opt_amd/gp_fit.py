@@ -106,8 +106,9 @@ class _Lockstep:
     """Collects one theta from every live optimiser thread, evaluates them in one
     batch, hands each thread its own result."""
 
-    def __init__(self, evaluate, n_workers):
+    def __init__(self, evaluate, n_workers, pass_ids=False):
         self.evaluate = evaluate
+        self.pass_ids = pass_ids
         self.cv = threading.Condition()
         self.active = n_workers
         self.pending = {}
@@ -137,10 +138,11 @@ class _Lockstep:
         thetas = np.stack([self.pending[i] for i in ids])
         self.pending = {}
         try:
-            lml, grad, _ = self.evaluate(thetas)
+            out = self.evaluate(thetas, ids) if self.pass_ids else self.evaluate(thetas)
+            val, grad = out[0], out[1]
             self.launches += 1
             for k, i in enumerate(ids):
-                self.results[i] = (float(lml[k]), grad[k].copy())
+                self.results[i] = (float(val[k]), grad[k].copy())
         except BaseException as e:  # every waiting thread re-raises
             for i in ids:
                 self.results[i] = e

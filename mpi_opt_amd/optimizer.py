@@ -20,25 +20,22 @@ MI355X mapping: the candidate scoring (posterior + EI/PI/LCB + top-k over the
 candidate batch) runs in ``libmpo.so`` on the GPU (:class:`~mpi_opt_amd.gp.DeviceGP`),
 together with the GP factorisation, and so does the objective of the GP
 hyper-parameter refit (:mod:`~mpi_opt_amd.gp_fit`: LML + gradient, all L-BFGS-B
-restarts batched into one launch per iteration).  The L-BFGS-B control flow itself
-and the 5 x 20-iteration polish of single points stay on the host: they are the
-reference's host-side control flow, not per-candidate work.
+restarts batched into one launch per iteration), and so does the objective of the
+acquisition polish (``mpo_gp_acq_grad``: the 3 x 5 L-BFGS-B runs of one ask step
+batched into one launch per iteration).  Only the L-BFGS-B control flow -- the
+reference's host-side scipy loop -- stays on the host.
 """
 from __future__ import annotations
 
 import copy as _copy
-import math
+import threading
 
 import numpy as np
 from scipy.optimize import fmin_l_bfgs_b
-from scipy.stats import norm
 
 from . import _lib
 from .gp_fit import fit_lml
 from .space import Space, check_random_state
-
-SQRT5 = math.sqrt(5.0)
-
 
 # --------------------------------------------------------------------------
 # GP hyper-parameter fit (device LML objective, sklearn's restart/L-BFGS-B loop)
@@ -60,12 +57,10 @@ class GPModel:
         self.amp, self.length_scale, self.noise = float(amp), np.asarray(length_scale, float), float(noise)
         self.device = device
         self._dev = None
-        self._host = None
 
     def __getstate__(self):
         d = dict(self.__dict__)
         d["_dev"] = None
-        d["_host"] = None
         return d
 
     @property
@@ -76,59 +71,46 @@ class GPModel:
             self._dev = DeviceGP(self.Xt, self.y, self.amp, self.length_scale, self.noise, device=self.device)
         return self._dev
 
-    # host copy of the (small) factor, for single-point predictions with gradients
-    def _host_state(self):
-        if self._host is None:
-            g = self.dev
-            self._host = (g.L_inverse().cpu().numpy(), g.alpha().cpu().numpy(), g.y_mean, g.y_std)
-        return self._host
-
-    def predict_grad(self, x):
-        """mu, sd and their gradients at one transformed point (skopt
-        GaussianProcessRegressor.predict(return_mean_grad, return_std_grad))."""
-        W, alpha, y_mean, y_std = self._host_state()
-        ls2 = self.length_scale ** 2
-        diff = x[None, :] - self.Xt                       # (n, d)
-        r = np.sqrt(np.sum(diff * diff / ls2, axis=1))
-        t = SQRT5 * r
-        e = np.exp(-t)
-        k = self.amp * (1.0 + t + t * t / 3.0) * e
-        dk = (-5.0 / 3.0) * self.amp * (1.0 + t)[:, None] * e[:, None] * diff / ls2   # dk/dx (n, d)
-        mu_n = k @ alpha
-        v = W @ k
-        var = self.amp - v @ v
-        sd_n = math.sqrt(var) if var > 0 else 0.0
-        mu = y_std * mu_n + y_mean
-        mu_grad = y_std * (dk.T @ alpha)
-        if sd_n > 0:
-            sd_grad = -y_std * (dk.T @ (W.T @ v)) / sd_n
-        else:
-            sd_grad = np.zeros_like(x)
-        return mu, sd_n * y_std, mu_grad, sd_grad
-
     def predict_mean(self, X):
         mu, _ = self.dev.predict(np.atleast_2d(X))
         return mu
 
 
-def _acq_and_grad(model, x, y_opt, acq, xi, kappa):
-    """skopt gaussian_acquisition_1D: the minimised value and its gradient."""
-    mu, sd, mu_g, sd_g = model.predict_grad(np.asarray(x, dtype=float))
-    if acq == "LCB":
-        return mu - kappa * sd, mu_g - kappa * sd_g
-    if sd <= 0:
-        return 0.0, np.zeros_like(mu_g)
-    improve = y_opt - xi - mu
-    z = improve / sd
-    cdf, pdf = norm.cdf(z), norm.pdf(z)
-    improve_grad = (-mu_g * sd - sd_g * improve) / sd ** 2
-    if acq == "PI":
-        return -cdf, -(improve_grad * pdf)
-    ei = improve * cdf + sd * pdf
-    cdf_grad = improve_grad * pdf
-    pdf_grad = -improve * cdf_grad
-    grad = (-mu_g * cdf - pdf_grad) + (sd_g * pdf + pdf_grad)
-    return -ei, -grad
+def polish_lockstep(model, starts, acqs, y_opt, xi, kappa, bounds, maxiter=20):
+    """skopt's acquisition polish: ``fmin_l_bfgs_b(gaussian_acquisition_1D, x0,
+    bounds, approx_grad=False, maxiter=20)`` from every start ``starts[w]`` of
+    acquisition ``acqs[w]``.  The runs are independent; they step in lockstep (one
+    thread each, gp_fit._Lockstep) so that each round of evaluations is one
+    ``mpo_gp_acq_grad`` launch over all live runs.  Returns [(x, f)] per run."""
+    from .gp_fit import _Lockstep
+
+    codes = np.array([_lib.ACQ_FLAGS[a] for a in acqs], dtype=np.int32)
+
+    def evaluate(X, ids):
+        return model.dev.acq_grad(X, codes[ids], y_opt, xi, kappa)
+
+    step = _Lockstep(evaluate, len(starts), pass_ids=True)
+    out = [None] * len(starts)
+    errors = []
+
+    def run(w):
+        try:
+            xr, fr, _ = fmin_l_bfgs_b(lambda v: step(w, v), starts[w], bounds=bounds, approx_grad=False,
+                                      maxiter=maxiter)
+            out[w] = (xr, float(fr))
+        except BaseException as e:  # noqa: BLE001 -- re-raised on the caller's thread
+            errors.append(e)
+        finally:
+            step.retire()
+
+    threads = [threading.Thread(target=run, args=(w,), daemon=True) for w in range(len(starts))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    if errors:
+        raise errors[0]
+    return out
 
 
 class OptimizeResult(dict):
@@ -274,17 +256,16 @@ class Optimizer:
         k = 1 if self.acq_optimizer == "sampling" else min(self.n_restarts_optimizer, X.shape[0])
         top = self._score_topk(est, X, y_opt, xi, kappa, k)
         self.next_xs_ = []
+        if self.acq_optimizer == "lbfgs":
+            runs = [(a, i) for a in self.cand_acq_funcs_ for i in top[a]]
+            polished = polish_lockstep(est, [X[i] for _, i in runs], [a for a, _ in runs], y_opt, xi, kappa,
+                                       self.space.transformed_bounds)
         for acq in self.cand_acq_funcs_:
             idx = top[acq]
             if self.acq_optimizer == "sampling":
                 next_x = X[idx[0]]
             else:
-                results = []
-                for i in idx:
-                    xr, fr, _ = fmin_l_bfgs_b(lambda v, a=acq: _acq_and_grad(est, v, y_opt, a, xi, kappa),
-                                              X[i], bounds=self.space.transformed_bounds, approx_grad=False,
-                                              maxiter=20)
-                    results.append((xr, fr))
+                results = [polished[w] for w, (a, _) in enumerate(runs) if a == acq]
                 cand_xs = np.array([r[0] for r in results])
                 cand_acqs = np.array([r[1] for r in results])
                 next_x = cand_xs[np.argmin(cand_acqs)]

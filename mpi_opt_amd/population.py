@@ -65,6 +65,23 @@ class TrialSpec:
         k, F = self.kernel_size, self.nb_filters
         return 3 * self.flops_per_sample_fwd() - 2 * k * k * F * self.geometry()["H1"] ** 2
 
+    def hbm_bytes_train(self, batch):
+        """Algorithmic HBM bytes of one train step of this member over ``batch``
+        samples: the layer-by-layer schedule with every tensor written once and
+        read once per consuming kernel (f32).  Per sample: x read by conv1 fwd and
+        wgrad; a1 written, read by conv2 fwd / conv2 wgrad / dgrad's ReLU mask;
+        a2 written and read by the pool; dz2 written, read by conv2 wgrad and
+        dgrad; dz1 written, read by conv1 wgrad; the pooled / dense activations
+        and their gradients (K1, dense, 10) written and read twice.  Per member:
+        weights read twice (fwd, bwd), gradient written and read, Adam m, v read
+        and written, weights written."""
+        F, D = self.nb_filters, self.dense
+        g = self.geometry()
+        a1, a2, K1 = g["H1"] ** 2 * F, g["H2"] ** 2 * F, g["K1"]
+        per_sample = 2 * IMG * IMG + 4 * a1 + 2 * a2 + 3 * a2 + 2 * a1 + 3 * 2 * (K1 + D + NUM_CLASSES)
+        n_params = sum(int(np.prod(s)) for s in self.param_shapes().values())
+        return 4 * (batch * per_sample + 8 * n_params)
+
 
 MpoCnnSpec = _lib.MpoCnnSpec
 MpoPopSizes = _lib.MpoPopSizes

@@ -78,3 +78,80 @@ def test_pickle_roundtrip_after_fit(tmp_path):
     x = o2.ask()
     o2.tell(x, f2(x))      # refits on the device after unpickling
     assert len(o2.models) == len(opt.models) + 1
+
+
+@pytest.mark.parametrize("n,d", [(40, 5), (200, 10), (500, 10)])
+def test_acq_grad_matches_oracle(n, d):
+    """mpo_gp_acq_grad (the polish objective) against the oracle's restatement of
+    skopt gaussian_acquisition_1D: values and gradients of -EI, -PI and LCB at
+    random points, at an observation (sd -> 0) and at the box corners."""
+    from mpi_opt_amd.gp import DeviceGP
+    from mpi_opt_amd import _lib
+
+    X, y = O.synthetic_problem(n, d, seed=n)
+    amp, ls, noise = 1.7, np.linspace(0.3, 1.2, d), 1e-4
+    st = O.gp_from_theta(X, y, amp, ls, noise)
+    g = DeviceGP(X, y, amp, ls, noise, device="cuda:0")
+    rng = np.random.RandomState(1)
+    P = np.vstack([rng.uniform(size=(12, d)), X[3], np.zeros(d), np.ones(d)])
+    y_opt = float(np.min(y))
+    for acq in ("EI", "PI", "LCB"):
+        f, grad = g.acq_grad(P, [_lib.ACQ_FLAGS[acq]] * len(P), y_opt, 0.01, 1.96)
+        for b, x in enumerate(P):
+            fo, go = O.acquisition_and_grad(st, x, y_opt, acq)
+            scale = max(1.0, abs(fo))
+            assert abs(f[b] - fo) <= 1e-8 * scale, (acq, b, f[b], fo)
+            gs = max(1.0, np.abs(go).max())
+            np.testing.assert_allclose(grad[b], go, rtol=0, atol=1e-7 * gs, err_msg=f"{acq} point {b}")
+
+
+def test_acq_grad_mixed_batch_and_finite_differences():
+    """One launch over points with different acquisitions (the lockstep batch);
+    the gradient is the derivative of the value (central differences)."""
+    from mpi_opt_amd.gp import DeviceGP
+    from mpi_opt_amd import _lib
+
+    X, y = O.synthetic_problem(120, 6, seed=4)
+    g = DeviceGP(X, y, 1.1, np.full(6, 0.6), 1e-3, device="cuda:0")
+    rng = np.random.RandomState(2)
+    P = rng.uniform(0.1, 0.9, size=(15, 6))
+    acqs = ["EI", "LCB", "PI"] * 5
+    codes = [_lib.ACQ_FLAGS[a] for a in acqs]
+    y_opt = float(np.min(y))
+    f, grad = g.acq_grad(P, codes, y_opt)
+    for b in range(len(P)):
+        f1, _ = g.acq_grad(P[b:b + 1], codes[b:b + 1], y_opt)
+        assert f1[0] == f[b]            # batch composition does not change a point's value
+        h = 1e-6
+        fd = np.empty(6)
+        for j in range(6):
+            e = np.zeros(6)
+            e[j] = h
+            fp, _ = g.acq_grad((P[b] + e)[None], codes[b:b + 1], y_opt)
+            fm, _ = g.acq_grad((P[b] - e)[None], codes[b:b + 1], y_opt)
+            fd[j] = (fp[0] - fm[0]) / (2 * h)
+        np.testing.assert_allclose(grad[b], fd, rtol=1e-4, atol=1e-7, err_msg=acqs[b])
+
+
+def test_polish_lockstep_matches_sequential_lbfgs():
+    """The 3 x 5 lockstep polishes give what sequential fmin_l_bfgs_b runs on the
+    oracle objective give (same starts, bounds, maxiter=20)."""
+    from scipy.optimize import fmin_l_bfgs_b
+
+    from mpi_opt_amd.optimizer import GPModel, polish_lockstep
+
+    X, y = O.synthetic_problem(150, 5, seed=7)
+    amp, ls, noise = 0.9, np.full(5, 0.4), 1e-4
+    st = O.gp_from_theta(X, y, amp, ls, noise)
+    model = GPModel(X, y, amp, ls, noise, device="cuda:0")
+    rng = np.random.RandomState(3)
+    acqs = [a for a in ("EI", "LCB", "PI") for _ in range(5)]
+    starts = [rng.uniform(size=5) for _ in acqs]
+    bounds = [(0.0, 1.0)] * 5
+    y_opt = float(np.min(y))
+    got = polish_lockstep(model, starts, acqs, y_opt, 0.01, 1.96, bounds)
+    for w, (a, x0) in enumerate(zip(acqs, starts)):
+        xr, fr, _ = fmin_l_bfgs_b(lambda v, a=a: O.acquisition_and_grad(st, v, y_opt, a), x0, bounds=bounds,
+                                  approx_grad=False, maxiter=20)
+        assert abs(got[w][1] - fr) <= 1e-7 * max(1.0, abs(fr)), (w, a, got[w][1], fr)
+        np.testing.assert_allclose(got[w][0], xr, atol=1e-4)
