@@ -68,6 +68,7 @@ typedef struct MpoGpModel {
     const double* L;       /* [n][n]   lower Cholesky factor        */
     const double* W;       /* [n][n]   L^-1 (lower)                 */
     int32_t* info;         /* device int: 0 ok, j+1 = chol failed at column j */
+    const int32_t* wmeta;  /* per-wave B-stream plan of wfrag (scoring kernel) */
 } MpoGpModel;
 
 /* K(i,j) = amp * Matern52(|X_i/ls - X_j/ls|) + (i==j ? diag_add : 0).

@@ -51,37 +51,47 @@ __device__ __forceinline__ double matern52(double r, double amp) {
 
 // exp(-k) for k >= 0 without the generic exp's special-case handling (k is a
 // scaled distance: never negative, never NaN): Cody-Waite reduction
-// k = n ln2 + r, |r| <= ln2/2, degree-13 Taylor polynomial of exp(-r) (truncation
-// < 4e-18 relative), 2^-n by ldexp.  k is clamped at 800 (exp(-800) underflows to
-// exactly 0, as the padding rows need).  Within 2 ulp of exp(-k).
-__device__ __forceinline__ double exp_neg(double k) {
-    k = fmin(k, 800.0);
-    const double t = rint(k * 1.44269504088896340736);
-    const double r = fma(-t, 1.90821492927058770002e-10, fma(-t, 6.93147180369123816490e-01, k));
-    const double x = -r;
-    double p = 1.0 / 6227020800.0;                  // 1/13!
-    p = fma(p, x, 1.0 / 479001600.0);
-    p = fma(p, x, 1.0 / 39916800.0);
-    p = fma(p, x, 1.0 / 3628800.0);
-    p = fma(p, x, 1.0 / 362880.0);
-    p = fma(p, x, 1.0 / 40320.0);
-    p = fma(p, x, 1.0 / 5040.0);
-    p = fma(p, x, 1.0 / 720.0);
-    p = fma(p, x, 1.0 / 120.0);
-    p = fma(p, x, 1.0 / 24.0);
-    p = fma(p, x, 1.0 / 6.0);
-    p = fma(p, x, 0.5);
-    p = fma(p, x, 1.0);
-    p = fma(p, x, 1.0);
-    return ldexp(p, -(int)t);
+// -k = t ln2 + s, |s| <= ln2/2, with t = round(-k log2 e) from the 1.5*2^52
+// rounding constant (no v_rndne), a degree-11 polynomial of e^s fitted at the
+// Chebyshev nodes (8.6e-18 relative in exact arithmetic; 13 Taylor terms before),
+// 2^t by ldexp from the saturating v_cvt_i32 of t: exp(-k) underflows to exactly
+// 0 for every k past ~745 and stays finite for every k < ~1e20 (|xs| far beyond
+// what a [0,1]-transformed space with skopt's length-scale bounds produces), so
+// no clamp instruction is needed.  Within 2 ulp of exp(-k).
+// a*b + c with the constant c read from an SGPR pair.  Written as plain fma the
+// compiler keeps loop-invariant coefficients in VGPRs and turns each Horner step
+// into v_mov_b64 + v_fmac_f64 (10 extra moves and 20 VGPRs per Matern).
+__device__ __forceinline__ double fma_sc(double a, double b, double c) {
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+    return r;
 }
 
-// sqrt of a non-negative finite r2 by v_rsq_f64, a Goldschmidt step and one
+__device__ __forceinline__ double exp_neg(double k) {
+    constexpr double kRound = 6755399441055744.0;           // 1.5 * 2^52
+    const double t = fma(k, -1.44269504088896340736, kRound) - kRound;
+    double x = fma(t, -6.93147180369123816490e-01, -k);
+    x = fma(t, -1.90821492927058770002e-10, x);
+    double p = 2.511274345242859e-08;
+    p = fma_sc(p, x, 2.76326459433635e-07);
+    p = fma_sc(p, x, 2.755723242556338e-06);
+    p = fma_sc(p, x, 2.4801485486569327e-05);
+    p = fma_sc(p, x, 0.00019841269899541455);
+    p = fma_sc(p, x, 0.0013888888952271288);
+    p = fma_sc(p, x, 0.008333333333315002);
+    p = fma_sc(p, x, 0.04166666666648857);
+    p = fma_sc(p, x, 0.1666666666666669);
+    p = fma_sc(p, x, 0.5000000000000018);
+    p = fma(p, x, 1.0);
+    p = fma(p, x, 1.0);
+    return ldexp(p, (int)t);
+}
+
+// sqrt of r2 >= 1e-300 (the distance loops start their sum at 1e-300, so a zero
+// distance never reaches v_rsq as 0) by v_rsq_f64, a Goldschmidt step and one
 // Newton correction (ocml's sequence without its denormal scaling and 0/inf
-// fix-ups: r2 is clamped below at 1e-300, whose square root 1e-150 gives the same
-// Matern value as 0).  Within 2 ulp; an ulp of r moves K* by <= 1e-14 relative.
+// fix-ups).  Within 2 ulp; an ulp of r moves K* by <= 1e-14 relative.
 __device__ __forceinline__ double sqrt_pos(double r2) {
-    r2 = fmax(r2, 1e-300);
     const double y = __builtin_amdgcn_rsq(r2);
     double s = r2 * y, h = 0.5 * y;
     const double e0 = fma(-h, s, 0.5);
@@ -90,6 +100,9 @@ __device__ __forceinline__ double sqrt_pos(double r2) {
     const double e1 = fma(-s, s, r2);
     return fma(e1, h, s);
 }
+
+// first term of every pairwise squared-distance sum (see sqrt_pos)
+constexpr double kR2Floor = 1e-300;
 
 // The scoring kernel's Matern WITHOUT the ConstantKernel amplitude:
 // (1 + k + k^2/3) exp(-k), k = sqrt(5 r2), k^2/3 = r2 * 5/3.  The kernel folds amp
@@ -126,10 +139,9 @@ __device__ __forceinline__ void wave_lex_min(double& v, long long& i) {
     }
 }
 
-// Rows [n, rows) are padding: a point 1e30 away in every real dimension, whose
-// Matern value underflows to exactly 0 (and alpha is 0 there): a scoring loop may
-// run over whole 32-observation groups without bounds checks.
-constexpr double kFarAway = 1e30;
+// Rows [n, rows) of xs are zero padding (alpha and the L^-1 fragments are zero
+// there): a scoring loop may run over whole 16-observation groups without bounds
+// checks; the padding K* values are finite and contribute nothing.
 
 __global__ void scale_rows_kernel(const double* __restrict__ X, int n, int rows, int d, int dp,
                                   const double* __restrict__ ls, double* __restrict__ xs,
@@ -137,7 +149,7 @@ __global__ void scale_rows_kernel(const double* __restrict__ X, int n, int rows,
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t < rows * dp) {
         const int i = t / dp, c = t % dp;
-        xs[t] = c < d ? (i < n ? X[(size_t)i * d + c] / ls[c] : kFarAway) : 0.0;
+        xs[t] = (c < d && i < n) ? X[(size_t)i * d + c] / ls[c] : 0.0;
     }
     if (ls_pad && t < dp) ls_pad[t] = t < d ? ls[t] : 1.0;
 }
@@ -252,14 +264,54 @@ __global__ void copy_kernel(const double* __restrict__ src, double* __restrict__
     if (t < n) dst[t] = src[t];
 }
 
-// B-fragment stream of W^T (W = L^-1 lower): column tile jt of 16 columns needs
-// the k-steps ks < 4(jt+1) (rows i <= 16 jt + 15); lane l of k-step ks holds
-// W^T[4 ks + (l>>4)][16 jt + (l&15)] = W[16 jt + (l&15)][4 ks + (l>>4)].
-__host__ __device__ constexpr size_t wfrag_tile_base(int jt) { return (size_t)128 * jt * (jt + 1); }
-inline size_t wfrag_elems(int np16) { return wfrag_tile_base(np16 / 16) + 16 * 64; }  // + prefetch slack
+// B-fragment streams of W^T (W = L^-1 lower), one per scoring wave.
+// Column tile jt (16 columns) needs the k-steps ks < 4(jt+1) (rows i <= 16 jt + 15):
+// jt+1 groups of 4 k-steps; lane l of k-step ks holds
+//   W^T[4 ks + (l>>4)][16 jt + (l&15)] = W[16 jt + (l&15)][4 ks + (l>>4)].
+// The T tiles are dealt to the block's 4 waves by LPT on their group counts, and each
+// wave's tiles are stored back to back, so a wave reads one contiguous stream across
+// its tile boundaries (a software pipeline that never drains), followed by
+// kStreamSlack groups of zeros for the prefetch that runs past its end.
+// wmeta (int32): wave record w at w*(T+4): [group offset, groups, tiles, jt...];
+//                tile_off[jt] at 4*(T+4) + jt (group offset of tile jt's first group).
+constexpr int kStreamSlack = 2;   // = the ring depth of the scoring kernel's B pipeline
+inline size_t wfrag_elems(int np16) {
+    const size_t T = np16 / 16;
+    return (T * (T + 1) / 2 + 4 * kStreamSlack) * 256;
+}
+inline size_t wmeta_elems(int np16) {
+    const int T = np16 / 16;
+    return (size_t)4 * (T + 4) + T + 4;
+}
+
+__global__ void wave_plan_kernel(int T, int32_t* __restrict__ meta) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    int load[4] = {0, 0, 0, 0}, cnt[4] = {0, 0, 0, 0};
+    for (int jt = T - 1; jt >= 0; --jt) {       // LPT: costliest tile to the least loaded wave
+        int w = 0;
+        for (int v = 1; v < 4; ++v)
+            if (load[v] < load[w]) w = v;
+        meta[w * (T + 4) + 3 + cnt[w]++] = jt;
+        load[w] += jt + 1;
+    }
+    int off = 0;
+    for (int w = 0; w < 4; ++w) {
+        int32_t* r = meta + w * (T + 4);
+        r[0] = off;
+        r[1] = load[w];
+        r[2] = cnt[w];
+        for (int t = cnt[w]; t <= T; ++t) r[3 + t] = 0;
+        int g = off;
+        for (int t = 0; t < cnt[w]; ++t) {
+            meta[4 * (T + 4) + r[3 + t]] = g;
+            g += r[3 + t] + 1;
+        }
+        off += load[w] + kStreamSlack;
+    }
+}
 
 __global__ void pack_wfrag_kernel(const double* __restrict__ W, int n, int ldw, int T,
-                                  double* __restrict__ wfrag) {
+                                  const int32_t* __restrict__ meta, double* __restrict__ wfrag) {
     const int jt = blockIdx.y;
     if (jt >= T) return;
     const int nks = 4 * (jt + 1);
@@ -268,10 +320,12 @@ __global__ void pack_wfrag_kernel(const double* __restrict__ W, int n, int ldw, 
     const int ks = e >> 6, l = e & 63;
     const int i = 4 * ks + (l >> 4), j = 16 * jt + (l & 15);
     const double v = (i < n && j < n && i <= j) ? W[(size_t)j * ldw + i] : 0.0;
-    wfrag[wfrag_tile_base(jt) + e] = v;
+    wfrag[(size_t)meta[4 * (T + 4) + jt] * 256 + e] = v;
 }
 
 // ---------------------------------------------------------------------------
+constexpr int kBM = 16;   // candidates per scoring workgroup (one 16-row MFMA m-tile)
+
 struct ScoreArgs {
     int n, np16, T, d;
     double amp, y_mean, y_std;
@@ -279,26 +333,38 @@ struct ScoreArgs {
     const double* ls;
     const double* alpha;
     const double* wfrag;
+    const int32_t* wmeta;
     const double* cand;
     long long m;
     double y_opt, xi, kappa;
     unsigned flags;
     int ei_positive;  // write +EI (mpo_gp_ei_score) instead of -EI into vals
+    int dbg;          // MPO_GP_DEBUG phase switches (timing experiments only; results invalid):
+                      // bit 0 skips the MFMA phase, bit 1 the Matern arithmetic, bit 2 the top-k
     double* mu;
     double* sd;
     double* vals;
     int k;
-    long long* part_idx;  // [nblocks][3][k]
+    long long* part_idx;  // [nparts][3][k]
     double* part_val;
+    double* mq;           // [m][2] (mu_n, q): scoring kernel -> score_finish_kernel
 };
 
-// Posterior, acquisitions and the tile's top-k from mu_n = K* alpha and
-// q = ||L^-1 k*||^2 of one candidate per lane (``live`` lanes own a row).
-__device__ __forceinline__ void score_epilogue(const ScoreArgs& a, bool live, long long gm, double mu_n, double q,
-                                               long long part, int lane) {
-    const bool valid = live && gm < a.m;
+// Posterior, acquisitions and per-wave top-k from the scoring kernel's
+// (mu_n = amp K'.alpha, q = amp^2 ||L^-1 K'||^2) per candidate: one candidate per
+// thread, every lane live (the scoring kernel's 16-candidate tiles would leave
+// 48 of 64 lanes idle here).  Wave w of block b writes part list b*4 + w.
+constexpr int kFinishThreads = 256;
+constexpr int kFinishCands = 64;   // candidates per partial top-k list (one wave)
+
+__global__ __launch_bounds__(kFinishThreads) void score_finish_kernel(ScoreArgs a, const double* __restrict__ mq) {
+    const int lane = threadIdx.x & 63;
+    const long long gm = (long long)blockIdx.x * kFinishThreads + threadIdx.x;
+    const long long part = gm >> 6;
+    const bool valid = gm < a.m;
     double mu = 0.0, sd = 0.0, vei = 0.0, vpi = 0.0, vlcb = 0.0;
-    if (live) {
+    if (valid) {
+        const double mu_n = mq[2 * gm], q = mq[2 * gm + 1];
         double var = a.amp - q;
         if (var < 0.0) var = 0.0;
         sd = sqrt(var) * a.y_std;
@@ -314,8 +380,6 @@ __device__ __forceinline__ void score_epilogue(const ScoreArgs& a, bool live, lo
             vpi = -0.0;
         }
         vlcb = mu - a.kappa * sd;
-    }
-    if (valid) {
         if (a.mu) a.mu[gm] = mu;
         if (a.sd) a.sd[gm] = sd;
         if (a.vals) {
@@ -324,71 +388,116 @@ __device__ __forceinline__ void score_epilogue(const ScoreArgs& a, bool live, lo
             if (a.flags & MPO_ACQ_LCB) a.vals[2 * a.m + gm] = vlcb;
         }
     }
-    if (a.k > 0) {
-        const double inf = __builtin_huge_val();
+    if (a.k <= 0 || (a.dbg & 4) || (long long)blockIdx.x * kFinishThreads + (threadIdx.x & ~63) >= a.m) return;
+    const double inf = __builtin_huge_val();
+    const long long big = 0x7fffffffffffffffLL;
 #pragma unroll
-        for (int acq = 0; acq < 3; ++acq) {
-            if (!(a.flags & (1u << acq))) continue;
-            double v = valid ? (acq == 0 ? vei : (acq == 1 ? vpi : vlcb)) : inf;
-            long long idx = valid ? gm : 0x7fffffffffffffffLL;
-            long long* pi = a.part_idx + ((size_t)part * 3 + acq) * a.k;
-            double* pv = a.part_val + ((size_t)part * 3 + acq) * a.k;
-            for (int r = 0; r < a.k; ++r) {
-                double bv = v;
-                long long bi = idx;
-                wave_lex_min(bv, bi);
-                if (lane == 0) { pv[r] = bv; pi[r] = bi; }
-                if (idx == bi) { v = inf; idx = 0x7fffffffffffffffLL; }
-            }
+    for (int acq = 0; acq < 3; ++acq) {
+        if (!(a.flags & (1u << acq))) continue;
+        double v = valid ? (acq == 0 ? vei : (acq == 1 ? vpi : vlcb)) : inf;
+        long long idx = valid ? gm : big;
+        long long* pi = a.part_idx + ((size_t)part * 3 + acq) * a.k;
+        double* pv = a.part_val + ((size_t)part * 3 + acq) * a.k;
+        for (int r = 0; r < a.k; ++r) {
+            double bv = v;
+            long long bi = idx;
+            wave_lex_min(bv, bi);
+            if (lane == 0) { pv[r] = bv; pi[r] = bi; }
+            if (idx == bi) { v = inf; idx = big; }
         }
     }
 }
 
-template <int BM, int DP, int D, int OCC>
+// One workgroup = 4 waves looping over 16-candidate tiles (kBM) tile = blockIdx.x,
+// += gridDim.x (the grid is sized to the resident capacity); the next tile's
+// candidate rows are loaded while the current one is scored.
+template <int DP, int D, int OCC>
 __global__ __launch_bounds__(256, OCC) void gp_score_kernel(ScoreArgs a) {
-    constexpr int MT = BM / 16;      // 16-row m-tiles per block
-    constexpr int G = 64 / BM;       // lanes groups per wave in phase 1
-    constexpr int S = 4 * G;         // i-slots per block in phase 1
+    constexpr int BM = kBM;
+    constexpr int S = 16;            // i-slots per block in phase 1 (4 per wave)
+    constexpr int EPT = (BM * DP + 255) / 256;   // candidate elements per thread in phase 0
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int np16 = a.np16;
-    double* kc = smem;                          // [np16/4][MT][64]
+    double* kc = smem;                          // [np16/4][64]: k-step ks at kc[ks*64]
     double* cs = kc + (size_t)np16 * BM;        // [BM][DP]
     double* red = cs + BM * DP;                 // [S][BM] (mu) then [4][BM] (q)
+    int32_t* mls = reinterpret_cast<int32_t*>(red + S * BM);   // the 4 wave records of wmeta
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const long long m0 = (long long)blockIdx.x * BM;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const long long ntiles = (a.m + BM - 1) / BM;
 
-    // ---- phase 0: candidate tile / ls -> LDS
-    for (int e = tid; e < BM * DP; e += 256) {
-        const int r = e / DP, c = e % DP;
-        const long long gm = m0 + r;
-        cs[e] = (gm < a.m && c < a.d) ? a.cand[gm * a.d + c] / a.ls[c] : 0.0;
+    for (int e = tid; e < 4 * (a.T + 4); e += 256) mls[e] = a.wmeta[e];
+    // thread tid owns elements tid + 256 u of the [BM][DP] candidate tile
+    double raw[EPT], ls_e[EPT];
+#pragma unroll
+    for (int u = 0; u < EPT; ++u) {
+        const int c = (tid + 256 * u) % DP;
+        ls_e[u] = c < a.d ? a.ls[c] : 1.0;
     }
+#define MPO_LOAD_TILE(TILE)                                                                    \
+    _Pragma("unroll") for (int u = 0; u < EPT; ++u) {                                          \
+        const int e = tid + 256 * u, r = e / DP, c = e % DP;                                   \
+        const long long gm = (TILE) * BM + r;                                                  \
+        raw[u] = (e < BM * DP && gm < a.m && c < a.d) ? a.cand[gm * a.d + c] : 0.0;            \
+    }
+    MPO_LOAD_TILE((long long)blockIdx.x)
     __syncthreads();
 
-    // ---- phase 1: K*[row][i] (Matern52) in A-fragment order, mu partials
+    // Phase-2 B-fragment stream of this wave (rotated by block so the heaviest one
+    // does not always land on the same SIMD).  B fragments arrive through asm loads
+    // with explicit vmcnt waits: the compiler's own waitcnt placement drained the
+    // ring every iteration (vmcnt(0) before register copies).  The ring lives
+    // inside phase 2 only and is drained at its end: a compiler copy of a ring
+    // register across a loop back-edge would read it before its load lands (a
+    // ring kept in flight across candidate tiles failed parity exactly so).
+    const int sw = (wave + (int)blockIdx.x) & 3;
+    const int32_t* mw = mls + sw * (a.T + 4);        // LDS: no vmcnt wait at tile ends
+    const int G = (a.dbg & 1) ? 0 : __builtin_amdgcn_readfirstlane(mw[1]);
+    const double* bs = a.wfrag + (size_t)__builtin_amdgcn_readfirstlane(mw[0]) * 256 + lane;
+#define MPO_LD(D, P, OFF) asm volatile("global_load_dwordx2 %0, %1, off offset:" #OFF : "=v"(D) : "v"(P) : "memory")
+#define MPO_LD4(B, P) { MPO_LD(B[0], P, 0); MPO_LD(B[1], P, 512); MPO_LD(B[2], P, 1024); MPO_LD(B[3], P, 1536); }
+
+    for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const long long m0 = tile * BM;
+
+    // ---- phase 0: candidate tile / ls -> LDS; the next tile's rows start loading
+#pragma unroll
+    for (int u = 0; u < EPT; ++u)
+        if (tid + 256 * u < BM * DP) cs[tid + 256 * u] = raw[u] / ls_e[u];
+    MPO_LOAD_TILE(tile + gridDim.x)
+    __syncthreads();
+
+    // ---- phase 1: K*[row][i] (Matern52) in A-fragment order, mu partials.  xs and
+    // alpha hold far-away / zero rows up to np16 + 16: no bounds check on i, and the
+    // next observation row is loaded while the current one is evaluated.
     {
-        const int row = lane % BM;
-        const int slot = wave * G + lane / BM;
-        double c[DP];
+        const int row = lane & 15;
+        const int slot = wave * 4 + (lane >> 4);
+        double c[D];
 #pragma unroll
-        for (int q = 0; q < DP; ++q) c[q] = cs[row * DP + q];
+        for (int q = 0; q < D; ++q) c[q] = cs[row * DP + q];
         double mu_acc = 0.0;
-        const int kc_row = (row >> 4) * 64 + (row & 15);
-        for (int i = slot; i < np16; i += S) {
-            double kv = 0.0;
-            if (i < a.n) {
-                const double* xi_ = a.xs + (size_t)i * DP;
-                double r2 = 0.0;
-#pragma unroll
-                for (int q = 0; q < D; ++q) {      // D real dims of the DP-padded rows
-                    const double t = c[q] - xi_[q];
-                    r2 += t * t;
-                }
-                kv = matern52_unit(r2);             // amp folded into mu and q below
-                mu_acc += kv * a.alpha[i];
+        if (a.dbg & 2) {
+            for (int i = slot; i < np16; i += S) kc[(size_t)(i >> 2) * 64 + row + (i & 3) * 16] = c[0];
+        } else {
+            // one observation row: r2, Matern, mu partial, K* into LDS
+#define MPO_EI_PAIR(XC, AC, I)                                                                     \
+            {                                                                                      \
+                double r2 = kR2Floor;                                                              \
+                _Pragma("unroll") for (int q = 0; q < D; ++q) {                                    \
+                    const double t = c[q] - XC[q];                                                 \
+                    r2 = fma(t, t, r2);                                                            \
+                }                                                                                  \
+                const double kv = matern52_unit(r2);   /* amp folded into mu and q below */        \
+                mu_acc = fma(kv, AC, mu_acc);                                                      \
+                kc[(size_t)((I) >> 2) * 64 + row + ((I) & 3) * 16] = kv;                           \
             }
-            kc[(size_t)((i >> 2) * MT) * 64 + kc_row + (i & 3) * 16] = kv;
+            for (int i = slot; i < np16; i += S) {
+                const double* xr = a.xs + (size_t)i * DP;
+                MPO_EI_PAIR(xr, a.alpha[i], i)
+            }
+#undef MPO_EI_PAIR
         }
         red[slot * BM + row] = mu_acc;
     }
@@ -401,87 +510,74 @@ __global__ __launch_bounds__(256, OCC) void gp_score_kernel(ScoreArgs a) {
     }
     __syncthreads();  // red is reused for the q partials below
 
-    // ---- phase 2: V = K* L^-T on f64 MFMA, lower-triangular k-steps only
+    // ---- phase 2: V = K* L^-T on f64 MFMA, lower-triangular k-steps only.  The
+    // wave walks its B-fragment stream (wave_plan_kernel) two 4-k-step groups ahead;
+    // the refills past the stream's end fetch the next candidate tile's first groups.
     {
-        double sq[MT][4];
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) sq[mt][r] = 0.0;
-        const int T = a.T;
-        for (int p = 0; p < T; ++p) {
-            const int q8 = p & 7;
-            const int owner = q8 < 4 ? q8 : 7 - q8;  // snake over descending tile cost
-            if (owner != wave) continue;
-            const int jt = T - 1 - p;
-            const double* bp = a.wfrag + wfrag_tile_base(jt) + lane;
-            const int nks = 4 * (jt + 1);
-            // CH independent accumulation chains per m-tile (k-step mod CH) hide
-            // the f64 MFMA dependency latency: 4 chains at one m-tile per wave.
-            constexpr int CH = 2;   // 4 chains at MT = 1 measured slower (1.94 vs 1.68 ms / 1M)
-            f64x4 acc[MT][CH];
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                for (int c = 0; c < CH; ++c) acc[mt][c] = f64x4{0.0, 0.0, 0.0, 0.0};
-            // nks is a multiple of 4.  B fragments stream from L2 two 4-k-step groups
-            // ahead (8 MFMAs ~ the L2 latency); slots past the tile read the next
-            // tile's fragments (wfrag has 8 k-steps of slack at its end), unused.
-            double bq[2][4];
-#pragma unroll
-            for (int g = 0; g < 2; ++g)
-#pragma unroll
-                for (int u = 0; u < 4; ++u) bq[g][u] = bp[(4 * g + u) * 64];
-            for (int ks = 0; ks < nks; ks += 8) {
-#pragma unroll
-                for (int g = 0; g < 2; ++g) {
-                    if (ks + 4 * g >= nks) break;
-                    const double* ap = kc + (size_t)(ks + 4 * g) * MT * 64 + lane;
-                    double cur[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        cur[u] = bq[g][u];
-                        bq[g][u] = bp[(ks + 8 + 4 * g + u) * 64];
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-#pragma unroll
-                        for (int mt = 0; mt < MT; ++mt)
-                            acc[mt][u % CH] = __builtin_amdgcn_mfma_f64_16x16x4f64(ap[(u * MT + mt) * 64], cur[u],
-                                                                                 acc[mt][u % CH], 0, 0, 0);
-                }
-            }
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    double v = acc[mt][0][r];
-#pragma unroll
-                    for (int c = 1; c < CH; ++c) v += acc[mt][c][r];
-                    sq[mt][r] += v * v;
-                }
+        double b0[4], b1[4];
+        MPO_LD4(b0, bs);
+        MPO_LD4(b1, bs + 256);
+        const double* bp = bs + 512;
+        const double* kl = kc + lane;
+        double sq[4] = {0.0, 0.0, 0.0, 0.0};
+        f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+        int t = 0, kg = 0, tlen = __builtin_amdgcn_readfirstlane(mw[3] + 1);
+        // one group: 4 MFMAs on two accumulation chains, then the ring slot is
+        // refilled with the group two ahead; at a column tile's last group
+        // ||V_row||^2 takes the tile's columns
+#define MPO_EI_GROUP(B)                                                                            \
+        {                                                                                          \
+            asm volatile("s_waitcnt vmcnt(4)" : "+v"(B[0]), "+v"(B[1]), "+v"(B[2]), "+v"(B[3])); \
+            const double* ap = kl + kg * 256;                                                      \
+            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(ap[0], B[0], acc0, 0, 0, 0);              \
+            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ap[64], B[1], acc1, 0, 0, 0);             \
+            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(ap[128], B[2], acc0, 0, 0, 0);            \
+            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ap[192], B[3], acc1, 0, 0, 0);            \
+            MPO_LD4(B, bp);                                                                        \
+            bp += 256;                                                                             \
+            if (++kg == tlen) {                                                                    \
+                _Pragma("unroll") for (int r = 0; r < 4; ++r) {                                    \
+                    const double v = acc0[r] + acc1[r];                                            \
+                    sq[r] = fma(v, v, sq[r]);                                                      \
+                }                                                                                  \
+                acc0 = f64x4{0.0, 0.0, 0.0, 0.0};                                                  \
+                acc1 = f64x4{0.0, 0.0, 0.0, 0.0};                                                  \
+                kg = 0;                                                                            \
+                tlen = __builtin_amdgcn_readfirstlane(mw[3 + (++t)] + 1);                          \
+            }                                                                                      \
         }
+        for (int g = 0; g < G; g += 2) {
+            MPO_EI_GROUP(b0)
+            if (g + 1 >= G) break;
+            MPO_EI_GROUP(b1)
+        }
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(b0[0]), "+v"(b0[1]), "+v"(b0[2]), "+v"(b0[3]), "+v"(b1[0]),
+                     "+v"(b1[1]), "+v"(b1[2]), "+v"(b1[3]));
+#undef MPO_EI_GROUP
         // f64 C/D map: col = lane & 15, row = (lane >> 4) + 4 r.  Sum the columns.
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                double v = sq[mt][r];
-                v += __shfl_xor(v, 1);
-                v += __shfl_xor(v, 2);
-                v += __shfl_xor(v, 4);
-                v += __shfl_xor(v, 8);
-                if ((lane & 15) == 0) red[wave * BM + mt * 16 + (lane >> 4) + 4 * r] = v;
-            }
+        for (int r = 0; r < 4; ++r) {
+            double v = sq[r];
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 4);
+            v += __shfl_xor(v, 8);
+            if ((lane & 15) == 0) red[wave * BM + (lane >> 4) + 4 * r] = v;
+        }
     }
     __syncthreads();
 
-    // ---- phase 3: posterior, acquisitions, block top-k (wave 0)
-    if (wave != 0) return;
-    const int row = lane;
-    const double q = row < BM ? (red[0 * BM + row] + red[1 * BM + row] + red[2 * BM + row] + red[3 * BM + row]) *
-                                    (a.amp * a.amp) : 0.0;
-    score_epilogue(a, row < BM, m0 + row, mu_n, q, blockIdx.x, lane);
+    // ---- phase 3: (mu_n, q) out (wave 0; the other waves go on to the next tile's
+    // phase 0 and meet wave 0 at its barrier, after which red may be rewritten)
+    if (tid < BM && m0 + tid < a.m) {
+        const double q = (red[0 * BM + tid] + red[1 * BM + tid] + red[2 * BM + tid] + red[3 * BM + tid]) *
+                         (a.amp * a.amp);
+        *reinterpret_cast<double2*>(a.mq + 2 * (m0 + tid)) = double2{mu_n, q};
+    }
+    }  // tile loop
+#undef MPO_LD4
+#undef MPO_LD
+#undef MPO_LOAD_TILE
 }
 
 // Merge per-block top-k lists.  grid = (G, 3): block g of acquisition y merges
@@ -576,73 +672,78 @@ inline int pad_dims(int d) {
 constexpr size_t kMaxLds = 160 * 1024;
 constexpr int kMergeGroups = 256;  // stage-1 top-k merge groups
 
-size_t score_lds_bytes(int bm, int dp, int np16) {
-    const int S = 4 * (64 / bm);
-    const int red = std::max(S * bm, 4 * bm);
-    return ((size_t)np16 * bm + (size_t)bm * dp + red) * sizeof(double);
+size_t score_lds_bytes(int dp, int np16) {
+    const int T = np16 / 16;
+    return ((size_t)np16 * kBM + (size_t)kBM * dp + 16 * kBM) * sizeof(double) + (size_t)4 * (T + 4) * sizeof(int32_t);
 }
 
-// Candidates per workgroup.  MPO_GP_BM (16/32/64) overrides the default for
-// experiments; the default prefers the variant that fits several workgroups per
-// CU (VALU Matern phase of one overlapping the MFMA phase of another).
-int choose_bm(int dp, int np16) {
-    const char* env = getenv("MPO_GP_BM");
-    const int forced = env ? atoi(env) : 0;
-    if ((forced == 16 || forced == 32 || forced == 64) && score_lds_bytes(forced, dp, np16) <= kMaxLds) return forced;
-    for (int bm : {16, 32, 64})
-        if (score_lds_bytes(bm, dp, np16) <= kMaxLds) return bm;
-    return -1;
-}
+bool score_fits(int dp, int np16) { return score_lds_bytes(dp, np16) <= kMaxLds; }
 
-template <int BM, int DP, int D, int OCC>
-hipError_t launch_score(const ScoreArgs& a, int nblocks, size_t lds, hipStream_t s) {
-    auto kern = gp_score_kernel<BM, DP, D, OCC>;
+// grid = the device's resident capacity for this variant (tiles are looped over)
+template <int DP, int D, int OCC>
+hipError_t launch_score(const ScoreArgs& a, int ntiles, size_t lds, hipStream_t s) {
+    auto kern = gp_score_kernel<DP, D, OCC>;
+    // The B ring's asm loads are invisible to the compiler: a spill of a ring
+    // register would store it before its load lands.  A variant whose register
+    // cap forces spills is refused instead of run.
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kern)) != hipSuccess || fa.localSizeBytes != 0)
+        return hipErrorInvalidDeviceFunction;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)lds);
-    hipLaunchKernelGGL(kern, dim3(nblocks), dim3(256), lds, s, a);
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), 256, lds);
+    int grid = std::max(1, std::min(ntiles, std::max(1, per_cu) * std::max(1, cus)));
+    const char* g = getenv("MPO_GP_GRID");   // experiments: "tiles" = one tile per workgroup
+    if (g && g[0] == 't') grid = ntiles;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, a);
     return hipGetLastError();
 }
 
-// occupancy hint for the 16-candidate variant (min waves per SIMD -> VGPR cap);
-// MPO_GP_OCC overrides for experiments
-inline int gp_occ16() {
-    const char* e = getenv("MPO_GP_OCC");
-    const int v = e ? atoi(e) : 6;
-    return (v == 1 || v == 5 || v == 6 || v == 8) ? v : 6;
+template <int DP, int D, int OCC>
+bool spill_free() {
+    static int ok = -1;
+    if (ok < 0) {
+        hipFuncAttributes fa;
+        ok = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(gp_score_kernel<DP, D, OCC>)) == hipSuccess &&
+             fa.localSizeBytes == 0;
+    }
+    return ok == 1;
 }
 
+// occupancy hint (min waves per SIMD -> VGPR cap): the highest spill-free one;
+// MPO_GP_OCC (2, 4, 5, 6) forces one for experiments
 template <int DP, int D>
-hipError_t launch_score_bm(int bm, const ScoreArgs& a, int nblocks, size_t lds, hipStream_t s) {
-    switch (bm) {
-        case 64: return launch_score<64, DP, D, 1>(a, nblocks, lds, s);
-        case 32: return launch_score<32, DP, D, 1>(a, nblocks, lds, s);
-        case 16:
-            switch (gp_occ16()) {
-                case 1: return launch_score<16, DP, D, 1>(a, nblocks, lds, s);
-                case 5: return launch_score<16, DP, D, 5>(a, nblocks, lds, s);
-                case 8: return launch_score<16, DP, D, 8>(a, nblocks, lds, s);
-                default: return launch_score<16, DP, D, 6>(a, nblocks, lds, s);
-            }
+hipError_t launch_score_occ(const ScoreArgs& a, int nblocks, size_t lds, hipStream_t s) {
+    const char* e = getenv("MPO_GP_OCC");
+    int occ = e ? atoi(e) : 0;
+    if (occ != 2 && occ != 4 && occ != 5 && occ != 6)
+        occ = spill_free<DP, D, 6>() ? 6 : spill_free<DP, D, 5>() ? 5 : spill_free<DP, D, 4>() ? 4 : 2;
+    switch (occ) {
+        case 6: return launch_score<DP, D, 6>(a, nblocks, lds, s);
+        case 5: return launch_score<DP, D, 5>(a, nblocks, lds, s);
+        case 4: return launch_score<DP, D, 4>(a, nblocks, lds, s);
+        default: return launch_score<DP, D, 2>(a, nblocks, lds, s);
     }
-    return hipErrorInvalidValue;
 }
 
 // (padded row width DP, distance dims D): d = 5 and d = 10 (the reference's mnist
 // space and the BASELINE config) get exact-width distance loops
-hipError_t launch_score_dp(int dp, int d, int bm, const ScoreArgs& a, int nblocks, size_t lds, hipStream_t s) {
+hipError_t launch_score_dp(int dp, int d, const ScoreArgs& a, int nblocks, size_t lds, hipStream_t s) {
     switch (dp) {
-        case 4: return launch_score_bm<4, 4>(bm, a, nblocks, lds, s);
-        case 8: return d == 5 ? launch_score_bm<8, 5>(bm, a, nblocks, lds, s)
-                              : launch_score_bm<8, 8>(bm, a, nblocks, lds, s);
-        case 12: return d == 10 ? launch_score_bm<12, 10>(bm, a, nblocks, lds, s)
-                                : launch_score_bm<12, 12>(bm, a, nblocks, lds, s);
-        case 16: return launch_score_bm<16, 16>(bm, a, nblocks, lds, s);
-        case 32: return launch_score_bm<32, 32>(bm, a, nblocks, lds, s);
+        case 4: return launch_score_occ<4, 4>(a, nblocks, lds, s);
+        case 8: return d == 5 ? launch_score_occ<8, 5>(a, nblocks, lds, s)
+                              : launch_score_occ<8, 8>(a, nblocks, lds, s);
+        case 12: return d == 10 ? launch_score_occ<12, 10>(a, nblocks, lds, s)
+                                : launch_score_occ<12, 12>(a, nblocks, lds, s);
+        case 16: return launch_score_occ<16, 16>(a, nblocks, lds, s);
+        case 32: return launch_score_occ<32, 32>(a, nblocks, lds, s);
     }
     return hipErrorInvalidValue;
 }
 
-constexpr int kWaveTile = 16;   // candidates per partial top-k list (the smallest block)
 
 int trsm_cols_per_block(int n) {
     size_t cb = 64;
@@ -814,6 +915,36 @@ __global__ __launch_bounds__(kGradThreads) void acq_grad_kernel(
     }
 }
 
+// Scoring workspace: per-wave partial top-k lists, the stage-1 merge lists, a
+// 3-entry tail (mpo_gp_ei_score's top-1) and the (mu_n, q) rows.
+struct ScoreWs {
+    long long* part_idx;
+    double* part_val;
+    long long* mid_idx;
+    double* mid_val;
+    long long* tail_idx;
+    double* tail_val;
+    double* mq;
+};
+
+inline int64_t score_nparts(int64_t m) { return (m + kFinishCands - 1) / kFinishCands; }
+
+inline ScoreWs carve_score_ws(void* ws, int64_t m, int k, size_t* used) {
+    const int64_t nparts = score_nparts(m);
+    const int kk = std::max(k, 1);
+    mpo::WsCarver c(ws);
+    ScoreWs w;
+    w.part_idx = c.take<long long>((size_t)nparts * 3 * kk);
+    w.part_val = c.take<double>((size_t)nparts * 3 * kk);
+    w.mid_idx = c.take<long long>((size_t)kMergeGroups * 3 * kk);
+    w.mid_val = c.take<double>((size_t)kMergeGroups * 3 * kk);
+    w.tail_idx = c.take<long long>(3 * kk);
+    w.tail_val = c.take<double>(3 * kk);
+    w.mq = c.take<double>((size_t)m * 2);
+    if (used) *used = c.used;
+    return w;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -854,15 +985,16 @@ size_t mpo_gp_prepare_ws_bytes(int n, int d) {
     const int dp = pad_dims(d);
     if (n <= 0 || dp < 0) return 0;
     const int np16 = (n + 15) / 16 * 16;
-    const int np32 = (n + 31) / 32 * 32;
+    const int xrows = np16 + 32;           // the scoring kernel reads one 16-row step past np16
     mpo::WsCarver c(nullptr);
-    c.take<double>((size_t)np32 * dp);     // xs (+ far-away padding rows)
+    c.take<double>((size_t)xrows * dp);    // xs (+ far-away padding rows)
     c.take<double>(dp);                    // ls_pad
     c.take<double>((size_t)n * n);         // L
     c.take<double>((size_t)n * n);         // W
-    c.take<double>(np32);                  // alpha (+ zero padding)
+    c.take<double>(xrows);                 // alpha (+ zero padding)
     c.take<double>(wfrag_elems(np16));     // wfrag
     c.take<int32_t>(4);                    // info
+    c.take<int32_t>(wmeta_elems(np16));    // wmeta
     return c.used + 256;
 }
 
@@ -877,22 +1009,23 @@ int mpo_gp_prepare(const double* X, const double* y_norm, int n, int d, const do
     MPO_CHECK_ARG(ws_bytes >= mpo_gp_prepare_ws_bytes(n, d), "mpo_gp_prepare: workspace too small (%zu < %zu)",
                   ws_bytes, mpo_gp_prepare_ws_bytes(n, d));
     const int np16 = (n + 15) / 16 * 16;
-    const int np32 = (n + 31) / 32 * 32;
-    if (choose_bm(dp, np16) < 0) { mpo::set_error("mpo_gp_prepare: n=%d exceeds the LDS-resident scoring limit", n); return MPO_ENOTSUP; }
+    const int xrows = np16 + 32;
+    if (!score_fits(dp, np16)) { mpo::set_error("mpo_gp_prepare: n=%d exceeds the LDS-resident scoring limit", n); return MPO_ENOTSUP; }
     hipStream_t s = static_cast<hipStream_t>(stream);
     mpo::WsCarver c(ws);
-    double* xs = c.take<double>((size_t)np32 * dp);
+    double* xs = c.take<double>((size_t)xrows * dp);
     double* ls_pad = c.take<double>(dp);
     double* L = c.take<double>((size_t)n * n);
     double* W = c.take<double>((size_t)n * n);
-    double* alpha = c.take<double>(np32);
+    double* alpha = c.take<double>(xrows);
     double* wfrag = c.take<double>(wfrag_elems(np16));
     int32_t* info = c.take<int32_t>(4);
+    int32_t* wmeta = c.take<int32_t>(wmeta_elems(np16));
 
-    hipLaunchKernelGGL(scale_rows_kernel, dim3((np32 * dp + 255) / 256), dim3(256), 0, s, X, n, np32, d, dp, ls, xs,
+    hipLaunchKernelGGL(scale_rows_kernel, dim3((xrows * dp + 255) / 256), dim3(256), 0, s, X, n, xrows, d, dp, ls, xs,
                        ls_pad);
     MPO_LAUNCH_CHECK();
-    hipLaunchKernelGGL(zero_kernel, dim3((np32 + 255) / 256), dim3(256), 0, s, alpha, np32);
+    hipLaunchKernelGGL(zero_kernel, dim3((xrows + 255) / 256), dim3(256), 0, s, alpha, xrows);
     MPO_LAUNCH_CHECK();
     hipLaunchKernelGGL(kernel_matrix_kernel, dim3((n + 63) / 64, n), dim3(64), 0, s, xs, n, dp, amp,
                        noise + kJitter, L, n);
@@ -910,7 +1043,13 @@ int mpo_gp_prepare(const double* X, const double* y_norm, int n, int d, const do
     rc = trsm_launch(L, n, n, alpha, 1, 1, 1, s);
     if (rc) return rc;
     const int T = np16 / 16;
-    hipLaunchKernelGGL(pack_wfrag_kernel, dim3((4 * T * 64 + 255) / 256, T), dim3(256), 0, s, W, n, n, T, wfrag);
+    const size_t nw = wfrag_elems(np16);
+    hipLaunchKernelGGL(zero_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, wfrag, (int)nw);
+    MPO_LAUNCH_CHECK();
+    hipLaunchKernelGGL(wave_plan_kernel, dim3(1), dim3(64), 0, s, T, wmeta);
+    MPO_LAUNCH_CHECK();
+    hipLaunchKernelGGL(pack_wfrag_kernel, dim3((4 * T * 64 + 255) / 256, T), dim3(256), 0, s, W, n, n, T, wmeta,
+                       wfrag);
     MPO_LAUNCH_CHECK();
 
     model->n = n;
@@ -927,29 +1066,23 @@ int mpo_gp_prepare(const double* X, const double* y_norm, int n, int d, const do
     model->L = L;
     model->W = W;
     model->info = info;
+    model->wmeta = wmeta;
     return MPO_OK;
     MPO_GUARD_END
 }
 
 size_t mpo_gp_score_ws_bytes(const MpoGpModel* model, int64_t m, int k) {
     if (!model || m <= 0 || k < 0 || k > MPO_TOPK_MAX) return 0;
-    if (choose_bm(model->dp, model->np16) < 0) return 0;
-    const int64_t nblocks = (m + kWaveTile - 1) / kWaveTile;   // partial lists per 16-candidate tile (upper bound)
-    const int kk = std::max(k, 1);
-    mpo::WsCarver c(nullptr);
-    c.take<long long>((size_t)nblocks * 3 * kk);
-    c.take<double>((size_t)nblocks * 3 * kk);
-    c.take<long long>((size_t)kMergeGroups * 3 * kk);
-    c.take<double>((size_t)kMergeGroups * 3 * kk);
-    c.take<long long>(3 * kk);
-    c.take<double>(3 * kk);
-    return c.used + 256;
+    if (!score_fits(model->dp, model->np16)) return 0;
+    size_t used = 0;
+    carve_score_ws(nullptr, m, k, &used);
+    return used + 256;
 }
 
 static int gp_score_impl(const MpoGpModel* model, const double* cand, int64_t m, double y_opt,
-                         double xi, double kappa, unsigned flags, int ei_positive, double* mu,
-                         double* sd, double* vals, int k, int64_t* topk_idx, double* topk_val,
-                         void* ws, size_t ws_bytes, hipStream_t s) {
+                  double xi, double kappa, unsigned flags, int ei_positive, double* mu,
+                  double* sd, double* vals, int k, int64_t* topk_idx, double* topk_val,
+                  void* ws, size_t ws_bytes, hipStream_t s) {
     MPO_CHECK_ARG(model && cand, "mpo_gp_acq_score: null model/candidates");
     MPO_CHECK_ARG(m > 0, "mpo_gp_acq_score: m must be > 0");
     MPO_CHECK_ARG((flags & ~7u) == 0 && flags != 0, "mpo_gp_acq_score: bad flags %u", flags);
@@ -957,17 +1090,16 @@ static int gp_score_impl(const MpoGpModel* model, const double* cand, int64_t m,
     MPO_CHECK_ARG(k == 0 || (topk_idx && topk_val), "mpo_gp_acq_score: topk outputs required for k>0");
     MPO_CHECK_ARG(k > 0 || mu || sd || vals, "mpo_gp_acq_score: nothing to compute");
     MPO_CHECK_ARG(ws && ws_bytes >= mpo_gp_score_ws_bytes(model, m, k), "mpo_gp_acq_score: workspace too small");
-    const int bm = choose_bm(model->dp, model->np16);
-    if (bm < 0) { mpo::set_error("mpo_gp_acq_score: model too large"); return MPO_ENOTSUP; }
-    const int64_t nblocks64 = (m + bm - 1) / bm;
-    MPO_CHECK_ARG(nblocks64 < (1LL << 31), "mpo_gp_acq_score: too many candidates");
-    const int nblocks = (int)nblocks64;
-    mpo::WsCarver c(ws);
-    const int kk = std::max(k, 1);
-    long long* part_idx = c.take<long long>((size_t)nblocks * 3 * kk);
-    double* part_val = c.take<double>((size_t)nblocks * 3 * kk);
-    long long* mid_idx = c.take<long long>((size_t)kMergeGroups * 3 * kk);
-    double* mid_val = c.take<double>((size_t)kMergeGroups * 3 * kk);
+    if (!score_fits(model->dp, model->np16)) { mpo::set_error("mpo_gp_acq_score: model too large"); return MPO_ENOTSUP; }
+    const int64_t ntiles64 = (m + kBM - 1) / kBM;
+    MPO_CHECK_ARG(ntiles64 < (1LL << 31), "mpo_gp_acq_score: too many candidates");
+    const int ntiles = (int)ntiles64;
+    const int nparts = (int)score_nparts(m);
+    const ScoreWs w = carve_score_ws(ws, m, k, nullptr);
+    long long* part_idx = w.part_idx;
+    double* part_val = w.part_val;
+    long long* mid_idx = w.mid_idx;
+    double* mid_val = w.mid_val;
 
     ScoreArgs a;
     a.n = model->n;
@@ -981,6 +1113,7 @@ static int gp_score_impl(const MpoGpModel* model, const double* cand, int64_t m,
     a.ls = model->ls;
     a.alpha = model->alpha;
     a.wfrag = model->wfrag;
+    a.wmeta = model->wmeta;
     a.cand = cand;
     a.m = m;
     a.y_opt = y_opt;
@@ -988,19 +1121,27 @@ static int gp_score_impl(const MpoGpModel* model, const double* cand, int64_t m,
     a.kappa = kappa;
     a.flags = flags;
     a.ei_positive = ei_positive;
+    {
+        const char* e = getenv("MPO_GP_DEBUG");
+        a.dbg = e ? atoi(e) : 0;
+    }
     a.mu = mu;
     a.sd = sd;
     a.vals = vals;
     a.k = k;
     a.part_idx = part_idx;
     a.part_val = part_val;
-    const size_t lds = score_lds_bytes(bm, model->dp, model->np16);
-    MPO_HIP(launch_score_dp(model->dp, model->d, bm, a, nblocks, lds, s));
+    a.mq = w.mq;
+    const size_t lds = score_lds_bytes(model->dp, model->np16);
+    MPO_HIP(launch_score_dp(model->dp, model->d, a, ntiles, lds, s));
+    hipLaunchKernelGGL(score_finish_kernel, dim3((unsigned)((m + kFinishThreads - 1) / kFinishThreads)),
+                       dim3(kFinishThreads), 0, s, a, w.mq);
+    MPO_LAUNCH_CHECK();
     if (k > 0) {
-        // stage 1: G groups of ~64 block-lists each; stage 2: one list
-        const int chunk = std::max(64, (nblocks + kMergeGroups - 1) / kMergeGroups);
-        const int G = (nblocks + chunk - 1) / chunk;
-        hipLaunchKernelGGL(topk_merge_kernel, dim3(G, 3), dim3(256), 0, s, part_idx, part_val, nblocks, chunk, k,
+        // stage 1: G groups of ~64 wave-lists each; stage 2: one list
+        const int chunk = std::max(64, (nparts + kMergeGroups - 1) / kMergeGroups);
+        const int G = (nparts + chunk - 1) / chunk;
+        hipLaunchKernelGGL(topk_merge_kernel, dim3(G, 3), dim3(256), 0, s, part_idx, part_val, nparts, chunk, k,
                            flags, mid_idx, mid_val, k, 0);
         MPO_LAUNCH_CHECK();
         hipLaunchKernelGGL(topk_merge_kernel, dim3(1, 3), dim3(256), 0, s, mid_idx, mid_val, G, G, k, flags,
@@ -1026,15 +1167,10 @@ int mpo_gp_ei_score(const MpoGpModel* model, const double* cand, int64_t m, doub
     MPO_CHECK_ARG(argmax, "mpo_gp_ei_score: null argmax");
     MPO_CHECK_ARG(ws_bytes >= mpo_gp_score_ws_bytes(model, m, 1), "mpo_gp_ei_score: workspace too small");
     // top-1 of -EI lands in the tail of the workspace the score call does not use
-    mpo::WsCarver c(ws);
-    if (choose_bm(model->dp, model->np16) < 0) { mpo::set_error("mpo_gp_ei_score: model too large"); return MPO_ENOTSUP; }
-    const int64_t nblocks = (m + kWaveTile - 1) / kWaveTile;   // the carve of mpo_gp_score_ws_bytes
-    c.take<long long>((size_t)nblocks * 3);
-    c.take<double>((size_t)nblocks * 3);
-    c.take<long long>((size_t)kMergeGroups * 3);
-    c.take<double>((size_t)kMergeGroups * 3);
-    long long* tidx = c.take<long long>(3);
-    double* tval = c.take<double>(3);
+    if (!score_fits(model->dp, model->np16)) { mpo::set_error("mpo_gp_ei_score: model too large"); return MPO_ENOTSUP; }
+    const ScoreWs w = carve_score_ws(ws, m, 1, nullptr);
+    long long* tidx = w.tail_idx;
+    double* tval = w.tail_val;
     hipStream_t s = static_cast<hipStream_t>(stream);
     int rc = gp_score_impl(model, cand, m, y_opt, xi, 1.96, MPO_ACQ_EI, 1, mu, sd, ei, 1,
                            reinterpret_cast<int64_t*>(tidx), tval, ws, ws_bytes, s);
