@@ -301,16 +301,17 @@ def bench_gp_fit(args, torch, dev, cpu):
         torch.cuda.synchronize(dev)
         sizes[n] = {"fits_per_s": 1.0 / dt, "ms_per_fit": dt * 1e3, "launches_per_fit": det["launches"],
                     "kernel_ms_per_launch": e0.elapsed_time(e1) / 10, "lml": det["lml"],
-                    "kernel": "lml_sweep_kernel" if n > 192 else "lml_grad_kernel (LDS Cholesky)"}
+                    "kernel": "split block sweep" if n > 48 else "lml_grad_kernel (LDS Cholesky)"}
     s200 = sizes[200]
     out = {"metric": "GP refits/sec (skopt LML L-BFGS-B, 3 starts, N=200 obs, D=10, fp64)",
            "value": s200["fits_per_s"], "unit": "fits/s", "ms_per_fit": s200["ms_per_fit"],
            "launches_per_fit": s200["launches_per_fit"], "lml": s200["lml"], "dtype": "f64",
            "by_n": {str(k): v for k, v in sizes.items()},
-           "kernel": {"name": "lml_grad_kernel", "ms_per_launch": s200["kernel_ms_per_launch"],
+           "kernel": {"name": "split block sweep (sw_pivot_kernel + sw_update_kernel per 32-wide block, "
+                              "sw_build/alpha/pairs/final)", "ms_per_launch": s200["kernel_ms_per_launch"],
                       "thetas_per_launch": 3,
-                      "note": "one 1024-thread workgroup per theta: latency-bound (factorisation recurrences), "
-                              "not a roofline kernel; n > 192 runs the block-sweep kernel"}}
+                      "note": "one LML evaluation of 3 thetas = 2 launches per 32-wide pivot block + 5; latency-"
+                              "bound (the sequential pivot sweeps), not a roofline kernel"}}
     if cpu:
         from oracle import gp_ei as O
 

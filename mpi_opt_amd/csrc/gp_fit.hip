@@ -830,6 +830,377 @@ __global__ __launch_bounds__(kFitThreads) void lml_sweep_kernel(LmlArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Split block sweep (n > kSplitMinN): the same sweep as lml_sweep_kernel, spread
+// over the device.  The single-workgroup kernel runs every rank-32 trailing update
+// on ONE CU (2.45 ms per launch at n = 500: the n^3 MFMA work of a theta on 4
+// SIMDs); here each sweep step is two launches --
+//   sw_pivot_kernel   (one workgroup per theta) old block column C -> global,
+//                     pivot block swept by wave 0 (log det, failure flag
+//                     accumulate in the workspace), G = C P^-1 -> global;
+//   sw_update_kernel  (many workgroups per theta, one 16x16 lower tile per wave
+//                     at a time) A_IJ -= G_I C_J^T outside block k, block
+//                     column k <- G, pivot block <- -P^-1
+// -- bracketed by sw_build_kernel (xs, K; many workgroups) and sw_finish_kernel
+// (alpha, the pair/gradient phase and the LML; one workgroup per theta).  Same
+// arithmetic in the same order as lml_sweep_kernel, so both give the same bits.
+constexpr int kSplitMinN = 48;    // past it the split beats both single-workgroup kernels (0.09 vs 0.20 ms at n = 64)
+constexpr int kUpdThreads = 256;
+constexpr int kUpdTilesPerWave = 4;
+
+// per-theta workspace (doubles): xs | alpha | A [np][np] | G [np][32] | C [np][32]
+// | P^-1 [32][32] | logdet, fail
+__host__ __device__ inline long long ss_ws_doubles(int n, int d) {
+    auto al = [](long long x) { return (x + 31) & ~31LL; };
+    const long long np = sw_np(n);
+    return al((long long)n * d) + al(np) + np * np + 2 * np * kSwNb + kSwNb * kSwNb + 32;
+}
+
+struct SsPtrs {
+    double *xs, *alpha, *A, *G, *C, *P, *acc;   // acc[0] = log det, acc[1] = failure column (as double)
+};
+
+__device__ __forceinline__ SsPtrs ss_ptrs(const LmlArgs& a, int b) {
+    auto al = [](long long x) { return (x + 31) & ~31LL; };
+    const long long np = sw_np(a.n);
+    SsPtrs p;
+    p.xs = a.ws + (long long)b * a.ws_stride;
+    p.alpha = p.xs + al((long long)a.n * a.d);
+    p.A = p.alpha + al(np);
+    p.G = p.A + np * np;
+    p.C = p.G + np * kSwNb;
+    p.P = p.C + np * kSwNb;
+    p.acc = p.P + kSwNb * kSwNb;
+    return p;
+}
+
+template <int DP>
+__device__ __forceinline__ void ss_theta(const LmlArgs& a, int b, double& amp, double& noise, double (&ls)[DP]) {
+    const double* th = a.theta + (long long)b * (a.d + 2);
+    amp = exp(th[0]);
+    noise = exp(th[a.d + 1]);
+#pragma unroll
+    for (int c = 0; c < DP; ++c) ls[c] = c < a.d ? exp(th[1 + c]) : 1.0;
+}
+
+// grid (1, B): xs = X / ls, the log det / failure accumulators
+template <int DP>
+__global__ __launch_bounds__(256) void sw_xs_kernel(LmlArgs a) {
+    const int b = blockIdx.y;
+    const SsPtrs p = ss_ptrs(a, b);
+    double amp, noise, ls[DP];
+    ss_theta<DP>(a, b, amp, noise, ls);
+    for (int e = threadIdx.x; e < a.n * a.d; e += blockDim.x) {
+        const int c = e % a.d;
+        double lc = 1.0;
+#pragma unroll
+        for (int q = 0; q < DP; ++q)
+            if (q == c) lc = ls[q];
+        p.xs[e] = a.X[e] / lc;
+    }
+    if (threadIdx.x == 0) { p.acc[0] = 0.0; p.acc[1] = 0.0; }
+}
+
+// grid (np/16, B): K rows [16 bx, 16 bx + 16) -- the lower triangle and the full
+// diagonal 16x16 tiles, identity on the padding (as lml_sweep_kernel phase 1)
+template <int DP>
+__global__ __launch_bounds__(256) void sw_build_kernel(LmlArgs a) {
+    const int b = blockIdx.y, n = a.n, d = a.d, np = (int)sw_np(n);
+    const SsPtrs p = ss_ptrs(a, b);
+    double amp, noise, ls[DP];
+    ss_theta<DP>(a, b, amp, noise, ls);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int i = 16 * blockIdx.x + wave; i < 16 * blockIdx.x + 16; i += 4) {
+        double xi[DP];
+#pragma unroll
+        for (int c = 0; c < DP; ++c) xi[c] = (c < d && i < n) ? p.xs[i * d + c] : 0.0;
+        const int jend = (i | 15) + 1;
+        for (int j = lane; j < jend && j < np; j += 64) {
+            double v;
+            if (i >= n || j >= n) {
+                v = i == j ? 1.0 : 0.0;
+            } else if (i == j) {
+                v = amp * 1.0 + noise + kFitJitter;
+            } else {
+                double r2 = 0.0;
+#pragma unroll
+                for (int c = 0; c < DP; ++c)
+                    if (c < d) {
+                        const double t = xi[c] - p.xs[j * d + c];
+                        r2 += t * t;
+                    }
+                const double k = sqrt(r2) * kSqrt5;
+                v = amp * ((1.0 + k + k * k / 3.0) * exp(-k));
+            }
+            p.A[(long long)i * np + j] = v;
+        }
+    }
+}
+
+// grid (1, B), kFitThreads: steps a-c of sweep step k (see lml_sweep_kernel)
+__global__ __launch_bounds__(kFitThreads) void sw_pivot_kernel(LmlArgs a, int k) {
+    const int b = blockIdx.y, np = (int)sw_np(a.n), ntile = np / 16, k0 = k * kSwNb;
+    const SsPtrs p = ss_ptrs(a, b);
+    __shared__ double Pb[kSwNb * kSwLd];   // pivot block rows of C
+    __shared__ double Pi[kSwNb * kSwLd];   // P^-1
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // the old block column C (row-major [np][32], global: the G phase and the
+    // update kernel read it from L2; np is up to 2048, past the LDS)
+    // rows i >= k0 read row segments A[i][k0 .. k0+32); rows i < k0 read the block's
+    // rows A[k0+c][0 .. k0) (the upper part of the column, stored transposed) --
+    // both walks coalesced
+#pragma unroll 4
+    for (int e = tid; e < (np - k0) * kSwNb; e += kFitThreads) {
+        const int i = k0 + (e >> 5), c = e & 31, j = k0 + c;
+        const double v = i >= j ? p.A[(long long)i * np + j] : p.A[(long long)j * np + i];
+        p.C[(long long)i * kSwNb + c] = v;
+        if ((i >> 5) == k) Pb[(i - k0) * kSwLd + c] = v;
+    }
+#pragma unroll 4
+    for (int e = tid; e < k0 * kSwNb; e += kFitThreads) {
+        const int c = e / k0, i = e - c * k0;
+        p.C[(long long)i * kSwNb + c] = p.A[(long long)(k0 + c) * np + i];
+    }
+    __threadfence_block();
+    __syncthreads();
+    if (wave == 0) {
+        const int l = lane & 31;
+        double r[kSwNb];
+#pragma unroll
+        for (int j = 0; j < kSwNb; ++j) r[j] = Pb[l * kSwLd + j];
+        double prod = 1.0;
+        int bad = 0;
+#pragma unroll
+        for (int c = 0; c < kSwNb; ++c) {
+            const double pv = readlane_f64(r[c], c);
+            if (!(pv > 0.0) || !isfinite(pv)) bad = bad ? bad : c + 1;
+            prod *= pv;
+            const double ip = 1.0 / pv;
+            const bool piv = l == c;
+            const double t = r[c] * ip;
+#pragma unroll
+            for (int j = 0; j < kSwNb; ++j) {
+                if (j == c) continue;
+                const double pj = readlane_f64(r[j], c);
+                r[j] = piv ? r[j] * ip : fma(-t, pj, r[j]);
+            }
+            r[c] = piv ? -ip : t;
+        }
+        if (lane < kSwNb) {
+#pragma unroll
+            for (int j = 0; j < kSwNb; ++j) {
+                Pi[l * kSwLd + j] = -r[j];
+                p.P[l * kSwNb + j] = -r[j];
+            }
+        }
+        if (lane == 0) {
+            p.acc[0] += log(prod);
+            if (bad && p.acc[1] == 0.0) p.acc[1] = (double)(k0 + bad);
+        }
+    }
+    __syncthreads();
+    for (int R = wave; R < ntile; R += kFitWaves) {
+        if ((R >> 1) == k) continue;
+        f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+        const double* ar = p.C + (long long)(16 * R + (lane & 15)) * kSwNb + (lane >> 4);
+        const int br = (lane >> 4) * kSwLd + (lane & 15);
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            const double av = ar[4 * ks];
+            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, Pi[br + 4 * ks * kSwLd], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, Pi[br + 4 * ks * kSwLd + 16], acc1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int rr = (lane >> 4) + 4 * q, c0 = lane & 15, c1 = 16 + c0;
+            p.G[((long long)R * 8 + (c0 >> 2)) * 64 + rr + 16 * (c0 & 3)] = acc0[q];
+            p.G[((long long)R * 8 + (c1 >> 2)) * 64 + rr + 16 * (c1 & 3)] = acc1[q];
+        }
+    }
+}
+
+// grid (nwg, B), kUpdThreads: step d of sweep step k over this workgroup's waves
+__global__ __launch_bounds__(kUpdThreads) void sw_update_kernel(LmlArgs a, int k) {
+    const int b = blockIdx.y, np = (int)sw_np(a.n), ntile = np / 16, k0 = k * kSwNb;
+    const SsPtrs p = ss_ptrs(a, b);
+    const int lane = threadIdx.x & 63;
+    const int gw = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kUpdThreads / 64) + (threadIdx.x >> 6)));
+    const int nw = gridDim.x * (kUpdThreads / 64);
+    const int nt_low = ntile * (ntile + 1) / 2;
+    for (int t = gw; t < nt_low; t += nw) {
+        int I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+        while (I * (I + 1) / 2 > t) --I;
+        while ((I + 1) * (I + 2) / 2 <= t) ++I;
+        const int J = t - I * (I + 1) / 2;
+        if ((I >> 1) == k || (J >> 1) == k) continue;
+        f64x4 acc;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = p.A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)];
+        const double* cb = p.C + (long long)(16 * J + (lane & 15)) * kSwNb + (lane >> 4);
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-p.G[((long long)I * 8 + ks) * 64 + lane], cb[4 * ks], acc, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) p.A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)] = acc[q];
+    }
+    for (long long e = (long long)blockIdx.x * kUpdThreads + threadIdx.x; e < (long long)np * kSwNb;
+         e += (long long)gridDim.x * kUpdThreads) {
+        const int i = (int)(e >> 5), c = (int)(e & 31), j = k0 + c;
+        if ((i >> 5) == k) {
+            p.A[(long long)i * np + j] = -p.P[(i - k0) * kSwNb + c];
+        } else {
+            const double gv = p.G[((long long)(i >> 4) * 8 + (c >> 2)) * 64 + (i & 15) + 16 * (c & 3)];
+            if (i > j) p.A[(long long)i * np + j] = gv;
+            else p.A[(long long)j * np + i] = gv;
+        }
+    }
+}
+
+// grid (np/16, B), 256 threads: alpha = K^-1 y for the 16 rows of row tile I;
+// wave w sums the column tiles J = w (mod 4), each tile read from the lower
+// storage (transposed above the diagonal); fixed-order reductions
+__global__ __launch_bounds__(256) void sw_alpha_kernel(LmlArgs a) {
+    __shared__ double part[4][16];
+    const int b = blockIdx.y, n = a.n, np = (int)sw_np(n), ntile = np / 16, I = blockIdx.x;
+    const SsPtrs p = ss_ptrs(a, b);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 15, cq = lane >> 4;
+    const int i = 16 * I + r;
+    double sacc = 0.0;
+    for (int J = wave; J < ntile; J += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = 16 * J + cq + 4 * u;
+            const double kij = j <= i ? -p.A[(long long)i * np + j] : -p.A[(long long)j * np + i];
+            sacc = fma(kij, j < n ? a.y[j] : 0.0, sacc);
+        }
+    }
+    sacc += __shfl_xor(sacc, 16);
+    sacc += __shfl_xor(sacc, 32);
+    if (cq == 0) part[wave][r] = sacc;
+    __syncthreads();
+    if (threadIdx.x < 16) {
+        const int ii = 16 * I + threadIdx.x;
+        const double v = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
+        p.alpha[ii] = ii < n ? v : 0.0;
+    }
+}
+
+// per-theta partial gradients of the pair kernel: [kPairGroups][DP + 2] after the
+// workspace's own end (mpo_gp_lml_ws_bytes adds them)
+constexpr int kPairGroups = 64;
+
+// grid (kPairGroups, B), 256 threads: pairs i >= j of rows i = gw (mod waves),
+// W_ij dK_ij/dtheta (as lml_sweep_kernel phase 4); one partial per workgroup
+template <int DP>
+__global__ __launch_bounds__(256) void sw_pairs_kernel(LmlArgs a, double* __restrict__ partials) {
+    __shared__ double red[4][DP + 2];
+    const int b = blockIdx.y, n = a.n, d = a.d, np = (int)sw_np(n);
+    const SsPtrs p = ss_ptrs(a, b);
+    double amp, noise, ls[DP];
+    ss_theta<DP>(a, b, amp, noise, ls);
+    (void)ls;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int gw = blockIdx.x * 4 + wave, nw = gridDim.x * 4;
+    double g[DP + 2];
+#pragma unroll
+    for (int c = 0; c < DP + 2; ++c) g[c] = 0.0;
+    if (p.acc[1] == 0.0) {
+        for (int i = gw; i < n; i += nw) {
+            const double ai = p.alpha[i];
+            double xi[DP];
+#pragma unroll
+            for (int c = 0; c < DP; ++c) xi[c] = c < d ? p.xs[i * d + c] : 0.0;
+            for (int j = lane; j <= i; j += 64) {
+                const double W = (ai * p.alpha[j] + p.A[(long long)i * np + j]) * (i == j ? 1.0 : 2.0);
+                const double* xj = p.xs + j * d;
+                double r2 = 0.0;
+#pragma unroll
+                for (int c = 0; c < DP; ++c)
+                    if (c < d) {
+                        const double t = xi[c] - xj[c];
+                        r2 += t * t;
+                    }
+                const double sq = sqrt(5.0 * r2);
+                const double e = exp(-sq);
+                const double Mij = i == j ? 1.0 : (1.0 + sq + sq * sq / 3.0) * e;
+                g[0] += W * (amp * Mij);
+                const double f = W * amp * (5.0 / 3.0) * (sq + 1.0) * e;
+#pragma unroll
+                for (int c = 0; c < DP; ++c)
+                    if (c < d) {
+                        const double t = xi[c] - xj[c];
+                        g[1 + c] += f * (t * t);
+                    }
+                if (i == j) g[DP + 1] += W * noise;
+            }
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < DP + 2; ++c) {
+        const double v = wave_sum_bcast(g[c]);
+        if (lane == 0) red[wave][c] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < DP + 2) {
+        const int c = threadIdx.x;
+        partials[((long long)b * gridDim.x + blockIdx.x) * (DP + 2) + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+    }
+}
+
+// grid (1, B), 64 threads: y.alpha, the LML, the gradient from the pair partials
+// (fixed order), or sklearn's LinAlgError branch (-inf, zeros)
+template <int DP>
+__global__ __launch_bounds__(64) void sw_final_kernel(LmlArgs a, const double* __restrict__ partials, int groups) {
+    const int b = blockIdx.y, n = a.n, d = a.d, lane = threadIdx.x;
+    const SsPtrs p = ss_ptrs(a, b);
+    double* out = a.grad + (long long)b * (d + 2);
+    if (p.acc[1] != 0.0) {
+        if (lane == 0) { a.lml[b] = -INFINITY; a.info[b] = (int)p.acc[1]; }
+        for (int c = lane; c < d + 2; c += 64) out[c] = 0.0;
+        return;
+    }
+    double ya = 0.0;
+    for (int i = lane; i < n; i += 64) ya = fma(a.y[i], p.alpha[i], ya);
+    ya = wave_sum_bcast(ya);
+    if (lane == 0) {
+        a.lml[b] = -0.5 * ya - 0.5 * p.acc[0] - 0.5 * n * kLog2Pi;
+        a.info[b] = 0;
+    }
+    if (lane < d + 2) {
+        const int src = lane == 0 ? 0 : (lane == d + 1 ? DP + 1 : lane);
+        double sum = 0.0;
+        for (int w = 0; w < groups; ++w) sum += partials[((long long)b * groups + w) * (DP + 2) + src];
+        out[lane] = 0.5 * sum;
+    }
+}
+
+template <int DP>
+int launch_split(const LmlArgs& a, int B, hipStream_t s) {
+    const int np = (int)sw_np(a.n), nbk = np / kSwNb, ntile = np / 16;
+    const int nt_low = ntile * (ntile + 1) / 2;
+    const int nwg = std::max(1, (nt_low + 4 * kUpdTilesPerWave - 1) / (4 * kUpdTilesPerWave));
+    hipLaunchKernelGGL(sw_xs_kernel<DP>, dim3(1, B), dim3(256), 0, s, a);
+    MPO_LAUNCH_CHECK();
+    hipLaunchKernelGGL(sw_build_kernel<DP>, dim3(ntile, B), dim3(256), 0, s, a);
+    MPO_LAUNCH_CHECK();
+    for (int k = 0; k < nbk; ++k) {
+        hipLaunchKernelGGL(sw_pivot_kernel, dim3(1, B), dim3(kFitThreads), 0, s, a, k);
+        MPO_LAUNCH_CHECK();
+        hipLaunchKernelGGL(sw_update_kernel, dim3(nwg, B), dim3(kUpdThreads), 0, s, a, k);
+        MPO_LAUNCH_CHECK();
+    }
+    double* partials = a.ws + (long long)B * a.ws_stride;   // [B][kPairGroups][DP + 2]
+    hipLaunchKernelGGL(sw_alpha_kernel, dim3(ntile, B), dim3(256), 0, s, a);
+    MPO_LAUNCH_CHECK();
+    hipLaunchKernelGGL(sw_pairs_kernel<DP>, dim3(kPairGroups, B), dim3(256), 0, s, a, partials);
+    MPO_LAUNCH_CHECK();
+    hipLaunchKernelGGL(sw_final_kernel<DP>, dim3(1, B), dim3(64), 0, s, a, partials, kPairGroups);
+    MPO_LAUNCH_CHECK();
+    return MPO_OK;
+}
+
 inline int fit_dp(int d) {
     if (d <= 4) return 4;
     if (d <= 8) return 8;
@@ -849,16 +1220,25 @@ int launch_sweep(const LmlArgs& a, int B, hipStream_t s) {
     return MPO_OK;
 }
 
-// which LML kernel: the LDS-packed Cholesky kernel for n <= kSwMinN (small,
-// latency-bound factors), the block sweep for kSwMinN < n <= kSwMaxN (0.44 vs
-// 0.68 ms per launch at n = 200, 0.60 at 256, 2.45 at 500: scripts/fit_probe.py),
-// the global-memory Cholesky past that.  MPO_FIT_KERNEL=sweep / panel force one.
+// which LML kernel: the LDS-packed Cholesky kernel for n <= kSplitMinN (small,
+// latency-bound factors), the split block sweep past it (0.30 / 0.35 / 0.87 ms
+// per launch at n = 200 / 256 / 500 against 0.44 / 0.60 / 2.45 for the
+// single-workgroup sweep and 0.68 for the LDS Cholesky at 200: scripts/fit_probe.py).
+// MPO_FIT_KERNEL = panel / sweep / split forces one.
 constexpr int kSwMinN = 192;
 inline bool use_sweep(int n) {
     const char* e = getenv("MPO_FIT_KERNEL");
     if (e && std::string(e) == "panel" && n <= kFitLdsMaxN) return false;
     if (e && std::string(e) == "sweep" && n <= kSwMaxN) return true;
-    return n > kSwMinN && n <= kSwMaxN;
+    if (e && std::string(e) == "split") return false;
+    return n > kSwMinN && n <= std::min(kSwMaxN, kSplitMinN);
+}
+// the split sweep: n > kSplitMinN (MPO_FIT_KERNEL=split forces it for n > 16)
+inline bool use_split(int n) {
+    const char* e = getenv("MPO_FIT_KERNEL");
+    if (e && std::string(e) == "split") return n > 16 && n <= kFitMaxN;
+    if (e && (std::string(e) == "sweep" || std::string(e) == "panel")) return false;
+    return n > kSplitMinN;
 }
 
 template <bool kLds, int DP>
@@ -877,8 +1257,9 @@ extern "C" {
 
 size_t mpo_gp_lml_ws_bytes(int n, int d, int batch) {
     if (n <= 0 || n > kFitMaxN || fit_dp(d) < 0 || batch <= 0) return 0;
-    const long long per = std::max(fit_ws_doubles(n, d, n <= kFitLdsMaxN), n <= kSwMaxN ? sw_ws_doubles(n, d) : 0LL);
-    return (size_t)per * sizeof(double) * batch + 256;
+    const long long per = std::max(std::max(fit_ws_doubles(n, d, n <= kFitLdsMaxN), n <= kSwMaxN ? sw_ws_doubles(n, d) : 0LL),
+                                   ss_ws_doubles(n, d));
+    return ((size_t)per * batch + (size_t)batch * kPairGroups * 34) * sizeof(double) + 256;   // + pair partials
 }
 
 int mpo_gp_lml_grad(const double* X, const double* y_norm, int n, int d, const double* theta, int batch,
@@ -894,12 +1275,23 @@ int mpo_gp_lml_grad(const double* X, const double* y_norm, int n, int d, const d
     MPO_CHECK_ARG(ws_bytes >= mpo_gp_lml_ws_bytes(n, d, batch), "mpo_gp_lml_grad: workspace too small (%zu < %zu)",
                   ws_bytes, mpo_gp_lml_ws_bytes(n, d, batch));
     const bool use_lds = n <= kFitLdsMaxN;
-    const bool sweep = use_sweep(n);
+    const bool split = use_split(n);
+    const bool sweep = !split && use_sweep(n);
     LmlArgs a{X, y_norm, n, d, theta, lml, grad, info,
               reinterpret_cast<double*>(mpo::align_up(reinterpret_cast<uintptr_t>(ws), 256)),
-              sweep ? sw_ws_doubles(n, d) : fit_ws_doubles(n, d, use_lds), 0};
+              split ? ss_ws_doubles(n, d) : sweep ? sw_ws_doubles(n, d) : fit_ws_doubles(n, d, use_lds), 0};
     if (const char* e = getenv("MPO_FIT_DEBUG")) a.stop = atoi(e);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    if (split) {
+        MPO_CHECK_ARG(batch <= 65535, "mpo_gp_lml_grad: batch %d too large", batch);
+        switch (dp) {
+            case 4: return launch_split<4>(a, batch, s);
+            case 8: return launch_split<8>(a, batch, s);
+            case 12: return launch_split<12>(a, batch, s);
+            case 16: return launch_split<16>(a, batch, s);
+            default: return launch_split<32>(a, batch, s);
+        }
+    }
     if (sweep) {
         switch (dp) {
             case 4: return launch_sweep<4>(a, batch, s);

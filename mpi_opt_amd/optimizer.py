@@ -249,7 +249,7 @@ class Optimizer:
             if self.model_queue_size is not None and len(self.models) > self.model_queue_size:
                 self.models.pop(0)
 
-        X = self.space.transform(self.space.rvs(n_samples=self.n_points, random_state=self.rng))
+        X = self.space.rvs_transformed(n_samples=self.n_points, random_state=self.rng)
         y_opt = float(np.min(self.yi))
         xi = self.acq_func_kwargs.get("xi", 0.01)
         kappa = self.acq_func_kwargs.get("kappa", 1.96)

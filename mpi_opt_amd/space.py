@@ -238,6 +238,18 @@ class Space:
         cols = [d.rvs(n_samples, rng) for d in self.dimensions]
         return [[_py(cols[j][i]) for j in range(len(cols))] for i in range(n_samples)]
 
+    def rvs_transformed(self, n_samples=1, random_state=None):
+        """``transform(rvs(n_samples, random_state))`` without the round trip through
+        Python lists: the same draws in the same order (skopt draws column by
+        column), each column transformed as a numpy array -- the same values.  The
+        acquisition candidates of every ask (n_points = 10000) come from here."""
+        rng = check_random_state(random_state)
+        cols = []
+        for d in self.dimensions:
+            t = np.asarray(d.transform(d.rvs(n_samples, rng)), dtype=float)
+            cols.append(t.reshape(n_samples, -1))
+        return np.hstack(cols) if cols else np.zeros((n_samples, 0))
+
     def transform(self, X):
         X = [list(x) for x in X]
         cols = []

@@ -47,3 +47,19 @@ def test_bad_dimensions():
         Real(1.0, 0.0)
     with pytest.raises(ValueError):
         check_dimension("nope")
+
+
+def test_rvs_transformed_is_transform_of_rvs():
+    """The candidate sampler draws exactly what transform(rvs()) would, in the same
+    random-stream order (the next draw after it agrees too)."""
+    from mpi_opt_amd.models import mnist_space
+    from mpi_opt_amd.space import Categorical, Integer, Real, Space
+
+    for dims in (mnist_space(), [Real(1e-5, 1e1, prior="log-uniform"), Integer(3, 9), Categorical(["a", "b", "c"]),
+                                 Real(-2.0, 3.0), Categorical([True, False])]):
+        sp = Space(dims)
+        r1, r2 = np.random.RandomState(7), np.random.RandomState(7)
+        a = sp.transform(sp.rvs(n_samples=500, random_state=r1))
+        b = sp.rvs_transformed(n_samples=500, random_state=r2)
+        assert a.shape == b.shape and np.array_equal(a, b)
+        assert r1.uniform() == r2.uniform()
