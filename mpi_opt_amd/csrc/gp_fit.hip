@@ -950,21 +950,40 @@ __global__ __launch_bounds__(kFitThreads) void sw_pivot_kernel(LmlArgs a, int k)
     // rows i >= k0 read row segments A[i][k0 .. k0+32); rows i < k0 read the block's
     // rows A[k0+c][0 .. k0) (the upper part of the column, stored transposed) --
     // both walks coalesced
-#pragma unroll 4
-    for (int e = tid; e < (np - k0) * kSwNb; e += kFitThreads) {
-        const int i = k0 + (e >> 5), c = e & 31, j = k0 + c;
-        const double v = i >= j ? p.A[(long long)i * np + j] : p.A[(long long)j * np + i];
-        p.C[(long long)i * kSwNb + c] = v;
-        if ((i >> 5) == k) Pb[(i - k0) * kSwLd + c] = v;
-    }
-#pragma unroll 4
-    for (int e = tid; e < k0 * kSwNb; e += kFitThreads) {
-        const int c = e / k0, i = e - c * k0;
-        p.C[(long long)i * kSwNb + c] = p.A[(long long)(k0 + c) * np + i];
+    // A was just written by the update kernel's workgroups on every XCD: each read
+    // is a trip past this XCD's L2, so all of a thread's reads are issued before
+    // any of its stores (one round trip instead of one per element)
+    constexpr int kCopyBatch = 16;   // np * 32 / 1024 <= 16 for np <= 512; larger np loops
+    for (int e0 = 0; e0 < np * kSwNb; e0 += kCopyBatch * kFitThreads) {
+        double v[kCopyBatch];
+        long long dst[kCopyBatch];
+#pragma unroll
+        for (int u = 0; u < kCopyBatch; ++u) {
+            const int e = e0 + u * kFitThreads + tid;
+            dst[u] = -1;
+            if (e < (np - k0) * kSwNb) {            // rows i >= k0: row segments
+                const int i = k0 + (e >> 5), c = e & 31, j = k0 + c;
+                v[u] = i >= j ? p.A[(long long)i * np + j] : p.A[(long long)j * np + i];
+                dst[u] = (long long)i * kSwNb + c;
+            } else if (e < np * kSwNb) {              // rows i < k0: the block's rows, transposed
+                const int f = e - (np - k0) * kSwNb;
+                const int c = f / k0, i = f - c * k0;
+                v[u] = p.A[(long long)(k0 + c) * np + i];
+                dst[u] = (long long)i * kSwNb + c;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kCopyBatch; ++u) {
+            if (dst[u] < 0) continue;
+            p.C[dst[u]] = v[u];
+            const int i = (int)(dst[u] >> 5);
+            if ((i >> 5) == k) Pb[(i - k0) * kSwLd + (int)(dst[u] & 31)] = v[u];
+        }
     }
     __threadfence_block();
     __syncthreads();
-    if (wave == 0) {
+    if (a.stop == 21) return;   // diagnostics only (MPO_FIT_DEBUG): column copy alone
+    if (wave == 0 && a.stop != 22) {
         const int l = lane & 31;
         double r[kSwNb];
 #pragma unroll
@@ -1000,6 +1019,7 @@ __global__ __launch_bounds__(kFitThreads) void sw_pivot_kernel(LmlArgs a, int k)
         }
     }
     __syncthreads();
+    if (a.stop == 23) return;   // diagnostics only: no G phase
     for (int R = wave; R < ntile; R += kFitWaves) {
         if ((R >> 1) == k) continue;
         f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};

@@ -63,6 +63,9 @@ for n in a.n:
             t0 = time.perf_counter()
             _, det = fit_lml(X, y, random_state=0, device="cuda:0", return_details=True)
             dt = time.perf_counter() - t0
+        if a.reps == 0:
+            print(f"n={n} d={a.d} kernel={kern}: {k_ms:.3f} ms per launch (3 thetas)", flush=True)
+            continue
         print(f"n={n} d={a.d} kernel={kern}: {k_ms:.3f} ms per launch (3 thetas); refit {dt * 1e3:.1f} ms, "
               f"{det['launches']} launches ({dt / det['launches'] * 1e3:.2f} ms/launch with host), "
               f"lml {det['lml']:.9f}", flush=True)
