@@ -848,16 +848,19 @@ constexpr int kSplitMinN = 48;    // past it the split beats both single-workgro
 constexpr int kUpdThreads = 256;
 constexpr int kUpdTilesPerWave = 4;
 
-// per-theta workspace (doubles): xs | alpha | A [np][np] | G [np][32] | C [np][32]
-// | P^-1 [32][32] | logdet, fail
+// per-theta workspace (doubles): xs | alpha | A [np][np] | G [np][32] | C0, C1 [np][32]
+// | P^-1 [32][32] | logdet, fail.  C_k (block column k before sweep k, row-major
+// [np][32]) lives in C[k & 1]: the update kernel of step k writes C_{k+1} as it
+// produces those entries, so the pivot kernel never re-reads a block column of A.
 __host__ __device__ inline long long ss_ws_doubles(int n, int d) {
     auto al = [](long long x) { return (x + 31) & ~31LL; };
     const long long np = sw_np(n);
-    return al((long long)n * d) + al(np) + np * np + 2 * np * kSwNb + kSwNb * kSwNb + 32;
+    return al((long long)n * d) + al(np) + np * np + 3 * np * kSwNb + kSwNb * kSwNb + 32;
 }
 
 struct SsPtrs {
-    double *xs, *alpha, *A, *G, *C, *P, *acc;   // acc[0] = log det, acc[1] = failure column (as double)
+    double *xs, *alpha, *A, *G, *C0, *C1, *P, *acc;   // acc[0] = log det, acc[1] = failure column (as double)
+    __device__ double* C(int k) const { return (k & 1) ? C1 : C0; }
 };
 
 __device__ __forceinline__ SsPtrs ss_ptrs(const LmlArgs& a, int b) {
@@ -868,8 +871,9 @@ __device__ __forceinline__ SsPtrs ss_ptrs(const LmlArgs& a, int b) {
     p.alpha = p.xs + al((long long)a.n * a.d);
     p.A = p.alpha + al(np);
     p.G = p.A + np * np;
-    p.C = p.G + np * kSwNb;
-    p.P = p.C + np * kSwNb;
+    p.C0 = p.G + np * kSwNb;
+    p.C1 = p.C0 + np * kSwNb;
+    p.P = p.C1 + np * kSwNb;
     p.acc = p.P + kSwNb * kSwNb;
     return p;
 }
@@ -945,42 +949,33 @@ __global__ __launch_bounds__(kFitThreads) void sw_pivot_kernel(LmlArgs a, int k)
     __shared__ double Pi[kSwNb * kSwLd];   // P^-1
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // the old block column C (row-major [np][32], global: the G phase and the
-    // update kernel read it from L2; np is up to 2048, past the LDS)
-    // rows i >= k0 read row segments A[i][k0 .. k0+32); rows i < k0 read the block's
-    // rows A[k0+c][0 .. k0) (the upper part of the column, stored transposed) --
-    // both walks coalesced
-    // A was just written by the update kernel's workgroups on every XCD: each read
-    // is a trip past this XCD's L2, so all of a thread's reads are issued before
-    // any of its stores (one round trip instead of one per element)
-    constexpr int kCopyBatch = 16;   // np * 32 / 1024 <= 16 for np <= 512; larger np loops
-    for (int e0 = 0; e0 < np * kSwNb; e0 += kCopyBatch * kFitThreads) {
-        double v[kCopyBatch];
-        long long dst[kCopyBatch];
+    // C_k: at k = 0 copied from A (row segments for rows >= k0, the block's rows
+    // transposed for rows < k0; all of a thread's reads before its stores); for
+    // k > 0 the previous update kernel wrote it.  The pivot rows go to the LDS.
+    double* C = p.C(k);
+    if (k == 0) {
+        constexpr int kCopyBatch = 16;
+        for (int e0 = 0; e0 < np * kSwNb; e0 += kCopyBatch * kFitThreads) {
+            double v[kCopyBatch];
+            int dst[kCopyBatch];
 #pragma unroll
-        for (int u = 0; u < kCopyBatch; ++u) {
-            const int e = e0 + u * kFitThreads + tid;
-            dst[u] = -1;
-            if (e < (np - k0) * kSwNb) {            // rows i >= k0: row segments
-                const int i = k0 + (e >> 5), c = e & 31, j = k0 + c;
-                v[u] = i >= j ? p.A[(long long)i * np + j] : p.A[(long long)j * np + i];
-                dst[u] = (long long)i * kSwNb + c;
-            } else if (e < np * kSwNb) {              // rows i < k0: the block's rows, transposed
-                const int f = e - (np - k0) * kSwNb;
-                const int c = f / k0, i = f - c * k0;
-                v[u] = p.A[(long long)(k0 + c) * np + i];
-                dst[u] = (long long)i * kSwNb + c;
+            for (int u = 0; u < kCopyBatch; ++u) {
+                const int e = e0 + u * kFitThreads + tid;
+                dst[u] = -1;
+                if (e < np * kSwNb) {
+                    const int i = e >> 5, c = e & 31;
+                    v[u] = i >= c ? p.A[(long long)i * np + c] : p.A[(long long)c * np + i];
+                    dst[u] = e;
+                }
             }
-        }
 #pragma unroll
-        for (int u = 0; u < kCopyBatch; ++u) {
-            if (dst[u] < 0) continue;
-            p.C[dst[u]] = v[u];
-            const int i = (int)(dst[u] >> 5);
-            if ((i >> 5) == k) Pb[(i - k0) * kSwLd + (int)(dst[u] & 31)] = v[u];
+            for (int u = 0; u < kCopyBatch; ++u)
+                if (dst[u] >= 0) C[dst[u]] = v[u];
         }
+        __threadfence_block();
+        __syncthreads();
     }
-    __threadfence_block();
+    for (int e = tid; e < kSwNb * kSwNb; e += kFitThreads) Pb[(e >> 5) * kSwLd + (e & 31)] = C[(long long)k0 * kSwNb + e];
     __syncthreads();
     if (a.stop == 21) return;   // diagnostics only (MPO_FIT_DEBUG): column copy alone
     if (wave == 0 && a.stop != 22) {
@@ -1023,7 +1018,7 @@ __global__ __launch_bounds__(kFitThreads) void sw_pivot_kernel(LmlArgs a, int k)
     for (int R = wave; R < ntile; R += kFitWaves) {
         if ((R >> 1) == k) continue;
         f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-        const double* ar = p.C + (long long)(16 * R + (lane & 15)) * kSwNb + (lane >> 4);
+        const double* ar = C + (long long)(16 * R + (lane & 15)) * kSwNb + (lane >> 4);
         const int br = (lane >> 4) * kSwLd + (lane & 15);
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks) {
@@ -1044,6 +1039,12 @@ __global__ __launch_bounds__(kFitThreads) void sw_pivot_kernel(LmlArgs a, int k)
 __global__ __launch_bounds__(kUpdThreads) void sw_update_kernel(LmlArgs a, int k) {
     const int b = blockIdx.y, np = (int)sw_np(a.n), ntile = np / 16, k0 = k * kSwNb;
     const SsPtrs p = ss_ptrs(a, b);
+    const double* Cc = p.C(k);
+    // C_{k+1} (next block column, rows i, columns k1 .. k1+32) as its entries are
+    // produced: from the lower entries only (the pivot kernel's copy reads lower
+    // storage for both halves of a diagonal tile), so the bits match that copy
+    const int k1 = k0 + kSwNb;
+    double* Cn = k1 < np ? p.C(k + 1) : nullptr;
     const int lane = threadIdx.x & 63;
     const int gw = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kUpdThreads / 64) + (threadIdx.x >> 6)));
     const int nw = gridDim.x * (kUpdThreads / 64);
@@ -1057,12 +1058,21 @@ __global__ __launch_bounds__(kUpdThreads) void sw_update_kernel(LmlArgs a, int k
         f64x4 acc;
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc[q] = p.A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)];
-        const double* cb = p.C + (long long)(16 * J + (lane & 15)) * kSwNb + (lane >> 4);
+        const double* cb = Cc + (long long)(16 * J + (lane & 15)) * kSwNb + (lane >> 4);
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks)
             acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-p.G[((long long)I * 8 + ks) * 64 + lane], cb[4 * ks], acc, 0, 0, 0);
 #pragma unroll
         for (int q = 0; q < 4; ++q) p.A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)] = acc[q];
+        if (Cn && ((J >> 1) == k + 1 || (I >> 1) == k + 1)) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int i = 16 * I + (lane >> 4) + 4 * q, j = 16 * J + (lane & 15);
+                if (i < j) continue;                                    // upper half of a diagonal tile
+                if ((j >> 5) == k + 1) Cn[(long long)i * kSwNb + (j - k1)] = acc[q];
+                if ((i >> 5) == k + 1) Cn[(long long)j * kSwNb + (i - k1)] = acc[q];
+            }
+        }
     }
     for (long long e = (long long)blockIdx.x * kUpdThreads + threadIdx.x; e < (long long)np * kSwNb;
          e += (long long)gridDim.x * kUpdThreads) {
@@ -1073,6 +1083,7 @@ __global__ __launch_bounds__(kUpdThreads) void sw_update_kernel(LmlArgs a, int k
             const double gv = p.G[((long long)(i >> 4) * 8 + (c >> 2)) * 64 + (i & 15) + 16 * (c & 3)];
             if (i > j) p.A[(long long)i * np + j] = gv;
             else p.A[(long long)j * np + i] = gv;
+            if (Cn && (i >> 5) == k + 1) Cn[(long long)j * kSwNb + (i - k1)] = gv;   // row j < k1 of C_{k+1}
         }
     }
 }
