@@ -66,6 +66,8 @@ __host__ __device__ constexpr inline int wg_ns(int nt) { return nt * 16 + ((nt &
 // ---- argument blocks ----------------------------------------------------------
 struct ConvArgs {
     const float* in; long long in_ms; int in_ps;          // input (+ channel offset), member / pixel strides
+    const float* bnc; long long bnc_ms;                   // BN site coef [4][H] (scale, shift at 2H, 3H): the
+                                                          // input is cat and the conv sees ELU(x scale + shift)
     const int* order; long long ord_ms; long long row0;   // sample gather (initial conv only)
     long long img_floats;
     const float* w; long long w_ms;                       // padded weights [K16 + slack][N16]
@@ -75,6 +77,7 @@ struct ConvArgs {
 
 struct WgArgs {
     const float* in; long long in_ms; int in_ps;
+    const float* bnc; long long bnc_ms;                   // as ConvArgs::bnc
     const int* order; long long ord_ms; long long row0;
     long long img_floats;
     const float* dout; long long dout_ms; int dout_ps;
@@ -85,7 +88,7 @@ struct WgArgs {
 struct BnArgs {
     const float* x; long long x_ms; int x_ps;             // cat (channels [0, Cin))
     float* z; long long z_ms;                             // [B][H][W][Cin]
-    float* coef; long long coef_ms;                       // [4][H]: mean, inv, scale, shift
+    float* coef; long long coef_ms;                       // [4][H]: mean, inv, scale = gamma inv, shift = beta - mean scale
     const float* params; long long p_ms; long long g_off, b_off;
     float* state; long long s_ms; long long mm_off, mv_off;
     float* grads;                                         // member stride p_ms
@@ -133,6 +136,16 @@ struct Walk3 {
         if (x >= W) { x -= W; ++r; }
     }
 };
+
+// z = ELU(BN(x)) of one element of image row h: the BN sites' conv / wgrad inputs
+// and their backward's ELU' are formed from cat on the fly, so z is never stored
+// (dn_bn_coef_kernel writes scale / shift).  ELU as TensorFlow's Elu kernel forms
+// it, exp(y) - 1 (not expm1), on the hardware exp: every consumer re-forms z, so
+// it must be cheap (expm1f here cost the conv and wgrad staging 10-35%).
+__device__ __forceinline__ float bn_elu(float x, float s, float t) {
+    const float y = x * s + t;
+    return y > 0.f ? y : __expf(y) - 1.f;
+}
 
 __device__ __forceinline__ double block_sum(double v, double* red) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
@@ -223,12 +236,16 @@ __global__ __launch_bounds__(256) void dn_conv_kernel(ConvArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int krow = lane >> 4, kcol = lane & 15;
 
+    const float* bnc = a.bnc ? a.bnc + m * a.bnc_ms : nullptr;
     Walk3 wk(tid, Wp, Cp, 256);
     for (int e = tid; e < img_elems; e += 256, wk.next()) {
         const int r = wk.r, col = wk.x, c = wk.c;
         const int gy = y0 + r - P, gx = col - P;
         float v = 0.f;
-        if (gy >= 0 && gy < H && gx >= 0 && gx < W && c < Cin) v = src[((long long)gy * W + gx) * a.in_ps + c];
+        if (gy >= 0 && gy < H && gx >= 0 && gx < W && c < Cin) {
+            v = src[((long long)gy * W + gx) * a.in_ps + c];
+            if (bnc) v = bn_elu(v, bnc[2 * H + gy], bnc[3 * H + gy]);   // zero padding stays zero
+        }
         img[e] = v;
     }
     // tap offsets, each 16-k group stored as [krow][u] so a lane reads its four
@@ -385,6 +402,7 @@ __global__ __launch_bounds__(kWgWaves * 64) void dn_wgrad3_kernel(WgArgs a) {
     const int b0 = grp * a.spg, b1 = min(a.B, b0 + a.spg);
     const float* inm = a.in + m * a.in_ms;
     const float* dom = a.dout + m * a.dout_ms;
+    const float* bnc = a.bnc ? a.bnc + m * a.bnc_ms : nullptr;
     for (int b = b0; b < b1; ++b) {
         const float* src = a.order ? a.in + (long long)a.order[m * a.ord_ms + a.row0 + b] * a.img_floats
                                    : inm + (long long)b * H * W * a.in_ps;
@@ -398,8 +416,14 @@ __global__ __launch_bounds__(kWgWaves * 64) void dn_wgrad3_kernel(WgArgs a) {
                     const int r = wk.r, x = wk.x, c4 = wk.c;
                     const int gy = y0 + r - P;
                     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (gy >= 0 && gy < H)
+                    if (gy >= 0 && gy < H) {
                         v = *reinterpret_cast<const float4*>(src + ((long long)gy * W + x) * a.in_ps + 4 * c4);
+                        if (bnc) {
+                            const float sc = bnc[2 * H + gy], sh = bnc[3 * H + gy];
+                            v = make_float4(bn_elu(v.x, sc, sh), bn_elu(v.y, sc, sh), bn_elu(v.z, sc, sh),
+                                            bn_elu(v.w, sc, sh));
+                        }
+                    }
                     *reinterpret_cast<float4*>(img + (r * Wp + x + P) * Cp + 4 * c4) = v;
                 }
             } else {
@@ -409,7 +433,10 @@ __global__ __launch_bounds__(kWgWaves * 64) void dn_wgrad3_kernel(WgArgs a) {
                     const int r = wk.r, x = wk.x, c = wk.c;
                     const int gy = y0 + r - P;
                     float v = 0.f;
-                    if (gy >= 0 && gy < H) v = src[((long long)gy * W + x) * a.in_ps + c];
+                    if (gy >= 0 && gy < H) {
+                        v = src[((long long)gy * W + x) * a.in_ps + c];
+                        if (bnc) v = bn_elu(v, bnc[2 * H + gy], bnc[3 * H + gy]);
+                    }
                     img[(r * Wp + x + P) * Cp + c] = v;
                 }
             }
@@ -492,13 +519,23 @@ __global__ __launch_bounds__(kWgWaves * 64) void dn_wgrad1_kernel(WgArgs a) {
     // k-step s covers pixels [p0 + 4s, p0 + 4s + 4); wave w takes s = w, w + 8, ...
     const long long nsteps = (p1 - p0 + 3) >> 2;
     float av[2][MT], bv[2][NT];
+    const float* bnc = a.bnc ? a.bnc + m * a.bnc_ms : nullptr;
     auto ld = [&](long long s, float (&A)[MT], float (&Bv)[NT]) {
         const long long p = p0 + 4 * s + krow;
         const bool ok = p < p1;
         const float* zp = z + p * a.in_ps + kcol;
         const float* dp = d + p * a.dout_ps + kcol;
+        float sc = 1.f, sh = 0.f;
+        if (bnc && ok) {
+            const int h = (int)(((unsigned)p / (unsigned)a.W) % (unsigned)a.H);   // p < 2^31
+            sc = bnc[2 * a.H + h];
+            sh = bnc[3 * a.H + h];
+        }
 #pragma unroll
-        for (int i = 0; i < MT; ++i) A[i] = (ok && am[i]) ? zp[i * 16] : 0.f;
+        for (int i = 0; i < MT; ++i) {
+            const float v = (ok && am[i]) ? zp[i * 16] : 0.f;
+            A[i] = (bnc && ok && am[i]) ? bn_elu(v, sc, sh) : v;
+        }
 #pragma unroll
         for (int j = 0; j < NT; ++j) Bv[j] = (ok && bm[j]) ? dp[j * 16] : 0.f;
     };
@@ -644,13 +681,15 @@ __global__ __launch_bounds__(256) void dn_bn_apply_kernel(BnArgs a, const double
         const float inv = (float)(1.0 / sqrt((double)var + (double)kBnEps));
         const float* pm = a.params + m * a.p_ms;
         const float gam = pm[a.g_off + h], bet = pm[a.b_off + h];
+        sc[0] = gam * inv;
+        sc[1] = bet - mean * gam * inv;
         if (b == 0) {
             float* coef = a.coef + m * a.coef_ms;
             coef[h] = mean;
             coef[H + h] = inv;
+            coef[2 * H + h] = sc[0];
+            coef[3 * H + h] = sc[1];
         }
-        sc[0] = gam * inv;
-        sc[1] = bet - mean * gam * inv;
     }
     __syncthreads();
     const float s = sc[0], t = sc[1];
@@ -659,8 +698,45 @@ __global__ __launch_bounds__(256) void dn_bn_apply_kernel(BnArgs a, const double
     Walk2 wk(tid, Cin, 256);
     for (int e = tid; e < rowe; e += 256, wk.next()) {
         const int w = wk.q, c = wk.c;
-        const float y = xr[(long long)w * a.x_ps + c] * s + t;
-        zr[e] = y > 0.f ? y : expm1f(y);
+        zr[e] = bn_elu(xr[(long long)w * a.x_ps + c], s, t);
+    }
+}
+
+// The coefficients alone (the sites whose consumers form z themselves): grid
+// (member), one thread per image row h -- the fold, moving averages and
+// (mean, inv, scale, shift) exactly as dn_bn_apply's block (b = 0) computes them.
+__global__ __launch_bounds__(64) void dn_bn_coef_kernel(BnArgs a, const double* __restrict__ part, int S) {
+    const int m = blockIdx.x;
+    const int H = a.H, rowe = a.W * a.Cin;
+    for (int h = threadIdx.x; h < H; h += 64) {
+        float mean, var;
+        if (a.train) {
+            double s = 0.0, q = 0.0;
+            for (int sl = 0; sl < S; ++sl) {
+                const double* o = part + (((long long)m * S + sl) * H + h) * 2;
+                s += o[0];
+                q += o[1];
+            }
+            const double n = (double)a.B * rowe;
+            const double mu = s / n;
+            mean = (float)mu;
+            var = (float)fmax(q / n - mu * mu, 0.0);
+            float* st = a.state + m * a.s_ms;
+            st[a.mm_off + h] = kBnMomentum * st[a.mm_off + h] + (1.f - kBnMomentum) * mean;
+            st[a.mv_off + h] = kBnMomentum * st[a.mv_off + h] + (1.f - kBnMomentum) * var;
+        } else {
+            const float* st = a.state + m * a.s_ms;
+            mean = st[a.mm_off + h];
+            var = st[a.mv_off + h];
+        }
+        const float inv = (float)(1.0 / sqrt((double)var + (double)kBnEps));
+        const float* pm = a.params + m * a.p_ms;
+        const float gam = pm[a.g_off + h], bet = pm[a.b_off + h];
+        float* coef = a.coef + m * a.coef_ms;
+        coef[h] = mean;
+        coef[H + h] = inv;
+        coef[2 * H + h] = gam * inv;
+        coef[3 * H + h] = bet - mean * gam * inv;
     }
 }
 
@@ -668,11 +744,13 @@ __global__ __launch_bounds__(256) void dn_bn_apply_kernel(BnArgs a, const double
 // dbeta[h] = sum dy, dgamma[h] = sum dy xhat (dn_bn_bwd_reduce, slice partials);
 // dx = gamma inv / n (n dy - dbeta - xhat dgamma) stored or added into dcat
 // (dn_bn_bwd_apply, one block per (b, h) row).
-__device__ __forceinline__ float bn_dy(const BnArgs& a, const float* zr, const float* dzr, const float* dgr, int e,
-                                       int c) {
-    const float zz = zr[e];
+// ELU'(y) from cat (z is never stored): 1 for y > 0, else e^y (= z + 1; the
+// hardware exp is enough for a derivative factor and far cheaper than expm1f)
+__device__ __forceinline__ float bn_dy(const BnArgs& a, float x, float s, float t, const float* dzr, const float* dgr,
+                                       int e, int c) {
+    const float y = x * s + t;
     const float d = a.bcast ? dgr[c] * a.inv_hw : dzr[e];
-    return d * (zz > 0.f ? 1.f : zz + 1.f);
+    return d * (y > 0.f ? 1.f : __expf(y));
 }
 
 __global__ __launch_bounds__(256) void dn_bn_bwd_reduce_kernel(BnArgs a, double* __restrict__ part, int S, int bs) {
@@ -681,20 +759,20 @@ __global__ __launch_bounds__(256) void dn_bn_bwd_reduce_kernel(BnArgs a, double*
     const int H = a.H, W = a.W, Cin = a.Cin;
     const int rowe = W * Cin;
     const float* coef = a.coef + m * a.coef_ms;
-    const float mean = coef[h], inv = coef[H + h];
+    const float mean = coef[h], inv = coef[H + h], bs_ = coef[2 * H + h], bt_ = coef[3 * H + h];
     const int b0 = sl * bs, b1 = min(a.B, b0 + bs);
     double sdy = 0.0, sdyx = 0.0;
     for (int b = b0; b < b1; ++b) {
         const float* xr = a.x + m * a.x_ms + ((long long)b * H + h) * W * a.x_ps;
         const long long zo = ((long long)b * H + h) * rowe;
-        const float* zr = a.z + m * a.z_ms + zo;
         const float* dzr = a.bcast ? nullptr : a.dz + m * a.dz_ms + zo;
         const float* dgr = a.bcast ? a.dg + m * a.dg_ms + (long long)b * Cin : nullptr;
         Walk2 wk(tid, Cin, 256);
         for (int e = tid; e < rowe; e += 256, wk.next()) {
             const int w = wk.q, c = wk.c;
-            const float dy = bn_dy(a, zr, dzr, dgr, e, c);
-            const float xh = (xr[(long long)w * a.x_ps + c] - mean) * inv;
+            const float xv = xr[(long long)w * a.x_ps + c];
+            const float dy = bn_dy(a, xv, bs_, bt_, dzr, dgr, e, c);
+            const float xh = (xv - mean) * inv;
             sdy += dy;
             sdyx += (double)dy * xh;
         }
@@ -715,7 +793,7 @@ __global__ __launch_bounds__(256) void dn_bn_bwd_apply_kernel(BnArgs a, const do
     const int b = row / H, h = row - b * H;
     const int rowe = W * Cin;
     const float* coef = a.coef + m * a.coef_ms;
-    const float mean = coef[h], inv = coef[H + h];
+    const float mean = coef[h], inv = coef[H + h], bs_ = coef[2 * H + h], bt_ = coef[3 * H + h];
     if (tid == 0) {
         double sdy = 0.0, sdyx = 0.0;
         for (int sl = 0; sl < S; ++sl) {
@@ -738,15 +816,15 @@ __global__ __launch_bounds__(256) void dn_bn_bwd_apply_kernel(BnArgs a, const do
     const float n = (float)a.B * rowe;
     const float* xr = a.x + m * a.x_ms + ((long long)b * H + h) * W * a.x_ps;
     const long long zo = ((long long)b * H + h) * rowe;
-    const float* zr = a.z + m * a.z_ms + zo;
     const float* dzr = a.bcast ? nullptr : a.dz + m * a.dz_ms + zo;
     const float* dgr = a.bcast ? a.dg + m * a.dg_ms + (long long)b * Cin : nullptr;
     float* dxr = a.dx + m * a.dx_ms + ((long long)b * H + h) * W * a.dx_ps;
     Walk2 wk(tid, Cin, 256);
     for (int e = tid; e < rowe; e += 256, wk.next()) {
         const int w = wk.q, c = wk.c;
-        const float dy = bn_dy(a, zr, dzr, dgr, e, c);
-        const float xh = (xr[(long long)w * a.x_ps + c] - mean) * inv;
+        const float xv = xr[(long long)w * a.x_ps + c];
+        const float dy = bn_dy(a, xv, bs_, bt_, dzr, dgr, e, c);
+        const float xh = (xv - mean) * inv;
         const float v = ca * (n * dy - fb - xh * fg);
         float* q = dxr + (long long)w * a.dx_ps + c;
         if (a.accumulate) *q += v; else *q = v;
@@ -1055,7 +1133,9 @@ int build_plan(DnPlan& p) {
     for (auto& ly : ls) {
         long long ms;
         if (ly.kind != K_CONV0) {
-            ly.z_off = ar.take((long long)B * ly.H * ly.W * ly.cin, &ms);
+            // z = ELU(BN(cat)) is stored for the head's GAP only; the other sites'
+            // convs, weight gradients and BN backward form it from cat on the fly
+            if (ly.kind == K_HEAD) ly.z_off = ar.take((long long)B * ly.H * ly.W * ly.cin, &ms);
             ly.coef_off = ar.take(4LL * ly.H, &ms);
             dz_max = std::max(dz_max, (long long)B * ly.H * ly.W * ly.cin);
         }
@@ -1218,7 +1298,8 @@ BnArgs bn_args(DnPlan& p, const Layer& ly, bool train) {
     BnArgs a{};
     const int s = ly.stage;
     a.x = p.act + p.cat_off[s]; a.x_ms = p.cat_ms[s]; a.x_ps = p.sC[s];
-    a.z = p.act + ly.z_off; a.z_ms = ((long long)p.B * ly.H * ly.W * ly.cin + 63) & ~63LL;
+    a.z = ly.z_off >= 0 ? p.act + ly.z_off : nullptr;
+    a.z_ms = ((long long)p.B * ly.H * ly.W * ly.cin + 63) & ~63LL;
     a.coef = p.act + ly.coef_off; a.coef_ms = (4LL * ly.H + 63) & ~63LL;
     a.params = p.params; a.p_ms = p.n_params; a.g_off = ly.g_off; a.b_off = ly.b_off;
     a.state = p.state; a.s_ms = p.n_state; a.mm_off = ly.mm_off; a.mv_off = ly.mv_off;
@@ -1262,8 +1343,11 @@ int enqueue_forward(DnPlan& p, const float* x, const int* labels, const int* ord
         if (train)
             hipLaunchKernelGGL(dn_bn_stats_kernel, dim3(ly.H, p.bn_S[li], n), dim3(256), 0, s, bn, bnp, p.bn_S[li],
                                p.bn_bs[li]);
-        hipLaunchKernelGGL(dn_bn_apply_kernel, dim3(B * ly.H, n), dim3(256), 0, s, bn, (const double*)bnp,
-                           p.bn_S[li]);
+        if (ly.kind == K_HEAD)   // the head's GAP reads z: the only site that stores it
+            hipLaunchKernelGGL(dn_bn_apply_kernel, dim3(B * ly.H, n), dim3(256), 0, s, bn, (const double*)bnp,
+                               p.bn_S[li]);
+        else
+            hipLaunchKernelGGL(dn_bn_coef_kernel, dim3(n), dim3(64), 0, s, bn, (const double*)bnp, p.bn_S[li]);
         if (ly.kind == K_HEAD) {
             HeadArgs h = head_args(p, labels, order, ord_ms, row0, train);
             h.loss_out = loss_out; h.loss_sum = loss_sum; h.correct = correct;
@@ -1273,7 +1357,8 @@ int enqueue_forward(DnPlan& p, const float* x, const int* labels, const int* ord
             continue;
         }
         ConvArgs c{};
-        c.in = bn.z; c.in_ms = bn.z_ms; c.in_ps = ly.cin;
+        c.in = bn.x; c.in_ms = bn.x_ms; c.in_ps = bn.x_ps;   // cat: the conv stages ELU(BN(x))
+        c.bnc = bn.coef; c.bnc_ms = bn.coef_ms;
         c.w = p.act + ly.wf_off; c.w_ms = ((long long)ly.wf_rows * ly.wf_n16 + 63) & ~63LL;
         c.H = ly.H; c.W = ly.W; c.Cin = ly.cin; c.N = ly.cout; c.R = ly.R;
         if (ly.kind == K_DENSE) {
@@ -1332,7 +1417,9 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
             w.in = x; w.in_ps = ly.cin; w.order = order; w.ord_ms = ord_ms; w.row0 = row0;
             w.img_floats = (long long)ly.H * ly.W * ly.cin;
         } else {
-            w.in = p.act + ly.z_off; w.in_ms = ((long long)B * ly.H * ly.W * ly.cin + 63) & ~63LL; w.in_ps = ly.cin;
+            const BnArgs bx = bn_args(p, ly, true);
+            w.in = bx.x; w.in_ms = bx.x_ms; w.in_ps = bx.x_ps;   // cat: the staging forms ELU(BN(x))
+            w.bnc = bx.coef; w.bnc_ms = bx.coef_ms;
         }
         DN_TRY(launch_wgrad(w, ly.ks, n, ly.G, s));
         const long long cnt = (long long)ly.ks * ly.ks * ly.cin * ly.cout;
