@@ -511,8 +511,8 @@ __global__ __launch_bounds__(256, OCC) void gp_score_kernel(ScoreArgs a) {
     __syncthreads();  // red is reused for the q partials below
 
     // ---- phase 2: V = K* L^-T on f64 MFMA, lower-triangular k-steps only.  The
-    // wave walks its B-fragment stream (wave_plan_kernel) two 4-k-step groups ahead;
-    // the refills past the stream's end fetch the next candidate tile's first groups.
+    // wave walks its B-fragment stream (wave_plan_kernel) two 4-k-step groups ahead
+    // (loading the ring's first groups before the mu barriers instead measured the same).
     {
         double b0[4], b1[4];
         MPO_LD4(b0, bs);
