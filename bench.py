@@ -185,7 +185,7 @@ def bench_ei(args, torch, dist, ws, rank, dev):
     y_opt = float(np.min(y))
     torch.cuda.synchronize(dev)
 
-    gathered = torch.empty(ws, 2, dtype=torch.float64, device=dev) if ws > 1 else None
+    gathered = torch.empty(ws * 2, dtype=torch.float64, device=dev) if ws > 1 else None   # [rank][value, index]
 
     def step():
         out = g.score(cand, y_opt, acqs=("EI",), k=k, want_mu_sd=True, want_values=True)
@@ -202,9 +202,16 @@ def bench_ei(args, torch, dist, ws, rank, dev):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    while time.perf_counter() - tw < 0.3:
+    while True:
         step()
         torch.cuda.synchronize(dev)
+        # every rank must run the same number of steps (each holds an all-gather):
+        # the ranks agree on whether any of them still needs warmup
+        more = torch.tensor([1.0 if time.perf_counter() - tw < 0.3 else 0.0], dtype=torch.float64, device=dev)
+        if ws > 1:
+            dist.all_reduce(more, op=dist.ReduceOp.MAX)
+        if float(more.item()) == 0.0:
+            break
     if ws > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -644,8 +651,12 @@ def main():
     if ws > 1:
         import torch.distributed as dist
 
+        # one rank per GPU over RCCL ("nccl").  MPO_BENCH_BACKEND=gloo with more ranks
+        # than GPUs is a rehearsal of the N > 1 path on a one-GPU box only.
+        backend = os.environ.get("MPO_BENCH_BACKEND", "nccl")
+        local = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
     dev = torch.device("cuda", local if ws > 1 else 0)
     if ws == 1 and args.gpus != 1:
         print(f"warning: --gpus {args.gpus} without torch.distributed.run; running 1 GPU", file=sys.stderr)

@@ -98,6 +98,8 @@ def run_search(args, x=None, y=None, log=print):
         if not dist.is_initialized():
             torch.cuda.set_device(local)
             dist.init_process_group("nccl")
+        # a caller that set up the group (bench.py) also chose this rank's device
+        local = torch.cuda.current_device()
     dev = torch.device("cuda", local)
     provider = BuilderFromFunction(model_fn=test_mnist, parameters=mnist_space())
     holdout = None
