@@ -96,6 +96,9 @@ struct BnArgs {
     const float* dg; long long dg_ms; float inv_hw;       // [B][Cin] / (H W)  (bcast == 1)
     float* dx; long long dx_ms; int dx_ps;
     int B, H, W, Cin, train, bcast, accumulate;
+    int c0;        // dn_bn_stats reads channels [c0, Cin) (the growth slices new since the previous site)
+    int prev;      // dn_bn_coef adds the previous site's totals (tot) to the slice partials
+    double* tot;   // folded (sum, sum of squares) per (member, h): [n][H][2]
 };
 
 // ---- shared reductions -----------------------------------------------------------
@@ -621,23 +624,47 @@ __global__ void dn_prep_kernel(const float* __restrict__ params, long long p_ms,
 //                Training: block (b = 0) stores mean / inv and updates the moving
 //                averages; evaluation: the moving averages.
 // ============================================================================
+// V = 4: rows walked as float4 (Cin, the pixel strides and every base 16-B
+// aligned -- bn_vec4 on the host); V = 1 otherwise.
+template <int V>
+__device__ __forceinline__ void ldv(const float* p, float (&v)[V]) {
+    if constexpr (V == 4) {
+        const float4 t = *reinterpret_cast<const float4*>(p);
+        v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    } else {
+        v[0] = *p;
+    }
+}
+
+template <int V>
+__device__ __forceinline__ void stv(float* p, const float (&v)[V]) {
+    if constexpr (V == 4) *reinterpret_cast<float4*>(p) = float4{v[0], v[1], v[2], v[3]};
+    else *p = v[0];
+}
+
+template <int V>
 __global__ __launch_bounds__(256) void dn_bn_stats_kernel(BnArgs a, double* __restrict__ part, int S, int bs) {
     __shared__ double red[4];
     const int h = blockIdx.x, sl = blockIdx.y, m = blockIdx.z, tid = threadIdx.x;
-    const int H = a.H, W = a.W, Cin = a.Cin;
-    const int rowe = W * Cin;
+    const int H = a.H, W = a.W, Cv = (a.Cin - a.c0) / V;
+    const int rowv = W * Cv;
     const long long bstride = (long long)H * W * a.x_ps;
-    const float* xm = a.x + m * a.x_ms + (long long)h * W * a.x_ps;
+    const float* xm = a.x + m * a.x_ms + (long long)h * W * a.x_ps + a.c0;
     const int b0 = sl * bs, b1 = min(a.B, b0 + bs);
     double s = 0.0, q = 0.0;
-    Walk2 wk(tid, Cin, 256);
-    for (int e = tid; e < rowe; e += 256, wk.next()) {
-        const int w = wk.q, c = wk.c;
-        const float* p = xm + (long long)w * a.x_ps + c;
-        for (int b = b0; b < b1; ++b) {
-            const double v = p[b * bstride];
-            s += v;
-            q += v * v;
+    // (sample, pixel, channel group) flattened: every thread busy even for a
+    // 12-channel slice, loads of several samples in flight per thread
+    const float* xb = xm + b0 * bstride;
+    const int tot = (b1 - b0) * rowv;
+    Walk3 wk(tid, W, Cv, 256);
+#pragma unroll 4
+    for (int e = tid; e < tot; e += 256, wk.next()) {
+        float v[V];
+        ldv<V>(xb + wk.r * bstride + (long long)wk.x * a.x_ps + wk.c * V, v);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            s += (double)v[j];
+            q += (double)v[j] * v[j];
         }
     }
     s = block_sum(s, red);
@@ -649,50 +676,14 @@ __global__ __launch_bounds__(256) void dn_bn_stats_kernel(BnArgs a, double* __re
     }
 }
 
-__global__ __launch_bounds__(256) void dn_bn_apply_kernel(BnArgs a, const double* __restrict__ part, int S) {
-    __shared__ float sc[2];
+// The head site: z = ELU(x scale + shift) stored for the GAP (dn_bn_coef ran first)
+__global__ __launch_bounds__(256) void dn_bn_apply_kernel(BnArgs a) {
     const int row = blockIdx.x, m = blockIdx.y, tid = threadIdx.x;
     const int H = a.H, W = a.W, Cin = a.Cin;
     const int b = row / H, h = row - b * H;
     const int rowe = W * Cin;
-    if (tid == 0) {
-        float mean, var;
-        if (a.train) {
-            double s = 0.0, q = 0.0;
-            for (int sl = 0; sl < S; ++sl) {
-                const double* o = part + (((long long)m * S + sl) * H + h) * 2;
-                s += o[0];
-                q += o[1];
-            }
-            const double n = (double)a.B * rowe;
-            const double mu = s / n;
-            mean = (float)mu;
-            var = (float)fmax(q / n - mu * mu, 0.0);
-            if (b == 0) {
-                float* st = a.state + m * a.s_ms;
-                st[a.mm_off + h] = kBnMomentum * st[a.mm_off + h] + (1.f - kBnMomentum) * mean;
-                st[a.mv_off + h] = kBnMomentum * st[a.mv_off + h] + (1.f - kBnMomentum) * var;
-            }
-        } else {
-            const float* st = a.state + m * a.s_ms;
-            mean = st[a.mm_off + h];
-            var = st[a.mv_off + h];
-        }
-        const float inv = (float)(1.0 / sqrt((double)var + (double)kBnEps));
-        const float* pm = a.params + m * a.p_ms;
-        const float gam = pm[a.g_off + h], bet = pm[a.b_off + h];
-        sc[0] = gam * inv;
-        sc[1] = bet - mean * gam * inv;
-        if (b == 0) {
-            float* coef = a.coef + m * a.coef_ms;
-            coef[h] = mean;
-            coef[H + h] = inv;
-            coef[2 * H + h] = sc[0];
-            coef[3 * H + h] = sc[1];
-        }
-    }
-    __syncthreads();
-    const float s = sc[0], t = sc[1];
+    const float* coef = a.coef + m * a.coef_ms;
+    const float s = coef[2 * H + h], t = coef[3 * H + h];
     const float* xr = a.x + m * a.x_ms + ((long long)b * H + h) * W * a.x_ps;
     float* zr = a.z + m * a.z_ms + ((long long)b * H + h) * rowe;
     Walk2 wk(tid, Cin, 256);
@@ -702,21 +693,26 @@ __global__ __launch_bounds__(256) void dn_bn_apply_kernel(BnArgs a, const double
     }
 }
 
-// The coefficients alone (the sites whose consumers form z themselves): grid
-// (member), one thread per image row h -- the fold, moving averages and
-// (mean, inv, scale, shift) exactly as dn_bn_apply's block (b = 0) computes them.
+// The coefficients of a site: grid (member), one thread per image row h.  Training:
+// the S slice partials folded in fixed order (plus, for an incremental site, the
+// previous site's totals -- its statistics cover the channels before c0), stored
+// as this site's totals, then the moving averages; evaluation: the moving
+// averages.  Writes (mean, inv, scale = gamma inv, shift = beta - mean scale).
 __global__ __launch_bounds__(64) void dn_bn_coef_kernel(BnArgs a, const double* __restrict__ part, int S) {
     const int m = blockIdx.x;
     const int H = a.H, rowe = a.W * a.Cin;
     for (int h = threadIdx.x; h < H; h += 64) {
         float mean, var;
         if (a.train) {
-            double s = 0.0, q = 0.0;
+            double* tt = a.tot + ((long long)m * H + h) * 2;
+            double s = a.prev ? tt[0] : 0.0, q = a.prev ? tt[1] : 0.0;
             for (int sl = 0; sl < S; ++sl) {
                 const double* o = part + (((long long)m * S + sl) * H + h) * 2;
                 s += o[0];
                 q += o[1];
             }
+            tt[0] = s;
+            tt[1] = q;
             const double n = (double)a.B * rowe;
             const double mu = s / n;
             mean = (float)mu;
@@ -741,40 +737,57 @@ __global__ __launch_bounds__(64) void dn_bn_coef_kernel(BnArgs a, const double* 
 }
 
 // BN + ELU backward.  dy = dz * ELU'(z) (ELU' = 1 for z > 0, else z + 1);
-// dbeta[h] = sum dy, dgamma[h] = sum dy xhat (dn_bn_bwd_reduce, slice partials);
-// dx = gamma inv / n (n dy - dbeta - xhat dgamma) stored or added into dcat
-// (dn_bn_bwd_apply, one block per (b, h) row).
+// dbeta[h] = sum dy, dgamma[h] = sum dy xhat (dn_bn_bwd_reduce: slice partials,
+// folded in fixed order by dn_bn_bwd_fold into slot 0, which also stores the
+// gradients); dx = gamma inv / n (n dy - dbeta - xhat dgamma) stored or added
+// into dcat (dn_bn_bwd_apply: two (b, h) rows per 256-thread block, no barrier).
 // ELU'(y) from cat (z is never stored): 1 for y > 0, else e^y (= z + 1; the
 // hardware exp is enough for a derivative factor and far cheaper than expm1f)
-__device__ __forceinline__ float bn_dy(const BnArgs& a, float x, float s, float t, const float* dzr, const float* dgr,
-                                       int e, int c) {
-    const float y = x * s + t;
-    const float d = a.bcast ? dgr[c] * a.inv_hw : dzr[e];
-    return d * (y > 0.f ? 1.f : __expf(y));
+template <int V>
+__device__ __forceinline__ void bn_dy(const BnArgs& a, const float (&x)[V], float s, float t, const float* dzr,
+                                      const float* dgr, int e, int c, float (&dy)[V]) {
+    float d[V];
+    if (a.bcast) {
+        ldv<V>(dgr + c * V, d);
+#pragma unroll
+        for (int j = 0; j < V; ++j) d[j] *= a.inv_hw;
+    } else {
+        ldv<V>(dzr + e * V, d);
+    }
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+        const float y = x[j] * s + t;
+        dy[j] = d[j] * (y > 0.f ? 1.f : __expf(y));
+    }
 }
 
+template <int V>
 __global__ __launch_bounds__(256) void dn_bn_bwd_reduce_kernel(BnArgs a, double* __restrict__ part, int S, int bs) {
     __shared__ double red[4];
     const int h = blockIdx.x, sl = blockIdx.y, m = blockIdx.z, tid = threadIdx.x;
-    const int H = a.H, W = a.W, Cin = a.Cin;
-    const int rowe = W * Cin;
+    const int H = a.H, W = a.W, Cin = a.Cin, Cv = Cin / V;
+    const int rowe = W * Cin, rowv = W * Cv;
     const float* coef = a.coef + m * a.coef_ms;
     const float mean = coef[h], inv = coef[H + h], bs_ = coef[2 * H + h], bt_ = coef[3 * H + h];
     const int b0 = sl * bs, b1 = min(a.B, b0 + bs);
     double sdy = 0.0, sdyx = 0.0;
-    for (int b = b0; b < b1; ++b) {
-        const float* xr = a.x + m * a.x_ms + ((long long)b * H + h) * W * a.x_ps;
-        const long long zo = ((long long)b * H + h) * rowe;
-        const float* dzr = a.bcast ? nullptr : a.dz + m * a.dz_ms + zo;
-        const float* dgr = a.bcast ? a.dg + m * a.dg_ms + (long long)b * Cin : nullptr;
-        Walk2 wk(tid, Cin, 256);
-        for (int e = tid; e < rowe; e += 256, wk.next()) {
-            const int w = wk.q, c = wk.c;
-            const float xv = xr[(long long)w * a.x_ps + c];
-            const float dy = bn_dy(a, xv, bs_, bt_, dzr, dgr, e, c);
-            const float xh = (xv - mean) * inv;
-            sdy += dy;
-            sdyx += (double)dy * xh;
+    const long long xbs = (long long)H * W * a.x_ps, zbs = (long long)H * rowe;
+    const float* xb = a.x + m * a.x_ms + ((long long)b0 * H + h) * W * a.x_ps;
+    const float* dzb = a.bcast ? nullptr : a.dz + m * a.dz_ms + ((long long)b0 * H + h) * rowe;
+    const float* dgb = a.bcast ? a.dg + m * a.dg_ms + (long long)b0 * Cin : nullptr;
+    const int tot = (b1 - b0) * rowv;
+    Walk3 wk(tid, W, Cv, 256);   // (sample, pixel, channel group) flattened, as dn_bn_stats
+#pragma unroll 2
+    for (int e = tid; e < tot; e += 256, wk.next()) {
+        float xv[V], dy[V];
+        ldv<V>(xb + wk.r * xbs + (long long)wk.x * a.x_ps + wk.c * V, xv);
+        bn_dy<V>(a, xv, bs_, bt_, a.bcast ? nullptr : dzb + wk.r * zbs, a.bcast ? dgb + wk.r * Cin : nullptr,
+                 wk.x * Cv + wk.c, wk.c, dy);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const float xh = (xv[j] - mean) * inv;
+            sdy += dy[j];
+            sdyx += (double)dy[j] * xh;
         }
     }
     sdy = block_sum(sdy, red);
@@ -786,48 +799,63 @@ __global__ __launch_bounds__(256) void dn_bn_bwd_reduce_kernel(BnArgs a, double*
     }
 }
 
-__global__ __launch_bounds__(256) void dn_bn_bwd_apply_kernel(BnArgs a, const double* __restrict__ part, int S) {
-    __shared__ float sc[3];
-    const int row = blockIdx.x, m = blockIdx.y, tid = threadIdx.x;
-    const int H = a.H, W = a.W, Cin = a.Cin;
-    const int b = row / H, h = row - b * H;
-    const int rowe = W * Cin;
-    const float* coef = a.coef + m * a.coef_ms;
-    const float mean = coef[h], inv = coef[H + h], bs_ = coef[2 * H + h], bt_ = coef[3 * H + h];
-    if (tid == 0) {
+// grid (member), one thread per image row h: the S slice partials summed in fixed
+// order into slot 0 (each thread reads and writes only its own h), dgamma / dbeta
+__global__ __launch_bounds__(64) void dn_bn_bwd_fold_kernel(BnArgs a, double* __restrict__ part, int S) {
+    const int m = blockIdx.x, H = a.H;
+    for (int h = threadIdx.x; h < H; h += 64) {
         double sdy = 0.0, sdyx = 0.0;
         for (int sl = 0; sl < S; ++sl) {
             const double* o = part + (((long long)m * S + sl) * H + h) * 2;
             sdy += o[0];
             sdyx += o[1];
         }
-        if (b == 0) {
-            float* gm = a.grads + m * a.p_ms;
-            gm[a.g_off + h] = (float)sdyx;
-            gm[a.b_off + h] = (float)sdy;
-        }
-        const float gam = a.params[m * a.p_ms + a.g_off + h];
-        sc[0] = gam * inv / ((float)a.B * rowe);
-        sc[1] = (float)sdy;
-        sc[2] = (float)sdyx;
+        double* o = part + ((long long)m * S * H + h) * 2;
+        o[0] = sdy;
+        o[1] = sdyx;
+        float* gm = a.grads + m * a.p_ms;
+        gm[a.g_off + h] = (float)sdyx;
+        gm[a.b_off + h] = (float)sdy;
     }
-    __syncthreads();
-    const float ca = sc[0], fb = sc[1], fg = sc[2];
+}
+
+template <int V>
+__global__ __launch_bounds__(256) void dn_bn_bwd_apply_kernel(BnArgs a, const double* __restrict__ part, int S) {
+    const int tid = threadIdx.x & 127, m = blockIdx.y;
+    const int row = blockIdx.x * 2 + (threadIdx.x >> 7);
+    const int H = a.H, W = a.W, Cin = a.Cin, Cv = Cin / V;
+    if (row >= a.B * H) return;
+    const int b = row / H, h = row - b * H;
+    const int rowe = W * Cin, rowv = W * Cv;
+    const float* coef = a.coef + m * a.coef_ms;
+    const float mean = coef[h], inv = coef[H + h], bs_ = coef[2 * H + h], bt_ = coef[3 * H + h];
+    const double* o = part + ((long long)m * S * H + h) * 2;   // folded: slot 0
+    const float fb = (float)o[0], fg = (float)o[1];
     const float n = (float)a.B * rowe;
+    const float ca = a.params[m * a.p_ms + a.g_off + h] * inv / n;
     const float* xr = a.x + m * a.x_ms + ((long long)b * H + h) * W * a.x_ps;
     const long long zo = ((long long)b * H + h) * rowe;
     const float* dzr = a.bcast ? nullptr : a.dz + m * a.dz_ms + zo;
     const float* dgr = a.bcast ? a.dg + m * a.dg_ms + (long long)b * Cin : nullptr;
     float* dxr = a.dx + m * a.dx_ms + ((long long)b * H + h) * W * a.dx_ps;
-    Walk2 wk(tid, Cin, 256);
-    for (int e = tid; e < rowe; e += 256, wk.next()) {
-        const int w = wk.q, c = wk.c;
-        const float xv = xr[(long long)w * a.x_ps + c];
-        const float dy = bn_dy(a, xv, bs_, bt_, dzr, dgr, e, c);
-        const float xh = (xv - mean) * inv;
-        const float v = ca * (n * dy - fb - xh * fg);
-        float* q = dxr + (long long)w * a.dx_ps + c;
-        if (a.accumulate) *q += v; else *q = v;
+    Walk2 wk(tid, Cv, 128);
+    for (int e = tid; e < rowv; e += 128, wk.next()) {
+        float xv[V], dy[V], v[V];
+        ldv<V>(xr + (long long)wk.q * a.x_ps + wk.c * V, xv);
+        bn_dy<V>(a, xv, bs_, bt_, dzr, dgr, e, wk.c, dy);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const float xh = (xv[j] - mean) * inv;
+            v[j] = ca * (n * dy[j] - fb - xh * fg);
+        }
+        float* q = dxr + (long long)wk.q * a.dx_ps + wk.c * V;
+        if (a.accumulate) {
+            float d[V];
+            ldv<V>(q, d);
+#pragma unroll
+            for (int j = 0; j < V; ++j) v[j] += d[j];
+        }
+        stv<V>(q, v);
     }
 }
 
@@ -1032,7 +1060,8 @@ struct DnPlan {
     long long z_ms_max = 0;
     long long dz_off = 0, dz_ms = 0, dt_off = 0, dt_ms = 0, part_off = 0, part_ms = 0;
     long long head_off = 0, head_ms = 0, lr_off = 0;
-    long long bnp_off = 0;      // fp64 BN slice partials [n][S][H][2] (shared by all sites)
+    long long bnp_off = 0;
+    long long bnt_off = 0;      // fp64 BN totals of the latest site [n][H][2]      // fp64 BN slice partials [n][S][H][2] (shared by all sites)
     std::vector<int> bn_S, bn_bs;   // per layer: batch slices and samples per slice
     float *params = nullptr, *grads = nullptr, *m = nullptr, *v = nullptr, *state = nullptr, *act = nullptr;
     bool bound = false;
@@ -1179,6 +1208,10 @@ int build_plan(DnPlan& p) {
     }
     long long bnp_ms;
     p.bnp_off = ar.take(bnp_max * 2, &bnp_ms);   // doubles = 2 floats (arena offsets are 64-float aligned)
+    int hmax = 1;
+    for (const Layer& ly : ls) hmax = std::max(hmax, ly.H);
+    long long bnt_ms;
+    p.bnt_off = ar.take(4LL * hmax, &bnt_ms);     // [n][H][2] doubles, indexed contiguously
     p.dz_off = ar.take(dz_max, &p.dz_ms);
     p.dt_off = ar.take(std::max(dt_max, 1LL), &p.dt_ms);
     p.part_off = ar.take(part_max, &p.part_ms);
@@ -1294,6 +1327,17 @@ int enqueue_prep(DnPlan& p, bool with_dgrad, hipStream_t s) {
     return MPO_OK;
 }
 
+// float4 rows for the BN kernels: channel count, pixel strides, member strides and
+// base pointers all multiples of 4 floats (every reference geometry; an odd growth
+// rate falls back to the scalar instances)
+bool bn_vec4(const BnArgs& a) {
+    auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+    bool ok = a.Cin % 4 == 0 && a.c0 % 4 == 0 && a.x_ps % 4 == 0 && a.x_ms % 4 == 0 && al(a.x);
+    ok = ok && a.dx_ps % 4 == 0 && a.dx_ms % 4 == 0 && al(a.dx);
+    ok = ok && (a.bcast ? a.dg_ms % 4 == 0 && al(a.dg) : a.dz_ms % 4 == 0 && al(a.dz));
+    return ok;
+}
+
 BnArgs bn_args(DnPlan& p, const Layer& ly, bool train) {
     BnArgs a{};
     const int s = ly.stage;
@@ -1304,6 +1348,7 @@ BnArgs bn_args(DnPlan& p, const Layer& ly, bool train) {
     a.params = p.params; a.p_ms = p.n_params; a.g_off = ly.g_off; a.b_off = ly.b_off;
     a.state = p.state; a.s_ms = p.n_state; a.mm_off = ly.mm_off; a.mv_off = ly.mv_off;
     a.grads = p.grads;
+    a.tot = reinterpret_cast<double*>(p.act + p.bnt_off);
     a.B = p.B; a.H = ly.H; a.W = ly.W; a.Cin = ly.cin; a.train = train ? 1 : 0;
     return a;
 }
@@ -1340,14 +1385,21 @@ int enqueue_forward(DnPlan& p, const float* x, const int* labels, const int* ord
         BnArgs bn = bn_args(p, ly, train);
         const size_t li = &ly - p.layers.data();
         double* bnp = reinterpret_cast<double*>(p.act + p.bnp_off);
-        if (train)
-            hipLaunchKernelGGL(dn_bn_stats_kernel, dim3(ly.H, p.bn_S[li], n), dim3(256), 0, s, bn, bnp, p.bn_S[li],
-                               p.bn_bs[li]);
+        // a dense layer's or transition's input is the previous dense layer's input plus
+        // that layer's growth slice: only the slice is read, its totals carried over
+        const Layer* pv = li > 0 ? &p.layers[li - 1] : nullptr;
+        if (pv && pv->kind == K_DENSE && pv->stage == ly.stage && pv->coff == pv->cin &&
+            pv->cin + pv->cout == ly.cin) {
+            bn.c0 = pv->cin;
+            bn.prev = 1;
+        }
+        if (train) {
+            auto kern = bn_vec4(bn) ? dn_bn_stats_kernel<4> : dn_bn_stats_kernel<1>;
+            hipLaunchKernelGGL(kern, dim3(ly.H, p.bn_S[li], n), dim3(256), 0, s, bn, bnp, p.bn_S[li], p.bn_bs[li]);
+        }
+        hipLaunchKernelGGL(dn_bn_coef_kernel, dim3(n), dim3(64), 0, s, bn, (const double*)bnp, p.bn_S[li]);
         if (ly.kind == K_HEAD)   // the head's GAP reads z: the only site that stores it
-            hipLaunchKernelGGL(dn_bn_apply_kernel, dim3(B * ly.H, n), dim3(256), 0, s, bn, (const double*)bnp,
-                               p.bn_S[li]);
-        else
-            hipLaunchKernelGGL(dn_bn_coef_kernel, dim3(n), dim3(64), 0, s, bn, (const double*)bnp, p.bn_S[li]);
+            hipLaunchKernelGGL(dn_bn_apply_kernel, dim3(B * ly.H, n), dim3(256), 0, s, bn);
         if (ly.kind == K_HEAD) {
             HeadArgs h = head_args(p, labels, order, ord_ms, row0, train);
             h.loss_out = loss_out; h.loss_sum = loss_sum; h.correct = correct;
@@ -1380,8 +1432,12 @@ int enqueue_forward(DnPlan& p, const float* x, const int* labels, const int* ord
 void enqueue_bn_bwd(DnPlan& p, const BnArgs& bn, int li, hipStream_t s) {
     double* bnp = reinterpret_cast<double*>(p.act + p.bnp_off);
     const int S = p.bn_S[li];
-    hipLaunchKernelGGL(dn_bn_bwd_reduce_kernel, dim3(bn.H, S, p.n), dim3(256), 0, s, bn, bnp, S, p.bn_bs[li]);
-    hipLaunchKernelGGL(dn_bn_bwd_apply_kernel, dim3(p.B * bn.H, p.n), dim3(256), 0, s, bn, (const double*)bnp, S);
+    const bool v4 = bn_vec4(bn);
+    hipLaunchKernelGGL(v4 ? dn_bn_bwd_reduce_kernel<4> : dn_bn_bwd_reduce_kernel<1>, dim3(bn.H, S, p.n), dim3(256), 0,
+                       s, bn, bnp, S, p.bn_bs[li]);
+    hipLaunchKernelGGL(dn_bn_bwd_fold_kernel, dim3(p.n), dim3(64), 0, s, bn, bnp, S);
+    hipLaunchKernelGGL(v4 ? dn_bn_bwd_apply_kernel<4> : dn_bn_bwd_apply_kernel<1>, dim3((p.B * bn.H + 1) / 2, p.n),
+                       dim3(256), 0, s, bn, (const double*)bnp, S);
 }
 
 int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_ms, long long row0, hipStream_t s) {
