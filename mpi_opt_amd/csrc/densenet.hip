@@ -859,39 +859,58 @@ __global__ __launch_bounds__(256) void dn_bn_bwd_apply_kernel(BnArgs a, const do
     }
 }
 
-// AvgPool2D((2,2), strides 2, valid): t [B][H][W][C] -> cat' [B][H/2][W/2][.] channels [0, C)
-__global__ void dn_pool_fwd_kernel(const float* __restrict__ t, long long t_ms, float* __restrict__ out, long long o_ms,
-                                   int o_ps, int B, int H, int W, int C) {
-    const int m = blockIdx.y, H2 = H / 2, W2 = W / 2;
-    const long long total = (long long)B * H2 * W2 * C;
-    const float* tm = t + m * t_ms;
-    float* om = out + m * o_ms;
-    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
-        const int c = (int)(e % C);
-        const long long pix = e / C;
-        const int x = (int)(pix % W2);
-        const long long r = pix / W2;
-        const int y = (int)(r % H2), b = (int)(r / H2);
-        const float* s = tm + (((long long)b * H + 2 * y) * W + 2 * x) * C + c;
-        om[pix * o_ps + c] = 0.25f * (s[0] + s[C] + s[(long long)W * C] + s[(long long)W * C + C]);
+// AvgPool2D((2,2), strides 2, valid): t [B][H][W][C] -> cat' [B][H/2][W/2][.] channels [0, C).
+// Two output rows per 256-thread block (grid (ceil(B H/2 / 2), member)), each row
+// walked as V-float channel groups -- no per-element 64-bit divisions.
+template <int V>
+__global__ __launch_bounds__(256) void dn_pool_fwd_kernel(const float* __restrict__ t, long long t_ms,
+                                                          float* __restrict__ out, long long o_ms, int o_ps, int B,
+                                                          int H, int W, int C) {
+    const int m = blockIdx.y, H2 = H / 2, W2 = W / 2, Cv = C / V;
+    const int row = blockIdx.x * 2 + (threadIdx.x >> 7), tid = threadIdx.x & 127;
+    if (row >= B * H2) return;
+    const int b = row / H2, y = row - b * H2;
+    const float* tr = t + m * t_ms + ((long long)b * H + 2 * y) * W * C;
+    float* orow = out + m * o_ms + (long long)row * W2 * o_ps;
+    const long long WC = (long long)W * C;
+    Walk2 wk(tid, Cv, 128);
+    for (int e = tid; e < W2 * Cv; e += 128, wk.next()) {
+        const float* s = tr + (long long)(2 * wk.q) * C + wk.c * V;
+        float s0[V], s1[V], s2[V], s3[V], v[V];
+        ldv<V>(s, s0);
+        ldv<V>(s + C, s1);
+        ldv<V>(s + WC, s2);
+        ldv<V>(s + WC + C, s3);
+#pragma unroll
+        for (int j = 0; j < V; ++j) v[j] = 0.25f * (s0[j] + s1[j] + s2[j] + s3[j]);
+        stv<V>(orow + (long long)wk.q * o_ps + wk.c * V, v);
     }
 }
 
-__global__ void dn_pool_bwd_kernel(const float* __restrict__ dcat, long long d_ms, int d_ps, float* __restrict__ dt,
-                                   long long t_ms, int B, int H, int W, int C) {
-    const int m = blockIdx.y, H2 = H / 2, W2 = W / 2;
-    const long long total = (long long)B * H * W * C;
-    const float* dm = dcat + m * d_ms;
-    float* tm = dt + m * t_ms;
-    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
-        const int c = (int)(e % C);
-        const long long pix = e / C;
-        const int x = (int)(pix % W);
-        const long long r = pix / W;
-        const int y = (int)(r % H), b = (int)(r / H);
-        float v = 0.f;
-        if ((y >> 1) < H2 && (x >> 1) < W2) v = 0.25f * dm[(((long long)b * H2 + (y >> 1)) * W2 + (x >> 1)) * d_ps + c];
-        tm[e] = v;
+// dt [B][H][W][C] = dcat'[y/2][x/2][c] / 4 (zero in a floor-mode odd last row / column)
+template <int V>
+__global__ __launch_bounds__(256) void dn_pool_bwd_kernel(const float* __restrict__ dcat, long long d_ms, int d_ps,
+                                                          float* __restrict__ dt, long long t_ms, int B, int H, int W,
+                                                          int C) {
+    const int m = blockIdx.y, H2 = H / 2, W2 = W / 2, Cv = C / V;
+    const int row = blockIdx.x * 2 + (threadIdx.x >> 7), tid = threadIdx.x & 127;
+    if (row >= B * H) return;
+    const int b = row / H, y = row - b * H;
+    const bool live_y = (y >> 1) < H2;
+    const float* dr = dcat + m * d_ms + ((long long)b * H2 + (y >> 1)) * W2 * d_ps;
+    float* trow = dt + m * t_ms + (long long)row * W * C;
+    Walk2 wk(tid, Cv, 128);
+    for (int e = tid; e < W * Cv; e += 128, wk.next()) {
+        float v[V];
+        if (live_y && (wk.q >> 1) < W2) {
+            ldv<V>(dr + (long long)(wk.q >> 1) * d_ps + wk.c * V, v);
+#pragma unroll
+            for (int j = 0; j < V; ++j) v[j] *= 0.25f;
+        } else {
+#pragma unroll
+            for (int j = 0; j < V; ++j) v[j] = 0.f;
+        }
+        stv<V>(trow + e * V, v);
     }
 }
 
@@ -1338,6 +1357,11 @@ bool bn_vec4(const BnArgs& a) {
     return ok;
 }
 
+bool pool_vec4(int C, int ps, long long ms_a, long long ms_b, const float* pa, const float* pb) {
+    auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+    return C % 4 == 0 && ps % 4 == 0 && ms_a % 4 == 0 && ms_b % 4 == 0 && al(pa) && al(pb);
+}
+
 BnArgs bn_args(DnPlan& p, const Layer& ly, bool train) {
     BnArgs a{};
     const int s = ly.stage;
@@ -1420,8 +1444,10 @@ int enqueue_forward(DnPlan& p, const float* x, const int* labels, const int* ord
             const long long tms = ((long long)B * ly.H * ly.W * ly.cout + 63) & ~63LL;
             c.out = p.act + ly.t_off; c.out_ms = tms; c.out_ps = ly.cout;
             DN_TRY(launch_conv<1>(c, n, B, s));
-            const long long tot = (long long)B * (ly.H / 2) * (ly.W / 2) * ly.cout;
-            hipLaunchKernelGGL(dn_pool_fwd_kernel, flat_grid(tot, n), dim3(256), 0, s, p.act + ly.t_off, tms,
+            const bool v4 = pool_vec4(ly.cout, p.sC[st + 1], tms, p.cat_ms[st + 1], p.act + ly.t_off,
+                                      p.act + p.cat_off[st + 1]);
+            hipLaunchKernelGGL(v4 ? dn_pool_fwd_kernel<4> : dn_pool_fwd_kernel<1>,
+                               dim3((B * (ly.H / 2) + 1) / 2, n), dim3(256), 0, s, p.act + ly.t_off, tms,
                                p.act + p.cat_off[st + 1], p.cat_ms[st + 1], p.sC[st + 1], B, ly.H, ly.W, ly.cout);
         }
     }
@@ -1461,8 +1487,10 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
         long long dout_ms;
         int dout_ps;
         if (ly.kind == K_TRANS) {
-            const long long tot = (long long)B * ly.H * ly.W * ly.cout;
-            hipLaunchKernelGGL(dn_pool_bwd_kernel, flat_grid(tot, n), dim3(256), 0, s, p.act + p.dcat_off[st + 1],
+            const bool v4 = pool_vec4(ly.cout, p.sC[st + 1], p.dt_ms, p.cat_ms[st + 1], p.act + p.dt_off,
+                                      p.act + p.dcat_off[st + 1]);
+            hipLaunchKernelGGL(v4 ? dn_pool_bwd_kernel<4> : dn_pool_bwd_kernel<1>, dim3((B * ly.H + 1) / 2, n),
+                               dim3(256), 0, s, p.act + p.dcat_off[st + 1],
                                p.cat_ms[st + 1], p.sC[st + 1], p.act + p.dt_off, p.dt_ms, B, ly.H, ly.W, ly.cout);
             dout = p.act + p.dt_off; dout_ms = p.dt_ms; dout_ps = ly.cout;
         } else {
