@@ -700,6 +700,145 @@ __global__ __launch_bounds__(kWgThreads) void conv_wgrad_kernel(StepArgs a, cons
     }
 }
 
+// conv1 weight gradient (Cin = 1): M = k*k + 1 rows (the last one the bias), N = F,
+// K = pixels.  M is at most 7 tiles, so the 8-wave m-group kernel above leaves most
+// of its waves idle behind a barrier per output row.  Here every wave holds every
+// m-tile of the member (MT = 1, 2, 4 or 7; padding tiles multiply the constant zero
+// row) and the 4 waves split the K dimension: wave w takes output rows w, w+4, ...
+// of the sample group's row stream.  The group's input images are staged in LDS
+// once (one barrier); B fragments come straight from memory one row ahead.  The 4
+// partial accumulators are summed through LDS in wave order (deterministic), into
+// the same partial slab as conv_wgrad<WG_CONV1>.
+constexpr int kW1Waves = 4;
+constexpr int kW1Slack = 64;   // zero floats past the last image (padded k-steps)
+
+__host__ __device__ constexpr inline int w1_lds_floats(int nb, int mt, int nt) {
+    return (nb * kImg * kImg + kW1Slack + 2) > (mt * nt * 4 * 64) ? (nb * kImg * kImg + kW1Slack + 2)
+                                                                  : (mt * nt * 4 * 64);
+}
+
+template <int NT, int MT>
+__global__ __launch_bounds__(kW1Waves * 64) void conv1_wgrad_kernel(StepArgs a, const WgItem* __restrict__ items) {
+    extern __shared__ __attribute__((aligned(16))) float sh[];   // images | slack | {0, 1}; then the reduction
+    const WgItem it = items[blockIdx.x];
+    const Member& mb = a.mem[it.member];
+    const int k = mb.k, F = mb.F, Ho = mb.H1, Kw = k * k;
+    const int tid = threadIdx.x, lane = tid & 63, krow = lane >> 4, kcol = lane & 15;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nk4 = (Ho + 3) >> 2;   // <= 7 (Ho <= 27)
+    const int nb = it.b1 - it.b0, nrows = nb * Ho;
+    const int kC0 = nb * kImg * kImg + kW1Slack, kC1 = kC0 + 1;
+    const int* order = a.order + (long long)it.member * a.order_stride + a.row0;
+    const float* zero = a.act + a.zero_off;
+    const float* dz1 = a.act + mb.dz1;
+
+    // stage the group's images (the k-fold index gather happens here)
+    for (int bl = 0; bl < nb; ++bl) {
+        const float* src = a.x + (long long)order[it.b0 + bl] * (kImg * kImg);
+        for (int e = tid; e < kImg * kImg; e += kW1Waves * 64) sh[bl * kImg * kImg + e] = src[e];
+    }
+    for (int e = nb * kImg * kImg + tid; e <= kC1; e += kW1Waves * 64) sh[e] = e == kC1 ? 1.f : 0.f;
+
+    int aoff[MT], ast[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+        const int m = i * 16 + (lane & 15);
+        if (m < Kw) {
+            const int ky = m / k, kx = m - ky * k;
+            aoff[i] = ky * kImg + kx;
+            ast[i] = 1;
+        } else {
+            aoff[i] = m == Kw ? kC1 : kC0;
+            ast[i] = 0;
+        }
+    }
+    // B fragments of dout row r (sample it.b0 + r / Ho): pixel 4s + krow, channel 16j + kcol;
+    // past the row, the channels or the stream they read zeros
+    auto loadB = [&](int r, float (&dst)[7][NT]) {
+        const int bl = r / Ho, y = r - bl * Ho;
+        const float* row = dz1 + ((long long)(it.b0 + bl) * Ho + y) * Ho * F;
+#pragma unroll
+        for (int s = 0; s < 7; ++s) {
+            const int x = 4 * s + krow;
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const int n = j * 16 + kcol;
+                const bool ok = r < nrows && s < nk4 && x < Ho && n < F;
+                dst[s][j] = *(ok ? row + x * F + n : zero + lane);
+            }
+        }
+    };
+    f32x4 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto row = [&](int r, const float (&bq)[7][NT]) {
+        const int bl = r / Ho, y = r - bl * Ho;
+        int ab[MT];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) ab[i] = ast[i] ? aoff[i] + bl * kImg * kImg + y * kImg : aoff[i];
+#pragma unroll
+        for (int s = 0; s < 7; ++s) {
+            if (s >= nk4) break;
+            const int x = 4 * s + krow;
+            float av[MT];
+#pragma unroll
+            for (int i = 0; i < MT; ++i) av[i] = sh[ab[i] + x * ast[i]];
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bq[s][j], acc[i][j], 0, 0, 0);
+        }
+    };
+
+    float b0[7][NT], b1[7][NT];
+    loadB(wave, b0);
+    __syncthreads();
+    if (a.debug != 1) {
+        for (int r = wave; r < nrows; r += 2 * kW1Waves) {
+            loadB(r + kW1Waves, b1);
+            row(r, b0);
+            if (r + kW1Waves >= nrows) break;
+            loadB(r + 2 * kW1Waves, b0);
+            row(r + kW1Waves, b1);
+        }
+    }
+
+    // fixed-order cross-wave sum through LDS (reusing the image space), then the slab
+    __syncthreads();
+    for (int w = 0; w < kW1Waves; ++w) {
+        if (wave == w) {
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        float* q = sh + ((i * NT + j) * 4 + r) * 64 + lane;
+                        const float v = w == 0 ? acc[i][j][r] : *q + acc[i][j][r];
+                        if (w + 1 < kW1Waves) *q = v; else acc[i][j][r] = v;
+                    }
+        }
+        if (w + 1 < kW1Waves) __syncthreads();
+    }
+    if (wave != kW1Waves - 1) return;
+    float* part = a.act + mb.wp1 + (long long)it.group * (Kw + 1) * F;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int n = j * 16 + kcol;
+            if (n >= F) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = i * 16 + krow * 4 + r;
+                if (m <= Kw) part[(long long)m * F + n] = acc[i][j][r];
+            }
+        }
+}
+
 // Sum the per-group partial slabs (fixed order) into the weight gradients.
 __global__ void wgrad_reduce_kernel(StepArgs a, const MItem* __restrict__ items, int per_block) {
     const MItem it = items[blockIdx.y];
@@ -1188,6 +1327,7 @@ struct Plan {
     float *params = nullptr, *grads = nullptr, *m = nullptr, *v = nullptr, *act = nullptr;
     bool bound = false;
     size_t lds_conv_max = 0, lds_wg_max = 0;
+    bool wg1_wave = true;   // conv1 weight gradient on conv1_wgrad_kernel (env MPO_WG1_WAVE=0: the m-group kernel)
 };
 
 size_t conv_lds_bytes(int rows, int Wp, int Cin, int K, int nt) {
@@ -1336,13 +1476,18 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         const size_t lw2 = wg_lds_bytes(k, m.H1, F, m.H2, F);
         const size_t lw1 = wg_lds_bytes(k, kImg, 1, m.H1, F);
         LW2[i] = lw2; LW1[i] = lw1;
+        if (i == 0) P.wg1_wave = env_int("MPO_WG1_WAVE", 1) != 0;
         const int K2 = k * k * F, K1w = k * k;
         for (int g = 0; g < m.g2; ++g) {
             const int b0 = (int)((long long)B * g / m.g2), b1 = (int)((long long)B * (g + 1) / m.g2);
             for (int mg = 0; mg * kWgRows <= K2; ++mg) P.wg2.push_back({i, mg, b0, b1, g, wg_mt(K2, mg)});
         }
+        // conv1_wgrad_kernel: every m-tile in one wave, MT bucketed to 1, 2, 4 or 7
+        const int t1 = (K1w + 1 + 15) / 16, mt1 = t1 <= 1 ? 1 : t1 <= 2 ? 2 : t1 <= 4 ? 4 : 7;
+        if (P.wg1_wave) LW1[i] = (size_t)w1_lds_floats((B + m.g1 - 1) / m.g1, mt1, nt) * sizeof(float);
         for (int g = 0; g < m.g1; ++g) {
             const int b0 = (int)((long long)B * g / m.g1), b1 = (int)((long long)B * (g + 1) / m.g1);
+            if (P.wg1_wave) { P.wg1.push_back({i, 0, b0, b1, g, mt1}); continue; }
             for (int mg = 0; mg * kWgRows <= K1w; ++mg) P.wg1.push_back({i, mg, b0, b1, g, wg_mt(K1w, mg)});
         }
         P.lds_wg_max = std::max({P.lds_wg_max, lw2, lw1});
@@ -1441,6 +1586,16 @@ hipError_t launch_wg_nt(const StepArgs& a, const WgItem* items, int count, size_
     return hipGetLastError();
 }
 
+template <int NT>
+hipError_t launch_wg1_wave_nt(const StepArgs& a, const WgItem* items, int count, size_t lds, int mt, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    auto kern = mt == 1 ? conv1_wgrad_kernel<NT, 1> : mt == 2 ? conv1_wgrad_kernel<NT, 2>
+              : mt == 4 ? conv1_wgrad_kernel<NT, 4> : conv1_wgrad_kernel<NT, 7>;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(count), dim3(kW1Waves * 64), lds, s, a, items);
+    return hipGetLastError();
+}
+
 template <class Fn>
 hipError_t launch_segs(Plan& P, const Bucketed& bk, const char* name, hipStream_t s, Fn launch_nt) {
     for (const Seg& sg : bk.segs) {
@@ -1492,6 +1647,8 @@ template <int OP>
 hipError_t launch_wg(Plan& P, const StepArgs& a, size_t table_off, const Bucketed& bk, hipStream_t s) {
     const WgItem* base = dev_table<WgItem>(P, table_off);
     return launch_segs(P, bk, OP == WG_CONV1 ? "conv1_wgrad" : "conv2_wgrad", s, [&](const Seg& sg) {
+        if (OP == WG_CONV1 && P.wg1_wave)
+            return MPO_NT_SWITCH(launch_wg1_wave_nt, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, sg.sub, s);
         return MPO_NT_SWITCH(WgLaunch<OP>::template go, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, sg.sub, s);
     });
 }
