@@ -116,6 +116,13 @@ __device__ __forceinline__ bool drop_keep(unsigned base, unsigned elem, unsigned
 //  * forward conv: lanes 0-15 read 16 pixels at stride fp, lanes 16-31 the next
 //    channel (+1): fp = 2 (mod 4) puts the two halves on the even / odd banks;
 __host__ __device__ constexpr inline int fwd_fp(int c) { return c == 1 ? 1 : c + ((6 - (c & 3)) & 3); }
+//  * and the LDS row stride = Ho * fp (mod 32): output pixel m = y*Ho + x then sits at
+//    m * fp (mod 32), so a 16-pixel tile that wraps to the next row stays on 16
+//    distinct banks (a Wp * fp stride shifts the wrapped part by (k-1) * fp).
+//    conv1 (one channel, taps on adjacent lanes) keeps the plain Wp stride.
+__host__ __device__ constexpr inline int fwd_rs(int Wp, int Cin, int Ho) {
+    return Cin == 1 ? Wp : Wp * fwd_fp(Cin) + ((Ho * fwd_fp(Cin) - Wp * fwd_fp(Cin)) & 31);
+}
 
 // ============================================================================
 // Image-stationary implicit-GEMM convolution (forward and input-gradient).
@@ -129,6 +136,15 @@ __host__ __device__ constexpr inline int align4(int x) { return (x + 3) & ~3; }
 // dgrad image pixel stride: >= F rounded to 4 (zero channels for the 16-channel
 // k blocks) and = 2 (mod 4), which makes the 4x4-tile A reads bank-conflict free.
 __host__ __device__ constexpr inline int dgrad_fp(int F) { return ((F + 3) & ~3) + 2; }
+
+// dgrad LDS row stride: >= H2 * Fp and = 8 (mod 32).  A 4x4 patch reads rows dy at
+// dy * RS and columns dx at dx * Fp: with Fp = 2 (mod 4) the columns take the four
+// even residues mod 8 and the rows the four multiples of 8, so the 16 pixels (and
+// the next channel, +1, on the odd banks) are conflict-free.  An unpadded H2 * Fp is
+// = 0 or 16 (mod 32) (H2 even) and put rows dy and dy + 2 on the same banks.
+__host__ __device__ constexpr inline int dgrad_rs(int H2, int F) {
+    return H2 * dgrad_fp(F) + ((8 - ((H2 * dgrad_fp(F)) & 31)) & 31);
+}
 
 // Copy n contiguous floats (pixels of cin channels) into an LDS image with
 // pixel stride fp, without a per-element integer division.
@@ -242,7 +258,8 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
     const int M = it.R * Ho;
 
     float* img = smem;                                               // [rows][Wp][Fp]
-    const int img_elems = rows * Wp * Fp;
+    const int RS = fwd_rs(Wp, Cin, Ho);
+    const int img_elems = rows * RS;
     int* koff = reinterpret_cast<int*>(smem + align4(img_elems));   // [K16 + slack], groups of 16 as [krow][4]
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -251,7 +268,7 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
     // ---- stage the input rows + the tap-offset table (the only barrier)
     for (int r = 0; r < rows && a.debug != 2; ++r) {
         const float* src = in + (long long)(it.y0 + r) * Hin * Cin;
-        float* dst = img + r * Wp * Fp;
+        float* dst = img + r * RS;
         if (Cin == 1) {
             for (int e = tid; e < Hin; e += 256) dst[e] = src[e];
         } else {
@@ -264,7 +281,7 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
             const int kc = k * Cin;
             const int ky = kk / kc, rem = kk - ky * kc;
             const int kx = rem / Cin, c = rem - kx * Cin;
-            off = (ky * Wp + kx) * Fp + c;
+            off = ky * RS + kx * Fp + c;
         }
         const int g = kk >> 4, w = kk & 15;        // k = 16 g + 4 u + krow
         koff[g * 16 + (w & 3) * 4 + (w >> 2)] = off;
@@ -279,7 +296,7 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
         int base = 0;
         if (m < M) {
             const int y = m / Ho, xx = m - y * Ho;
-            base = (y * Wp + xx) * Fp;
+            base = y * RS + xx * Fp;
         }
         pb[i] = base;
     }
@@ -348,8 +365,9 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
     float* out = a.act + mb.dz1 + (long long)it.b * Ho * Ho * F;
     const float* relu_mask = a.act + mb.a1 + (long long)it.b * Ho * Ho * F;
 
-    float* img = smem;  // [rows][H2][Fp], channels >= F zero; then a 64-float zero block
-    const int zoff = align4(rows * H2 * Fp);
+    float* img = smem;  // [rows][RS] (H2 pixels of Fp), channels >= F zero; then a 64-float zero block
+    const int RS = dgrad_rs(H2, F);
+    const int zoff = align4(rows * RS);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: tile logic stays scalar
     const int krow = lane >> 4, kcol = lane & 15;
@@ -357,7 +375,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
     for (int e = tid; e < zoff + 64; e += 256) img[e] = 0.f;
     __syncthreads();
     for (int r = 0; r < rows && a.debug != 2; ++r)
-        stage_row(in + (long long)(gy_lo + r) * H2 * F, img + r * H2 * Fp, H2 * F, F, Fp, tid);
+        stage_row(in + (long long)(gy_lo + r) * H2 * F, img + r * RS, H2 * F, F, Fp, tid);
 
     // ---- this wave's 4x4 tiles, their tap rectangles and the wave's union rectangle
     const int CT = (Ho + 3) >> 2;
@@ -424,7 +442,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
         for (int i = 0; i < 4; ++i) {
             const int ry = py[i] + ky, cx = px[i] + kx;
             const int base = ((unsigned)ry < (unsigned)rows && (unsigned)cx < (unsigned)H2)
-                                 ? (ry * H2 + cx) * Fp + coff : zoff + krow;   // halo -> zero block
+                                 ? ry * RS + cx * Fp + coff : zoff + krow;   // halo -> zero block
 #pragma unroll
             for (int u = 0; u < 4; ++u) av[u][i] = img[base + u * 4];
         }
@@ -1330,15 +1348,16 @@ struct Plan {
     bool wg1_wave = true;   // conv1 weight gradient on conv1_wgrad_kernel (env MPO_WG1_WAVE=0: the m-group kernel)
 };
 
-size_t conv_lds_bytes(int rows, int Wp, int Cin, int K, int nt) {
+size_t conv_lds_bytes(int rows, int Wp, int Cin, int Ho, int K, int nt) {
     (void)nt;
     const int Fp = fwd_fp(Cin);
-    return (size_t)(align4(rows * Wp * Fp) + ((K + 15) & ~15) + kKoffSlack) * sizeof(float);
+    (void)Fp;
+    return (size_t)(align4(rows * fwd_rs(Wp, Cin, Ho)) + ((K + 15) & ~15) + kKoffSlack) * sizeof(float);
 }
 
 size_t dgrad_lds_bytes(int R, int k, int F, int H2) {
     const int rows = std::min(H2, R + k - 1);   // dz2 rows of the widest chunk (unpadded)
-    return (size_t)(align4(rows * H2 * dgrad_fp(F)) + 64) * sizeof(float);
+    return (size_t)(align4(rows * dgrad_rs(H2, F)) + 64) * sizeof(float);
 }
 
 size_t wg_lds_bytes(int k, int Hin, int Cin, int Ho, int F) {
@@ -1454,15 +1473,15 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
     for (int i = 0; i < n; ++i) {
         const Member& m = P.mem[i];
         const int k = m.k, F = m.F, nt = m.nt;
-        const int R1 = choose_rows(m.H1, [&](int R) { return conv_lds_bytes(R + k - 1, kImg, 1, k * k, nt); }, kc1, kc2);
-        const int R2 = choose_rows(m.H2, [&](int R) { return conv_lds_bytes(R + k - 1, m.H1, F, k * k * F, nt); }, kc1, kc2);
+        const int R1 = choose_rows(m.H1, [&](int R) { return conv_lds_bytes(R + k - 1, kImg, 1, m.H1, k * k, nt); }, kc1, kc2);
+        const int R2 = choose_rows(m.H2, [&](int R) { return conv_lds_bytes(R + k - 1, m.H1, F, m.H2, k * k * F, nt); }, kc1, kc2);
         // dgrad: 4x4-pixel tiles in bands of 4 rows, <= 16 tiles (4 per wave) per chunk:
         // R = 4 * floor(16 / CT); 4-row bands fewer if the LDS budget asks for it
         const size_t dgb = (size_t)kdg << 10;
         int Rd = 4 * std::max(1, 16 / ((m.H1 + 3) / 4));
         while (Rd > 4 && dgrad_lds_bytes(Rd, k, F, m.H2) > dgb) Rd -= 4;
-        const size_t l1 = conv_lds_bytes(R1 + k - 1, kImg, 1, k * k, nt);
-        const size_t l2 = conv_lds_bytes(R2 + k - 1, m.H1, F, k * k * F, nt);
+        const size_t l1 = conv_lds_bytes(R1 + k - 1, kImg, 1, m.H1, k * k, nt);
+        const size_t l2 = conv_lds_bytes(R2 + k - 1, m.H1, F, m.H2, k * k * F, nt);
         const size_t ld = dgrad_lds_bytes(Rd, k, F, m.H2);
         L1[i] = l1; L2[i] = l2; LD[i] = ld;
         for (int b = 0; b < B; ++b) {
