@@ -154,3 +154,27 @@ def test_population_isolation():
         la = eng_all.train_step(xd, yd, torch.from_numpy(tr).cuda(), st * BATCH).cpu().numpy()
         lo = eng_one.train_step(xd, yd, torch.from_numpy(tr[2:3]).cuda(), st * BATCH).cpu().numpy()
         assert la[2] == lo[0]
+
+
+def test_conv1_wgrad_kernels_agree(monkeypatch):
+    """conv1_wgrad_kernel (default) and the m-group conv_wgrad<WG_CONV1> kernel
+    (MPO_WG1_WAVE=0) give the same conv1 weight and bias gradients (different f32
+    summation orders: within 1e-5 of the tensor scale); the rest bit-identical."""
+    x, y = dataset(2)
+    tr, _ = orders(MEMBERS, x)
+    xd, yd = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    otr = torch.from_numpy(tr).cuda()
+    out = {}
+    for wave in ("1", "0"):
+        monkeypatch.setenv("MPO_WG1_WAVE", wave)
+        eng, specs, _ = make_engine()
+        eng.train_step(xd, yd, otr, 0)
+        out[wave] = (eng, eng.grads.cpu().numpy())
+    for i in range(len(MEMBERS)):
+        for name, (off, shape) in out["1"][0]._slices(i).items():
+            a = out["1"][1][off:off + int(np.prod(shape))]
+            b = out["0"][1][off:off + int(np.prod(shape))]
+            if name in ("w1", "b1"):
+                assert np.max(np.abs(a - b)) <= 1e-5 * (np.max(np.abs(b)) + 1e-30), (i, name)
+            else:
+                assert np.array_equal(a, b), (i, name)
