@@ -31,7 +31,7 @@ class MpoGpModel(ctypes.Structure):
         ("amp", ctypes.c_double), ("y_mean", ctypes.c_double), ("y_std", ctypes.c_double),
         ("xs", ctypes.c_void_p), ("ls", ctypes.c_void_p), ("alpha", ctypes.c_void_p),
         ("wfrag", ctypes.c_void_p), ("L", ctypes.c_void_p), ("W", ctypes.c_void_p),
-        ("info", ctypes.c_void_p), ("wmeta", ctypes.c_void_p),
+        ("info", ctypes.c_void_p), ("wmeta", ctypes.c_void_p), ("xb", ctypes.c_void_p),
     ]
 
 

@@ -159,6 +159,54 @@ __global__ void zero_kernel(double* __restrict__ p, int n) {
     if (t < n) p[t] = 0.0;
 }
 
+// MFMA form of the candidate-observation distance (gp_score_kernel<.., MD = 1>):
+// xb row i = (-2 xs_i, 1, |xs_i|^2, 0 ...), so that [c, |c|^2, 1, 0 ...] . xb_i =
+// |c - xs_i|^2 with an absolute rounding error of a few eps (|c|^2 + |xs_i|^2).
+// One block; xb[rows * dp] = 1.0 when every |xs_i|^2 <= kDistNorm, else 0.0.
+constexpr double kDistNorm = 2.0;
+__global__ __launch_bounds__(256) void xb_kernel(const double* __restrict__ xs, int rows, int d, int dp,
+                                                 double* __restrict__ xb) {
+    __shared__ int bad;
+    if (threadIdx.x == 0) bad = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < rows; i += 256) {
+        double xx = 0.0;
+        for (int c = 0; c < d; ++c) xx = fma(xs[(size_t)i * dp + c], xs[(size_t)i * dp + c], xx);
+        for (int c = 0; c < dp; ++c)
+            xb[(size_t)i * dp + c] = c < d ? -2.0 * xs[(size_t)i * dp + c] : c == d ? 1.0 : c == d + 1 ? xx : 0.0;
+        if (!(xx <= kDistNorm)) atomicOr(&bad, 1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) xb[(size_t)rows * dp] = bad ? 0.0 : 1.0;
+}
+
+// Self-check of the expanded distance on the model's own observations (r2 = 0 at
+// each one's own row and the smallest sd: its worst case): clears the xb flag
+// unless both (mu_n, q) rows -- direct and expanded -- agree within 1e-10: q
+// relative to sd^2 = amp - q, mu_n relative to its summand scale amp sum |alpha_i|
+// (the conditioning of K*.alpha; the parity tests measure mu against the same kind
+// of scale).
+__global__ __launch_bounds__(256) void xb_check_kernel(const double* __restrict__ mqd, const double* __restrict__ mqm,
+                                                       const double* __restrict__ alpha, int n, double amp,
+                                                       double* __restrict__ flag) {
+    __shared__ int bad;
+    __shared__ double red[4];
+    if (threadIdx.x == 0) bad = 0;
+    double sa = 0.0;
+    for (int i = threadIdx.x; i < n; i += 256) sa += fabs(alpha[i]);
+    for (int o = 32; o > 0; o >>= 1) sa += __shfl_down(sa, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sa;
+    __syncthreads();
+    const double mu_scale = amp * (red[0] + red[1] + red[2] + red[3]);
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const double mud = mqd[2 * i], qd = mqd[2 * i + 1], mum = mqm[2 * i], qm = mqm[2 * i + 1];
+        const bool ok = fabs(qm - qd) <= 1e-10 * fmax(amp - qd, 1e-300) && fabs(mum - mud) <= 1e-10 * mu_scale;
+        if (!ok) atomicOr(&bad, 1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && bad) flag[0] = 0.0;
+}
+
 __global__ void kernel_matrix_kernel(const double* __restrict__ xs, int n, int dp, double amp,
                                      double diag_add, double* __restrict__ K, int ldk) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -330,6 +378,8 @@ struct ScoreArgs {
     int n, np16, T, d;
     double amp, y_mean, y_std;
     const double* xs;
+    const double* xb;     // MD = 1: augmented observation rows (xb_kernel)
+    const double* xb_ok;  // MD = 1: device flag, every |xs_i|^2 <= kDistNorm
     const double* ls;
     const double* alpha;
     const double* wfrag;
@@ -411,8 +461,9 @@ __global__ __launch_bounds__(kFinishThreads) void score_finish_kernel(ScoreArgs 
 // One workgroup = 4 waves looping over 16-candidate tiles (kBM) tile = blockIdx.x,
 // += gridDim.x (the grid is sized to the resident capacity); the next tile's
 // candidate rows are loaded while the current one is scored.
-template <int DP, int D, int OCC>
+template <int DP, int D, int OCC, int MD>
 __global__ __launch_bounds__(256, OCC) void gp_score_kernel(ScoreArgs a) {
+    static_assert(!MD || D + 2 <= DP, "the MFMA distance needs two spare columns");
     constexpr int BM = kBM;
     constexpr int S = 16;            // i-slots per block in phase 1 (4 per wave)
     constexpr int EPT = (BM * DP + 255) / 256;   // candidate elements per thread in phase 0
@@ -478,7 +529,65 @@ __global__ __launch_bounds__(256, OCC) void gp_score_kernel(ScoreArgs a) {
 #pragma unroll
         for (int q = 0; q < D; ++q) c[q] = cs[row * DP + q];
         double mu_acc = 0.0;
-        if (a.dbg & 2) {
+        bool md = false;   // this tile on the MFMA distance (every |c|^2 <= kDistNorm)
+        if constexpr (MD) {
+            double cc = 0.0;
+#pragma unroll
+            for (int q = 0; q < D; ++q) cc = fma(c[q], c[q], cc);
+            md = __all(cc <= kDistNorm) && *a.xb_ok != 0.0;
+            if (md && !(a.dbg & 2)) {
+                // K*[16 candidates][16 observations] per tile t of this wave: r2 as one
+                // augmented dot product on f64 MFMA (A = [c, |c|^2, 1], B = xb), then the
+                // Matern per C element.  f64 C/D map: col = lane & 15 (observation),
+                // row = (lane >> 4) + 4 r (candidate).
+                const int kr = lane >> 4;
+                double af[DP / 4];
+#pragma unroll
+                for (int s = 0; s < DP / 4; ++s) {
+                    const int kk = 4 * s + kr;
+                    const double v = cs[row * DP + kk];
+                    af[s] = kk == D ? cc : kk == D + 1 ? 1.0 : v;
+                }
+                const int T16 = np16 >> 4;
+                const double* xbl = a.xb + (size_t)(lane & 15) * DP + kr;
+                double bq[DP / 4];
+                double mu4[4] = {0.0, 0.0, 0.0, 0.0};
+                for (int t = wave; t < T16; t += 4) {
+#pragma unroll
+                    for (int s = 0; s < DP / 4; ++s) bq[s] = xbl[(size_t)t * 16 * DP + 4 * s];
+                    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                    for (int s = 0; s < DP / 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(af[s], bq[s], acc, 0, 0, 0);
+                    const int i = t * 16 + (lane & 15);
+                    const double al = a.alpha[i];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const double kv = matern52_unit(fmax(acc[r], kR2Floor));
+                        kc[(size_t)(i >> 2) * 64 + kr + 4 * r + (i & 3) * 16] = kv;
+                        mu4[r] = fma(kv, al, mu4[r]);
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    double v = mu4[r];
+                    v += __shfl_xor(v, 1);
+                    v += __shfl_xor(v, 2);
+                    v += __shfl_xor(v, 4);
+                    v += __shfl_xor(v, 8);
+                    mu4[r] = v;
+                }
+                // this wave's 4 slots: the sum in slot 0, zeros in 1..3 (the mu fold below
+                // sums all 16 slots in order)
+                if ((lane & 15) == 0) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) red[(wave * 4 + q) * BM + kr + 4 * r] = q == 0 ? mu4[r] : 0.0;
+                }
+            }
+        }
+        if (md && !(a.dbg & 2)) {
+        } else if (a.dbg & 2) {
             for (int i = slot; i < np16; i += S) kc[(size_t)(i >> 2) * 64 + row + (i & 3) * 16] = c[0];
         } else {
             // one observation row: r2, Matern, mu partial, K* into LDS
@@ -499,7 +608,7 @@ __global__ __launch_bounds__(256, OCC) void gp_score_kernel(ScoreArgs a) {
             }
 #undef MPO_EI_PAIR
         }
-        red[slot * BM + row] = mu_acc;
+        if (!md || (a.dbg & 2)) red[slot * BM + row] = mu_acc;
     }
     __syncthreads();
     double mu_n = 0.0;
@@ -680,9 +789,9 @@ size_t score_lds_bytes(int dp, int np16) {
 bool score_fits(int dp, int np16) { return score_lds_bytes(dp, np16) <= kMaxLds; }
 
 // grid = the device's resident capacity for this variant (tiles are looped over)
-template <int DP, int D, int OCC>
+template <int DP, int D, int OCC, int MD>
 hipError_t launch_score(const ScoreArgs& a, int ntiles, size_t lds, hipStream_t s) {
-    auto kern = gp_score_kernel<DP, D, OCC>;
+    auto kern = gp_score_kernel<DP, D, OCC, MD>;
     // The B ring's asm loads are invisible to the compiler: a spill of a ring
     // register would store it before its load lands.  A variant whose register
     // cap forces spills is refused instead of run.
@@ -702,12 +811,12 @@ hipError_t launch_score(const ScoreArgs& a, int ntiles, size_t lds, hipStream_t 
     return hipGetLastError();
 }
 
-template <int DP, int D, int OCC>
+template <int DP, int D, int OCC, int MD>
 bool spill_free() {
     static int ok = -1;
     if (ok < 0) {
         hipFuncAttributes fa;
-        ok = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(gp_score_kernel<DP, D, OCC>)) == hipSuccess &&
+        ok = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(gp_score_kernel<DP, D, OCC, MD>)) == hipSuccess &&
              fa.localSizeBytes == 0;
     }
     return ok == 1;
@@ -715,18 +824,29 @@ bool spill_free() {
 
 // occupancy hint (min waves per SIMD -> VGPR cap): the highest spill-free one;
 // MPO_GP_OCC (2, 4, 5, 6) forces one for experiments
-template <int DP, int D>
-hipError_t launch_score_occ(const ScoreArgs& a, int nblocks, size_t lds, hipStream_t s) {
+template <int DP, int D, int MD>
+hipError_t launch_score_occ_md(const ScoreArgs& a, int nblocks, size_t lds, hipStream_t s) {
     const char* e = getenv("MPO_GP_OCC");
     int occ = e ? atoi(e) : 0;
     if (occ != 2 && occ != 4 && occ != 5 && occ != 6)
-        occ = spill_free<DP, D, 6>() ? 6 : spill_free<DP, D, 5>() ? 5 : spill_free<DP, D, 4>() ? 4 : 2;
+        occ = spill_free<DP, D, 6, MD>() ? 6 : spill_free<DP, D, 5, MD>() ? 5 : spill_free<DP, D, 4, MD>() ? 4 : 2;
     switch (occ) {
-        case 6: return launch_score<DP, D, 6>(a, nblocks, lds, s);
-        case 5: return launch_score<DP, D, 5>(a, nblocks, lds, s);
-        case 4: return launch_score<DP, D, 4>(a, nblocks, lds, s);
-        default: return launch_score<DP, D, 2>(a, nblocks, lds, s);
+        case 6: return launch_score<DP, D, 6, MD>(a, nblocks, lds, s);
+        case 5: return launch_score<DP, D, 5, MD>(a, nblocks, lds, s);
+        case 4: return launch_score<DP, D, 4, MD>(a, nblocks, lds, s);
+        default: return launch_score<DP, D, 2, MD>(a, nblocks, lds, s);
     }
+}
+
+// MD = 1 (the MFMA distance) when the model carries xb (d + 2 <= dp and the
+// rounding bound of mpo_gp_prepare holds); MPO_GP_DIST=0 forces the direct form
+template <int DP, int D>
+hipError_t launch_score_occ(const ScoreArgs& a, int nblocks, size_t lds, hipStream_t s) {
+    if constexpr (D + 2 <= DP) {
+        const char* e = getenv("MPO_GP_DIST");
+        if (a.xb && a.xb_ok && !(e && e[0] == '0')) return launch_score_occ_md<DP, D, 1>(a, nblocks, lds, s);
+    }
+    return launch_score_occ_md<DP, D, 0>(a, nblocks, lds, s);
 }
 
 // (padded row width DP, distance dims D): d = 5 and d = 10 (the reference's mnist
@@ -995,6 +1115,8 @@ size_t mpo_gp_prepare_ws_bytes(int n, int d) {
     c.take<double>(wfrag_elems(np16));     // wfrag
     c.take<int32_t>(4);                    // info
     c.take<int32_t>(wmeta_elems(np16));    // wmeta
+    c.take<double>((size_t)xrows * dp + 8);   // xb + its guard flag
+    c.take<double>(4 * (size_t)n);            // xb self-check (mu_n, q) rows, direct and expanded
     return c.used + 256;
 }
 
@@ -1021,6 +1143,8 @@ int mpo_gp_prepare(const double* X, const double* y_norm, int n, int d, const do
     double* wfrag = c.take<double>(wfrag_elems(np16));
     int32_t* info = c.take<int32_t>(4);
     int32_t* wmeta = c.take<int32_t>(wmeta_elems(np16));
+    double* xb = c.take<double>((size_t)xrows * dp + 8);
+    double* mqc = c.take<double>(4 * (size_t)n);
 
     hipLaunchKernelGGL(scale_rows_kernel, dim3((xrows * dp + 255) / 256), dim3(256), 0, s, X, n, xrows, d, dp, ls, xs,
                        ls_pad);
@@ -1051,6 +1175,39 @@ int mpo_gp_prepare(const double* X, const double* y_norm, int n, int d, const do
     hipLaunchKernelGGL(pack_wfrag_kernel, dim3((4 * T * 64 + 255) / 256, T), dim3(256), 0, s, W, n, n, T, wmeta,
                        wfrag);
     MPO_LAUNCH_CHECK();
+    // The expanded (MFMA) distance |c|^2 + |x|^2 - 2 c.x (d + 2 <= dp) carries an absolute
+    // error of a few eps (|c|^2 + |x|^2) instead of the direct form's eps r2.  Its device
+    // flag is set only when every |x|^2 <= kDistNorm and, scoring the observations
+    // themselves both ways, (mu_n, q) agree within 1e-10; candidate tiles with some
+    // |c|^2 > kDistNorm take the direct form in the kernel.  MPO_GP_DIST=0: never.
+    const char* de = getenv("MPO_GP_DIST");
+    const bool use_xb = d + 2 <= dp && !(de && de[0] == '0');
+    bool xb_set = false;
+    if (use_xb) {
+        double* flag = xb + (size_t)xrows * dp;
+        hipLaunchKernelGGL(xb_kernel, dim3(1), dim3(256), 0, s, xs, xrows, d, dp, xb);
+        MPO_LAUNCH_CHECK();
+        ScoreArgs sa{};
+        sa.n = n; sa.np16 = np16; sa.T = T; sa.d = d;
+        sa.amp = amp; sa.y_mean = y_mean; sa.y_std = y_std;
+        sa.xs = xs; sa.ls = ls_pad; sa.alpha = alpha; sa.wfrag = wfrag; sa.wmeta = wmeta;
+        sa.cand = X; sa.m = n; sa.flags = 1;
+        const int nt = (n + kBM - 1) / kBM;
+        const size_t lds = score_lds_bytes(dp, np16);
+        sa.mq = mqc;                                   // direct form
+        bool ok = launch_score_dp(dp, d, sa, nt, lds, s) == hipSuccess;
+        sa.mq = mqc + 2 * (size_t)n;                   // expanded form
+        sa.xb = xb;
+        sa.xb_ok = flag;
+        // a refused variant (MPO_GP_OCC forcing a spilling one) just leaves xb out
+        ok = ok && launch_score_dp(dp, d, sa, nt, lds, s) == hipSuccess;
+        if (ok) {
+            hipLaunchKernelGGL(xb_check_kernel, dim3(1), dim3(256), 0, s, mqc, mqc + 2 * (size_t)n, alpha, n, amp,
+                               flag);
+            MPO_LAUNCH_CHECK();
+        }
+        xb_set = ok;
+    }
 
     model->n = n;
     model->d = d;
@@ -1067,6 +1224,7 @@ int mpo_gp_prepare(const double* X, const double* y_norm, int n, int d, const do
     model->W = W;
     model->info = info;
     model->wmeta = wmeta;
+    model->xb = xb_set ? xb : nullptr;
     return MPO_OK;
     MPO_GUARD_END
 }
@@ -1110,6 +1268,8 @@ static int gp_score_impl(const MpoGpModel* model, const double* cand, int64_t m,
     a.y_mean = model->y_mean;
     a.y_std = model->y_std;
     a.xs = model->xs;
+    a.xb = model->xb;
+    a.xb_ok = model->xb ? model->xb + (size_t)(model->np16 + 32) * model->dp : nullptr;
     a.ls = model->ls;
     a.alpha = model->alpha;
     a.wfrag = model->wfrag;

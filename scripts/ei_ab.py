@@ -17,7 +17,7 @@ X, y = synthetic.gp_problem(200, 10, 0)
 ls = np.array([16.2, 1.91, 1.65, 9.84, 1.84, 2.94, 2.45, 9.09, 8.13, 1.94])
 g = DeviceGP(X, y, 17.4955, ls, 0.0465)
 cand = torch.from_numpy(synthetic.gp_candidates(1_000_000, 10, seed=1)).cuda()
-KEYS = ("MPO_GP_OCC", "MPO_GP_DEBUG")
+KEYS = ("MPO_GP_OCC", "MPO_GP_DEBUG", "MPO_GP_DIST")
 if len(sys.argv) > 1:
     VARIANTS = {}
     for arg in sys.argv[1:]:

@@ -13,6 +13,7 @@ import os
 
 import numpy as np
 import pytest
+import torch
 
 from mpi_opt_amd._lib import MpoError
 from oracle import gp_ei as O
@@ -182,3 +183,59 @@ def test_million_candidates_argmax_matches_skopt_form():
     sel = np.random.RandomState(3).choice(C.shape[0], 2048, replace=False)
     mu_x, sd_x = O.posterior_exact(st, C[sel])
     assert np.max(np.abs(out["sd"].cpu().numpy()[sel] - sd_x.astype(np.float64)) / sd_x.astype(np.float64)) < 1e-9
+
+
+def _xb_flag(g):
+    """The expanded-distance device flag of a prepared model (None without xb)."""
+    m = g.model
+    if not m.xb:
+        return None
+    off = m.xb + (m.np16 + 32) * m.dp * 8 - g._ws.data_ptr()
+    return float(g._ws[off:off + 8].cpu().numpy().view(np.float64)[0])
+
+
+@pytest.mark.parametrize("path", FIXTURES, ids=os.path.basename)
+def test_expanded_distance_matches_direct(path, monkeypatch):
+    """The MFMA (expanded) distance path -- enabled by mpo_gp_prepare's self-check when
+    d + 2 <= dp -- meets the 1e-9 bar against the exact posterior, agrees with the
+    direct differences within 1e-10 and gives the same top-k; MPO_GP_DIST=0 builds
+    no xb.  At the BASELINE fixture the self-check passes."""
+    f = load(path)
+    C = torch.from_numpy(f["C"]).cuda()
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MPO_GP_DIST", mode)
+        g = device_gp(f)
+        out[mode] = (g, g.score(C, float(f["y_opt"]), acqs=("EI",), k=5))
+    g1, o1 = out["1"]
+    assert not out["0"][0].model.xb
+    d, dp = g1.model.d, g1.model.dp
+    if d + 2 <= dp:
+        assert g1.model.xb
+        if os.path.basename(path) == "gp_ei_n200_d10.npz":
+            assert _xb_flag(g1) == 1.0
+    o0 = out["0"][1]
+    sd0, sd1 = o0["sd"].cpu().numpy(), o1["sd"].cpu().numpy()
+    assert np.max(np.abs(sd1 - f["sd_exact"]) / f["sd_exact"]) < 1e-9
+    assert np.max(np.abs(sd1 - sd0) / sd0) < 1e-10
+    mu0, mu1 = o0["mu"].cpu().numpy(), o1["mu"].cpu().numpy()
+    st = O.gp_from_theta(f["X"], f["y"], float(f["amp"]), f["ls"], float(f["noise"]))
+    assert np.max(np.abs(mu1 - f["mu_exact"]) / mu_scale(st, f["C"])) < 1e-9
+    assert np.array_equal(o0["topk"]["EI"][0].cpu().numpy(), o1["topk"]["EI"][0].cpu().numpy())
+
+
+def test_expanded_distance_far_candidates_fall_back(monkeypatch):
+    """Candidate tiles with |c/ls|^2 > kDistNorm take the direct form: candidates far
+    outside [0,1]^d (where the expansion would lose digits) still match the exact
+    posterior at the 1e-9 bar."""
+    f = load(os.path.join(GOLDEN, "gp_ei_n200_d10.npz"))
+    monkeypatch.setenv("MPO_GP_DIST", "1")
+    g = device_gp(f)
+    assert g.model.xb
+    C = f["C"][:512] * 40.0 - 20.0
+    st = O.gp_from_theta(f["X"], f["y"], float(f["amp"]), f["ls"], float(f["noise"]))
+    mu_x, sd_x = O.posterior_exact(st, C)
+    out = g.score(torch.from_numpy(C).cuda(), float(f["y_opt"]), acqs=("EI",), k=5)
+    sd = out["sd"].cpu().numpy()
+    assert np.all(np.isfinite(sd))
+    assert np.max(np.abs(sd - sd_x) / sd_x) < 1e-9
