@@ -479,6 +479,7 @@ __global__ __launch_bounds__(256, OCC) void gp_score_kernel(ScoreArgs a) {
     const long long ntiles = (a.m + BM - 1) / BM;
 
     for (int e = tid; e < 4 * (a.T + 4); e += 256) mls[e] = a.wmeta[e];
+    const bool xb_ok = MD && *a.xb_ok != 0.0;   // read once: the model-level guard of the expanded distance
     // thread tid owns elements tid + 256 u of the [BM][DP] candidate tile
     double raw[EPT], ls_e[EPT];
 #pragma unroll
@@ -534,7 +535,7 @@ __global__ __launch_bounds__(256, OCC) void gp_score_kernel(ScoreArgs a) {
             double cc = 0.0;
 #pragma unroll
             for (int q = 0; q < D; ++q) cc = fma(c[q], c[q], cc);
-            md = __all(cc <= kDistNorm) && *a.xb_ok != 0.0;
+            md = xb_ok && __all(cc <= kDistNorm);
             if (md && !(a.dbg & 2)) {
                 // K*[16 candidates][16 observations] per tile t of this wave: r2 as one
                 // augmented dot product on f64 MFMA (A = [c, |c|^2, 1], B = xb), then the

@@ -562,8 +562,7 @@ __global__ __launch_bounds__(kFitThreads) void lml_sweep_kernel(LmlArgs a) {
     double* A = alpha + al(np);                    // [np][np], lower triangle + full diagonal tiles
     double* G = A + (long long)np * np;            // [np][32]
     double* Cp = fsm;                              // [np][33] old block column
-    double* Pi = Cp + np * kSwLd;                  // [32][33] P^-1
-    double* Pr = Pi + kSwNb * kSwLd;               // [32][33] pivot-row broadcast / reductions
+    double* Pi = Cp + np * kSwLd;                  // [32][33] P^-1 (then a [32][33] pivot-row area, unused here)
     __shared__ int fail_s;
     __shared__ double logdet_s;
 
