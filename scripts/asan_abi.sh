@@ -17,8 +17,8 @@ for f in mpi_opt_amd/csrc/*.hip; do
 done
 $HIPCC $FLAGS -x hip -c mpi_opt_amd/csrc/api.cpp -o $B/api.o &
 wait
-$HIPCC -shared -fPIC --offload-arch=gfx950 -fsanitize=address -o $B/libmpo_asan.so $objs $B/api.o
-/opt/rocm/llvm/bin/clang++ -O1 -g -fsanitize=address -fno-omit-frame-pointer -std=c++17 tests/asan/abi_driver.cpp -o $B/abi_driver \
+$HIPCC -shared -fPIC --offload-arch=gfx950 -Xarch_host -fsanitize=address -o $B/libmpo_asan.so $objs $B/api.o
+/opt/rocm/llvm/bin/clang++ -O1 -g -fno-gpu-sanitize -fsanitize=address -fno-omit-frame-pointer -std=c++17 tests/asan/abi_driver.cpp -o $B/abi_driver \
     -L$B -lmpo_asan -Wl,-rpath,$(pwd)/$B
 # HIP's runtime keeps process-lifetime allocations: leak checking is off, every
 # other ASan check (overflows, use-after-free, double free) is on
