@@ -619,6 +619,22 @@ def cpu_baseline_search(search_out, concurrent=4):
                       f"({wall:.1f} s); the GP is not reached (n_initial_points = 10)"}
 
 
+def relaunch_distributed(n):
+    """``bench.py --gpus N`` started without torch.distributed.run: start
+    ``python -m torch.distributed.run --nproc-per-node N bench.py ...`` as a child
+    process (one rank per GPU; this process never touches the GPU), pass its
+    output through, return its exit code."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd, env={**os.environ, "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -636,6 +652,8 @@ def main():
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 traffic passes")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_distributed(args.gpus))
     ws, rank, local = dist_env()
     args.pmc = None
     if ws == 1 and not args.no_pmc and args.workload in ("ei", "train", "all") and shutil.which("rocprofv3"):
@@ -658,8 +676,6 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group(backend)
     dev = torch.device("cuda", local if ws > 1 else 0)
-    if ws == 1 and args.gpus != 1:
-        print(f"warning: --gpus {args.gpus} without torch.distributed.run; running 1 GPU", file=sys.stderr)
 
     res = bench_ei(args, torch, dist, ws, rank, dev) if args.workload in ("ei", "all") else None
     fit = None

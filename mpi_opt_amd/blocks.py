@@ -384,12 +384,25 @@ class DistributedEvaluator:
 class ShardedScorer:
     """Optimizer acquisition scoring split over the ranks of a
     :class:`DistributedEvaluator` (the candidate batch M/W per GPU, then a global
-    lowest-index top-k); plugs into ``Optimizer(scorer=...)``.  Not pickled."""
+    lowest-index top-k); plugs into ``Optimizer(scorer=...)``.  Not pickled.
 
-    def __init__(self, dist_eval):
+    Sharding costs a broadcast of the candidates and the observations, a device
+    GP factorisation on every rank and an all-gather; scoring costs ~1.3 ms per
+    million candidates on one GPU.  Below ``min_shard`` candidates (skopt's
+    ``n_points`` is 10 000) the request is scored on rank 0 alone, where the
+    fitted model is already resident -- the split pays only for large batches."""
+
+    def __init__(self, dist_eval, min_shard=1_000_000):
         self.dist_eval = dist_eval
+        self.min_shard = int(min_shard)
+        self.sharded_requests = 0
+        self.local_requests = 0
 
     def __call__(self, est, X, y_opt, acqs, xi, kappa, k):
+        if len(X) < self.min_shard or self.dist_eval.world == 1:
+            self.local_requests += 1
+            return {a: idx for a, (vals, idx) in _device_topk(est, X, y_opt, acqs, xi, kappa, k).items()}
+        self.sharded_requests += 1
         req = {"Xt": est.Xt, "y": est.y, "amp": est.amp, "ls": est.length_scale, "noise": est.noise,
                "cand": np.ascontiguousarray(X, dtype=np.float64), "y_opt": float(y_opt), "acqs": list(acqs),
                "xi": float(xi), "kappa": float(kappa), "k": int(k)}

@@ -443,4 +443,7 @@ def split_files(data_dir, pattern="*.h5", train_fraction=0.70):
     if not files:
         raise H5Error(f"no {pattern} files in {data_dir}")
     cut = int(len(files) * train_fraction)
+    if cut == 0 or cut == len(files):
+        raise H5Error(f"{len(files)} {pattern} file(s) in {data_dir}: the {train_fraction:.0%} file split leaves "
+                      f"{cut} for training and {len(files) - cut} for validation; both need at least one")
     return files[:cut], files[cut:]

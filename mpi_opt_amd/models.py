@@ -73,13 +73,14 @@ def test_mnist(**args):
 
 def test_densenet(nb_classes=3, img_dim=(150, 94, 5), depth=10, nb_dense_block=3, growth_rate=12,
                   dropout_rate=0.00, nb_filter=16, lr=1e-3):
-    """DenseNet spec (densenet.py:135-196 structure, mpiLAPI.py:197-201 entry)."""
-    assert (depth - 4) % 3 == 0, "Depth must be 3 N + 4"
-    return json.dumps({"class_name": "Model", "config": {
-        "name": "DenseNet", "arch": "densenet", "nb_classes": nb_classes, "img_dim": list(img_dim),
-        "depth": depth, "nb_dense_block": nb_dense_block, "growth_rate": growth_rate,
-        "dropout_rate": dropout_rate, "nb_filter": nb_filter, "weight_decay": 1e-4, "lr": lr}},
-        )
+    """mpiLAPI.py:197-201: ``DenseNet(...)`` (densenet.py:135-196), compiled with
+    ``Adam(lr)``, returned as ``to_json()`` -- the Keras functional-model JSON
+    (:func:`mpi_opt_amd.keras_json.densenet_json`).  ``to_json`` carries no
+    compile arguments, so ``lr`` does not reach the trainer (as in the reference)."""
+    from .keras_json import densenet_json
+
+    return densenet_json(nb_classes, img_dim, depth, nb_dense_block, growth_rate, nb_filter,
+                         dropout_rate=dropout_rate)
 
 
 class DenseNetSpec:
@@ -98,16 +99,17 @@ class DenseNetSpec:
 
 def spec_from_json(json_str, lr=1e-3, seed=0):
     """Ingest a Keras JSON into a device spec: the test_mnist Sequential topology
-    -> :class:`TrialSpec`; a DenseNet spec (``test_densenet`` / ``DenseNetModel``)
-    -> :class:`DenseNetSpec` (its own compiled lr, the searched dimension)."""
+    -> :class:`TrialSpec`; a functional DenseNet ``Model`` (densenet.py's graph,
+    from ``test_densenet`` / ``DenseNetModel.build`` or Keras itself) ->
+    :class:`DenseNetSpec` trained with the trainer's ``lr``."""
     d = json.loads(json_str)
-    cfg = d.get("config")
-    if d.get("class_name") == "Model" and isinstance(cfg, dict) and cfg.get("arch") == "densenet":
-        from .densenet import DenseNetArch
+    if d.get("class_name") in ("Model", "Functional"):
+        from .keras_json import densenet_arch_from_json
 
-        if float(cfg.get("dropout_rate", 0.0)) != 0.0:
-            raise ValueError("DenseNet population trains dropout_rate 0 (the reference grid, base_model.py:88)")
-        return DenseNetSpec(DenseNetArch.from_spec(cfg), cfg.get("lr", lr))
+        arch, wd = densenet_arch_from_json(d)
+        if abs(wd - 1e-4) > 1e-10:
+            raise ValueError(f"DenseNet population trains weight_decay 1e-4 (densenet.py:136), JSON has {wd}")
+        return DenseNetSpec(arch, lr)
     if d.get("class_name") != "Sequential":
         raise ValueError("population engine trains the test_mnist Sequential topology only")
     layers = d["config"]["layers"] if isinstance(d["config"], dict) else d["config"]
@@ -179,6 +181,8 @@ class DenseNetModel(BaseModel):
         self.input_shape = input_shape
 
     def build(self, params):
+        """base_model.py:62-73: the lr dimension (10**params[5]) is compiled into the
+        model, which ``to_json`` drops -- the JSON carries the architecture only."""
         return test_densenet(nb_classes=3, img_dim=self.input_shape, depth=int(params[0]),
                              nb_dense_block=int(params[1]), growth_rate=int(params[2]), dropout_rate=float(params[3]),
                              nb_filter=int(params[4]), lr=10.0 ** params[5])

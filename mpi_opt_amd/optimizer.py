@@ -169,6 +169,7 @@ class Optimizer:
             self.gains_ = np.zeros(3)
         self.Xi, self.yi, self.models = [], [], []
         self.cache_ = {}
+        self.trace = None       # a list here records each refit (theta, top-k, polish, pick) for parity tests
 
     # ---- ask -------------------------------------------------------------------
     def copy(self, random_state=None):
@@ -181,6 +182,7 @@ class Optimizer:
         opt._initial_samples = self._initial_samples
         if hasattr(self, "gains_"):
             opt.gains_ = np.copy(self.gains_)
+        opt.trace = [] if self.trace is not None else None
         if self.Xi:
             opt._tell(self.Xi, self.yi)
         return opt
@@ -204,6 +206,8 @@ class Optimizer:
             else:
                 lie = np.max(opt.yi) if opt.yi else 0.0
             opt._tell(x, lie)
+        if self.trace is not None:
+            self.batch_trace = opt.trace
         self.cache_ = {(n_points, strategy): X}
         return X
 
@@ -255,6 +259,8 @@ class Optimizer:
         kappa = self.acq_func_kwargs.get("kappa", 1.96)
         k = 1 if self.acq_optimizer == "sampling" else min(self.n_restarts_optimizer, X.shape[0])
         top = self._score_topk(est, X, y_opt, xi, kappa, k)
+        rec = {"theta": (est.amp, est.length_scale.copy(), est.noise), "top": dict(top), "polished": {}} \
+            if self.trace is not None else None
         self.next_xs_ = []
         if self.acq_optimizer == "lbfgs":
             runs = [(a, i) for a in self.cand_acq_funcs_ for i in top[a]]
@@ -269,14 +275,21 @@ class Optimizer:
                 cand_xs = np.array([r[0] for r in results])
                 cand_acqs = np.array([r[1] for r in results])
                 next_x = cand_xs[np.argmin(cand_acqs)]
+                if rec is not None:
+                    rec["polished"][acq] = (cand_xs, cand_acqs)
             self.next_xs_.append(np.clip(next_x, 0.0, 1.0))
         if self.acq_func == "gp_hedge":
             logits = np.array(self.gains_) - np.max(self.gains_)
             probs = np.exp(self.eta * logits)
             probs /= probs.sum()
-            next_x = self.next_xs_[int(np.argmax(self.rng.multinomial(1, probs)))]
+            pick = int(np.argmax(self.rng.multinomial(1, probs)))
         else:
-            next_x = self.next_xs_[0]
+            pick = 0
+        next_x = self.next_xs_[pick]
+        if rec is not None:
+            rec["pick"] = pick
+            rec["gains"] = np.copy(getattr(self, "gains_", np.zeros(0)))
+            self.trace.append(rec)
         self._next_x = self.space.inverse_transform(next_x.reshape(1, -1))[0]
 
     def _score_topk(self, est, X, y_opt, xi, kappa, k):
@@ -305,6 +318,15 @@ class Optimizer:
             x = self.ask()
             self.tell(x, func(x))
         return self._result()
+
+    def set_runtime(self, device=None, scorer=None):
+        """Re-attach the per-run state a checkpoint does not carry (the device of
+        this run and, when distributed, the candidate scorer); the models'
+        device posteriors are rebuilt lazily on ``device``."""
+        self.device = device
+        self.scorer = scorer
+        for m in self.models:
+            m.device, m._dev = device, None
 
     def __getstate__(self):
         d = _copy.copy(self.__dict__)

@@ -133,6 +133,8 @@ def run_search(args, x=None, y=None, log=print):
                              target_fom=args.target_objective, verbose=args.verbose, optimizer_kwargs=opt_kw)
     if args.previous_state:
         sched.load(args.previous_state)
+        # the pickle carries no device state: re-attach this run's device and scorer
+        sched.optimizer.set_runtime(device=dev, scorer=opt_kw.get("scorer"))
     t0 = time.perf_counter()
     state = sched.run(num_iterations=args.num_iterations)
     wall = time.perf_counter() - t0
@@ -149,7 +151,11 @@ def run_search(args, x=None, y=None, log=print):
         "optimizer_s": tm["ask_s"] + tm["tell_s"],
         "ask_s": tm["ask_s"], "tell_s": tm["tell_s"], "asks": tm["asks"], "tells": tm["tells"],
         "train_s": local_eval.train_s,
-        "trials_per_hour": 3600.0 * comm.trials_trained / wall if wall > 0 else None,
+        # headline on TOLD trials (the ones the optimizer saw); the in-flight tail the
+        # exit barrier trains (coordinator.py:98-101 never tells it) is reported apart
+        "trials_per_hour": 3600.0 * len(state.fom_list) / wall if wall > 0 else None,
+        "trained_per_hour": 3600.0 * comm.trials_trained / wall if wall > 0 else None,
+        "tail_trials": len(comm.tail),
         "best_fom": state.best_fom, "best_params": state.best_params,
     }
     log(f"search done: {report['trials_trained']} trials trained ({report['trials_told']} told) in "

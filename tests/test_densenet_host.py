@@ -96,8 +96,10 @@ def test_python_layer_geometry_matches_oracle_and_spec_ingestion():
         got = arch.layers()
         assert [{k: l[k] for k in ("kind", "H", "W", "cin", "cout")} for l in got] == \
                [{k: l[k] for k in ("kind", "H", "W", "cin", "cout")} for l in ref]
-    spec = spec_from_json(DenseNetModel(input_shape=(32, 32, 3)).build([10, 3, 12, 0.0, 16, -3]))
-    assert isinstance(spec, DenseNetSpec) and abs(spec.lr - 1e-3) < 1e-15
+    # the lr dimension (10**-2 here) is compiled into the Keras model and lost by to_json
+    # (base_model.py:67-73): the trainer's lr applies
+    spec = spec_from_json(DenseNetModel(input_shape=(32, 32, 3)).build([10, 3, 12, 0.0, 16, -2]), lr=1e-3)
+    assert isinstance(spec, DenseNetSpec) and spec.lr == 1e-3
     assert spec.arch.key() == ((32, 32, 3), 3, 10, 3, 12, 16)
     assert spec.flops_per_sample_train() == od.flops_per_sample_train(od.arch_layers(img_dim=(32, 32, 3),
                                                                                      nb_classes=3))

@@ -102,13 +102,23 @@ def _opt_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     ev = DistributedEvaluator(_evaluator())
     if rank == 0:
-        opt = _opt(ShardedScorer(ev))
+        import pickle
+
+        opt = _opt(ShardedScorer(ev, min_shard=0))      # force the split (default: >= 1M candidates only)
         X, y = _told_points()
         opt.tell(X, y)
         nxt = opt.ask()
         batch = opt.ask(3)
+        # resume from a checkpoint (search --previous-result): the scorer is re-attached
+        o2 = pickle.loads(pickle.dumps(opt))
+        assert o2.scorer is None
+        o2.set_runtime(device="cuda:0", scorer=opt.scorer)
+        before = opt.scorer.sharded_requests
+        o2.tell(list(batch[0]), 0.5)
+        resumed = o2.ask()
+        assert opt.scorer.sharded_requests > before
         ev.shutdown()
-        q.put((list(nxt), [list(b) for b in batch]))
+        q.put((list(nxt), [list(b) for b in batch], list(resumed)))
     else:
         ev.serve()
         q.put("served")
@@ -136,4 +146,7 @@ def test_sharded_optimizer_scoring_matches_single_gpu():
     X, y = _told_points()
     opt.tell(X, y)
     assert dist_out[0] == list(opt.ask())
-    assert dist_out[1] == [list(b) for b in opt.ask(3)]
+    batch = opt.ask(3)
+    assert dist_out[1] == [list(b) for b in batch]
+    opt.tell(list(batch[0]), 0.5)
+    assert dist_out[2] == list(opt.ask())

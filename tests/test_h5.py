@@ -70,3 +70,15 @@ def test_kfold_holdout_split():
     # synthetic data keeps option3's 70 % cut
     tr, va = kfold_split(100, 1, 0)
     assert len(tr) == 70 and len(va) == 30
+
+
+def test_split_files_rejects_an_empty_side(tmp_path):
+    """One file: 70 % of it is no training file -- a clear H5Error, not a numpy
+    concatenate failure deep inside load_xy."""
+    import shutil
+
+    from mpi_opt_amd.h5 import H5Error, split_files
+
+    shutil.copy(os.path.join(H5DIR, "mnist_a.h5"), tmp_path / "mnist_a.h5")
+    with pytest.raises(H5Error, match="both need at least one"):
+        split_files(str(tmp_path))

@@ -41,7 +41,9 @@ def test_unsupported_topologies_raise():
 def test_base_models_interface():
     d = M.DenseNetModel()
     assert d.get_name() == "DenseNet" and len(d.get_parameter_grid()) == 6
-    assert json.loads(d.build([10, 3, 12, 0.0, 16, -3]))["config"]["depth"] == 10
+    js = json.loads(d.build([10, 3, 12, 0.0, 16, -3]))     # Keras functional Model JSON (to_json)
+    assert js["class_name"] == "Model" and js["config"]["name"] == "DenseNet"
+    assert M.spec_from_json(json.dumps(js)).arch.depth == 10
     with pytest.raises(NotImplementedError):
         M.BaseModel().build([])
 
