@@ -594,6 +594,120 @@ def bench_search(args, torch, dist, ws, rank, dev):
     return out
 
 
+SEARCH3_ARGV = ["--world-size", "129", "--block-size", "2", "--n-fold", "5", "--num-iterations", "80",
+                "--epochs", "1", "--n-samples", "60000"]
+
+
+def bench_search_gp(args, torch, dist, ws, rank, dev):
+    """BASELINE configs[3]'s layout with the GP in the loop (the north_star search):
+    64 blocks (``-n 129 --block-size 2``), 5-fold CV, cl_min batches of
+    ``--num-iterations``.  Reduced to fit a bench run: 80 iterations instead of
+    256 and 1 epoch instead of 10 (stated in ``config.workload``).  The first 64
+    trials train as one population and are told one at a time; each of the
+    following launches pays the reference's tell + ``ask(num_iterations)`` (a
+    fresh cl_min batch after every fit, coordinator.py:46-50, 73) -- so the GP
+    refits (one per tell and per lie) run between the two populations.  Then,
+    on its own: ``Optimizer.ask(256)`` after 256 tells (the rank-0 term of the
+    full 256-trial search while the GPUs train)."""
+    import tempfile
+
+    from mpi_opt_amd import optimizer as OPT
+    from mpi_opt_amd import search
+    from mpi_opt_amd.models import mnist_space
+
+    argv = SEARCH3_ARGV + list(args.search3_args or [])
+    a = search.make_parser().parse_args(argv)
+    with tempfile.TemporaryDirectory() as tmp:
+        a.checkpoint = os.path.join(tmp, "coordinator.pkl")
+        if ws > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        rep = search.run_search(a, log=lambda *m: print(*m, file=sys.stderr, flush=True))
+        torch.cuda.synchronize(dev)
+        if ws > 1:
+            dist.barrier()
+        wall = time.perf_counter() - t0
+    if rank != 0:
+        return None
+    gp = rep["gp"]
+    opt_s = rep["ask_s"] + rep["tell_s"]
+    out = {"metric": "MNIST-CNN trials/hour, measured search with the GP in the loop (BASELINE configs[3] layout)",
+           "value": rep["trials_told"] * 3600.0 / wall, "unit": "trials/hour (told)", "n_gpus": ws,
+           "wall_s": wall, "scaling": "strong", "dtype": "f32 training, f64 GP",
+           "config": {"workload": "option3 search " + " ".join(argv) + " (configs[3]: -n 129 --block-size 2 "
+                                  "--n-fold 5; reduced to 80 iterations and 1 epoch for the bench)",
+                      "num_blocks": rep["num_blocks"], "populations": rep["populations"],
+                      "parallelism": f"(trial, fold) units LPT-sharded over {ws} GPU(s); GP on rank 0"},
+           "trials_told": rep["trials_told"], "trials_trained": rep["trials_trained"],
+           "tail_trials": rep["tail_trials"],
+           "split_s": {"optimizer_ask": rep["ask_s"], "optimizer_tell": rep["tell_s"], "training": rep["train_s"],
+                       "other": wall - opt_s - rep["train_s"]},
+           "optimizer_share": opt_s / wall, "asks": rep["asks"], "tells": rep["tells"],
+           "gp_refits": gp["refits"], "gp_refit_mean_n": gp["n_sum"] / max(1, gp["refits"]), "gp_refit_max_n": gp["n_max"],
+           "ms_per_refit": 1e3 * gp["refit_s"] / max(1, gp["refits"]),
+           "ms_per_proposal": 1e3 * gp["propose_s"] / max(1, gp["refits"]),
+           "best_fom": rep["best_fom"]}
+    # the rank-0 Amdahl term of the full search: ask(256) after 256 tells
+    rng = np.random.RandomState(256)
+    opt = OPT.Optimizer(mnist_space(), random_state=13579, device=dev)
+    pts = opt.space.rvs(n_samples=256, random_state=rng)
+    ys = [float(((p[0] - 30) / 40) ** 2 + ((p[3] - 120) / 150) ** 2 + (p[4] - 0.3) ** 2 + 0.1 * rng.rand())
+          for p in pts]
+    opt.tell(pts[:-1], ys[:-1], fit=False)
+    opt.tell(pts[-1], ys[-1])
+    OPT.reset_stats()
+    t0 = time.perf_counter()
+    batch = opt.ask(args.ask_n)
+    t_ask = time.perf_counter() - t0
+    st = dict(OPT.STATS)
+    out["ask256"] = {"n_points": args.ask_n, "told": 256, "seconds": t_ask, "refits": st["refits"],
+                     "refit_n_range": [256, st["n_max"]], "ms_per_refit": 1e3 * st["refit_s"] / st["refits"],
+                     "ms_per_proposal": 1e3 * st["propose_s"] / st["refits"], "distinct_points": len({tuple(b) for b in batch})}
+    out["_told_state"] = (pts, ys)
+    return out
+
+
+def _oracle_refit_seconds(pts, ys, n, reps=2):
+    """Seconds per skopt refit + proposal on the host (oracle: sklearn fit, einsum
+    posterior over 10 000 candidates, scipy L-BFGS-B polish) at n observations:
+    the copy refit + cl_min lies of ask(reps - 1)."""
+    from oracle.skopt_optimizer import SkoptOracle
+
+    from mpi_opt_amd.models import mnist_space
+
+    ora = SkoptOracle(mnist_space(), random_state=13579)
+    ora.Xi, ora.yi = [list(p) for p in pts[:n]], list(ys[:n])
+    ora._n_initial_points -= n
+    t0 = time.perf_counter()
+    ora.ask(reps - 1)
+    return (time.perf_counter() - t0) / reps
+
+
+def cpu_baseline_search_gp(out, cpu_train_trial_s):
+    """The same search on the host the way the reference runs it, from bounded
+    samples: the GP side is the oracle's skopt refit + proposal timed at the run's
+    mean observation count and multiplied by the run's refit count; training is
+    the torch-CPU restatement's per-trial time (the train leg's sample, 4 trials at
+    once on every core) for the trials the run trained, at its epochs and folds."""
+    pts, ys = out.pop("_told_state")
+    n_mean = int(round(out["gp_refit_mean_n"]))
+    s_refit = _oracle_refit_seconds(pts, ys, n_mean)
+    s_refit256 = _oracle_refit_seconds(pts, ys, 256)
+    epochs = 1
+    t_train = out["trials_trained"] * cpu_train_trial_s * epochs / 10.0
+    t_gp = out["gp_refits"] * s_refit
+    t = t_gp + t_train
+    return {"value": out["trials_told"] * 3600.0 / t, "unit": "trials/hour (told)", "cores": host_cores(),
+            "kind": "port", "seconds_gp": t_gp, "seconds_training": t_train, "s_per_refit_at_mean_n": s_refit,
+            "s_per_refit_n256": s_refit256, "ask256_seconds_est": s_refit256 * (out["ask256"]["refits"]),
+            "sample": f"GP: oracle skopt refit + proposal (sklearn GaussianProcessRegressor.fit, einsum posterior, "
+                      f"L-BFGS-B polish, 10 000 candidates) timed over 2 refits at n={n_mean} ({s_refit:.2f} s each) "
+                      f"and n=256 ({s_refit256:.2f} s) x the run's {out['gp_refits']} refits; training: torch-CPU "
+                      f"fp32 per-trial time of the train leg's sample ({cpu_train_trial_s:.0f} s of all cores per "
+                      f"10-epoch 5-fold trial, 4 at once) x {out['trials_trained']} trials x {epochs}/10 epochs"}
+
+
 def cpu_baseline_search(search_out, concurrent=4):
     """The same trials on the host the way the reference runs them: torch-CPU fp32
     single-trial training, ``num_blocks`` trials at once (cores // num_blocks
@@ -640,9 +754,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="all", choices=["ei", "fit", "train", "densenet", "search", "all"])
+    ap.add_argument("--workload", default="all",
+                    choices=["ei", "fit", "train", "densenet", "search", "search3", "all"])
     ap.add_argument("--search-args", nargs="*", default=None,
                     help="extra search CLI flags appended to configs[0]'s (e.g. --n-samples 6000)")
+    ap.add_argument("--search3-args", nargs="*", default=None,
+                    help="extra search CLI flags appended to the configs[3]-layout search's")
+    ap.add_argument("--ask-n", type=int, default=256, help="cl_min batch size of the standalone ask after 256 tells")
     ap.add_argument("--candidates", type=int, default=1_000_000)
     ap.add_argument("--train-trials", type=int, default=64)
     ap.add_argument("--train-steps", type=int, default=5)
@@ -684,6 +802,7 @@ def main():
     train = bench_train(args, torch, dist, ws, rank, dev) if args.workload in ("train", "all") else None
     dn = bench_densenet(args, torch, dist, ws, rank, dev) if args.workload in ("densenet", "all") else None
     srch = bench_search(args, torch, dist, ws, rank, dev) if args.workload in ("search", "all") else None
+    srch3 = bench_search_gp(args, torch, dist, ws, rank, dev) if args.workload in ("search3", "all") else None
     if rank == 0:
         cpu = ws == 1 and not args.no_cpu_baseline
         if srch is not None:
@@ -696,6 +815,13 @@ def main():
         if train is not None:
             trials = train.pop("_trials")
             train["cpu_baseline"] = cpu_baseline_train(trials) if cpu else None
+        if srch3 is not None:
+            if cpu:
+                tcpu = (train or {}).get("cpu_baseline") or cpu_baseline_train(sample_trials(32, seed=13579))
+                srch3["cpu_baseline"] = cpu_baseline_search_gp(srch3, 3600.0 / tcpu["value"])
+            else:
+                srch3.pop("_told_state")
+                srch3["cpu_baseline"] = None
         if dn is not None:
             dn["cpu_baseline"] = cpu_baseline_densenet() if cpu else None
         if res is not None:
@@ -708,8 +834,10 @@ def main():
                 res["densenet"] = dn
             if srch is not None:
                 res["search"] = srch
+            if srch3 is not None:
+                res["search_gp"] = srch3
         else:
-            res = next(r for r in (train, dn, srch, fit) if r is not None)
+            res = next(r for r in (train, dn, srch, srch3, fit) if r is not None)
         print(json.dumps(res), flush=True)
     if ws > 1:
         dist.barrier()

@@ -102,6 +102,112 @@ class DeviceLML:
                     h[cap * (k + 1):].view(np.int32)[:B].copy())
 
 
+# scipy's L-BFGS-B defaults as ``minimize(method="L-BFGS-B")`` and ``fmin_l_bfgs_b`` pass them
+MINIMIZE_FTOL = 2.2204460492503131e-09
+FMIN_FTOL = 1e7 * np.finfo(float).eps      # fmin_l_bfgs_b: factr=1e7 -> ftol = factr * eps
+
+
+def _setulb():
+    try:
+        from scipy.optimize import _lbfgsb
+        return _lbfgsb.setulb if "ln_task" in (_lbfgsb.setulb.__doc__ or "") else None
+    except ImportError:      # pragma: no cover -- another scipy: the threaded driver below is used
+        return None
+
+
+class _LbfgsbRun:
+    """One L-BFGS-B minimisation in reverse communication, step for step what
+    scipy 1.15's ``_minimize_lbfgsb`` does around ``_lbfgsb.setulb`` (with its
+    ``ScalarFunction`` cache: the objective is evaluated at the clipped x0 first,
+    and an FG request at an unchanged x reuses that value)."""
+
+    def __init__(self, x0, bounds, ftol, gtol, maxiter, maxfun, maxcor=10, maxls=20):
+        lo, hi = np.asarray(bounds, dtype=np.float64).T
+        self.x = np.clip(np.asarray(x0, dtype=np.float64).ravel(), lo, hi).astype(np.float64)
+        n = self.x.size
+        self.m, self.maxls, self.maxiter, self.maxfun = maxcor, maxls, maxiter, maxfun
+        self.factr, self.pgtol = ftol / np.finfo(float).eps, gtol
+        self.low, self.up = lo.copy(), hi.copy()
+        self.nbd = np.full(n, 2, dtype=np.int32)          # both bounds finite (every bound here is)
+        self.f = np.array(0.0, dtype=np.int32)
+        self.g = np.zeros((n,), dtype=np.int32)
+        self.wa = np.zeros(2 * maxcor * n + 5 * n + 11 * maxcor * maxcor + 8 * maxcor, np.float64)
+        self.iwa = np.zeros(3 * n, dtype=np.int32)
+        self.task = np.zeros(2, dtype=np.int32)
+        self.ln_task = np.zeros(2, dtype=np.int32)
+        self.lsave = np.zeros(4, dtype=np.int32)
+        self.isave = np.zeros(44, dtype=np.int32)
+        self.dsave = np.zeros(29, dtype=np.float64)
+        self.nit = 0
+        self.nfev = 0
+        self.sf_x = None          # ScalarFunction's cached point and values
+        self.sf_f = self.sf_g = None
+        self.started = False
+        self.done = False
+
+    def request(self):
+        """The first evaluation (ScalarFunction at x0): x to evaluate."""
+        return self.x.copy()
+
+    def deliver(self, x, f, g):
+        """f, g at x: into the ScalarFunction cache and, once setulb has asked for
+        them (every delivery after the first), into the run."""
+        self.sf_x, self.sf_f, self.sf_g = x, f, g
+        self.nfev += 1
+        if self.started:
+            self.f, self.g = f, g
+        self.started = True
+
+    def advance(self, setulb):
+        """Run setulb until it needs f, g at a new point (returns that point) or
+        stops (returns None)."""
+        while True:
+            self.g = self.g.astype(np.float64)
+            setulb(self.m, self.x, self.low, self.up, self.nbd, self.f, self.g, self.factr, self.pgtol, self.wa,
+                   self.iwa, self.task, self.lsave, self.isave, self.dsave, self.maxls, self.ln_task)
+            if self.task[0] == 3:
+                if np.array_equal(self.x, self.sf_x):
+                    self.f, self.g = self.sf_f, self.sf_g
+                    continue
+                return self.x.copy()
+            if self.task[0] == 1:
+                self.nit += 1
+                if self.nit >= self.maxiter:
+                    self.task[0], self.task[1] = 5, 504
+                elif self.nfev > self.maxfun:
+                    self.task[0], self.task[1] = 5, 502
+                continue
+            self.done = True
+            return None
+
+
+def lbfgsb_batched(evaluate, starts, bounds, ftol=MINIMIZE_FTOL, gtol=1e-5, maxiter=15000, maxfun=15000):
+    """Independent L-BFGS-B runs from ``starts`` whose objective evaluations are
+    batched: every round calls ``evaluate(X[B, n], ids) -> (f[B], g[B, n])`` once
+    with the point each live run needs.  One thread drives every run through
+    scipy's reverse-communication ``setulb`` exactly as ``scipy.optimize.minimize
+    (method="L-BFGS-B", jac=True)`` (``ftol=MINIMIZE_FTOL``) or ``fmin_l_bfgs_b``
+    (``ftol=FMIN_FTOL``) would, so each run's iterates are those of a sequential
+    scipy call.  Returns ([(x, f)] per run, number of rounds)."""
+    setulb = _setulb()
+    runs = [_LbfgsbRun(x0, bounds, ftol, gtol, maxiter, maxfun) for x0 in starts]
+    want = {i: r.request() for i, r in enumerate(runs)}
+    rounds = 0
+    while want:
+        ids = sorted(want)
+        f, g = evaluate(np.stack([want[i] for i in ids]), ids)
+        rounds += 1
+        for k, i in enumerate(ids):
+            runs[i].deliver(want[i], float(f[k]), np.array(g[k], dtype=np.float64))
+        nxt = {}
+        for i in ids:
+            x = runs[i].advance(setulb)
+            if x is not None:
+                nxt[i] = x
+        want = nxt
+    return [(r.x, float(r.f)) for r in runs], rounds
+
+
 class _Lockstep:
     """Collects one theta from every live optimiser thread, evaluates them in one
     batch, hands each thread its own result."""
@@ -173,6 +279,13 @@ def lockstep_lbfgsb(evaluate, d, random_state=None, n_restarts_optimizer=2, retu
     for _ in range(n_restarts_optimizer):
         starts.append(rng.uniform(bounds[:, 0], bounds[:, 1]))
 
+    if _setulb() is not None:                # one thread, setulb in reverse communication
+        def neg(thetas, ids):
+            v, g = evaluate(thetas)[:2]
+            return -np.asarray(v), -np.asarray(g)
+        optima, launches = lbfgsb_batched(neg, starts, bounds)
+        return _pick(optima, starts, launches, d, return_details)
+
     step = _Lockstep(evaluate, len(starts))
     optima = [None] * len(starts)
     errors = []
@@ -196,10 +309,14 @@ def lockstep_lbfgsb(evaluate, d, random_state=None, n_restarts_optimizer=2, retu
         t.join()
     if errors:
         raise errors[0]
+    return _pick(optima, starts, step.launches, d, return_details)
+
+
+def _pick(optima, starts, launches, d, return_details):
+    """sklearn: the optimum with the lowest -LML, first on ties (_gpr.py:331-333)."""
     best = int(np.argmin([o[1] for o in optima]))
     theta = np.exp(optima[best][0])
     out = (float(theta[0]), theta[1:d + 1].copy(), float(theta[d + 1]))
     if return_details:
-        return out, {"optima": optima, "starts": starts, "launches": step.launches,
-                     "lml": -optima[best][1]}
+        return out, {"optima": optima, "starts": starts, "launches": launches, "lml": -optima[best][1]}
     return out

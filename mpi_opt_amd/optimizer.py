@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import copy as _copy
 import threading
+import time
 
 import numpy as np
 from scipy.optimize import fmin_l_bfgs_b
@@ -82,12 +83,16 @@ def polish_lockstep(model, starts, acqs, y_opt, xi, kappa, bounds, maxiter=20):
     acquisition ``acqs[w]``.  The runs are independent; they step in lockstep (one
     thread each, gp_fit._Lockstep) so that each round of evaluations is one
     ``mpo_gp_acq_grad`` launch over all live runs.  Returns [(x, f)] per run."""
-    from .gp_fit import _Lockstep
+    from .gp_fit import FMIN_FTOL, _Lockstep, _setulb, lbfgsb_batched
 
     codes = np.array([_lib.ACQ_FLAGS[a] for a in acqs], dtype=np.int32)
 
     def evaluate(X, ids):
         return model.dev.acq_grad(X, codes[ids], y_opt, xi, kappa)
+
+    if _setulb() is not None:        # one thread drives every run (setulb reverse communication)
+        out, _ = lbfgsb_batched(evaluate, starts, bounds, ftol=FMIN_FTOL, maxiter=maxiter)
+        return out
 
     step = _Lockstep(evaluate, len(starts), pass_ids=True)
     out = [None] * len(starts)
@@ -111,6 +116,15 @@ def polish_lockstep(model, starts, acqs, y_opt, xi, kappa, bounds, maxiter=20):
     if errors:
         raise errors[0]
     return out
+
+
+#: process-wide accounts of the GP work (bench / search reports): refits, their
+#: observation counts and the seconds spent refitting vs proposing
+STATS = {"refits": 0, "n_sum": 0, "n_max": 0, "refit_s": 0.0, "propose_s": 0.0}
+
+
+def reset_stats():
+    STATS.update(refits=0, n_sum=0, n_max=0, refit_s=0.0, propose_s=0.0)
 
 
 class OptimizeResult(dict):
@@ -244,7 +258,13 @@ class Optimizer:
     def _fit_and_propose(self):
         Xt = self.space.transform(self.Xi)
         y = np.asarray(self.yi, dtype=float)
+        t0 = time.perf_counter()
         amp, ls, noise = fit_gp_hyperparameters(Xt, y, random_state=self._gp_seed, device=self.device)
+        t1 = time.perf_counter()
+        STATS["refits"] += 1
+        STATS["n_sum"] += len(y)
+        STATS["n_max"] = max(STATS["n_max"], len(y))
+        STATS["refit_s"] += t1 - t0
         est = GPModel(Xt, y, amp, ls, noise, device=self.device)
         if hasattr(self, "next_xs_") and self.acq_func == "gp_hedge":
             self.gains_ -= est.predict_mean(np.vstack(self.next_xs_))
@@ -291,6 +311,7 @@ class Optimizer:
             rec["gains"] = np.copy(getattr(self, "gains_", np.zeros(0)))
             self.trace.append(rec)
         self._next_x = self.space.inverse_transform(next_x.reshape(1, -1))[0]
+        STATS["propose_s"] += time.perf_counter() - t1
 
     def _score_topk(self, est, X, y_opt, xi, kappa, k):
         """skopt's ``np.argsort(values)[:k]`` per acquisition (lowest index first on

@@ -131,6 +131,9 @@ def run_search(args, x=None, y=None, log=print):
         opt_kw["scorer"] = ShardedScorer(evaluator)       # candidates split M/W over the GPUs
     sched = AskTellScheduler(comm, num_blocks, provider.parameters, checkpoint=args.checkpoint,
                              target_fom=args.target_objective, verbose=args.verbose, optimizer_kwargs=opt_kw)
+    from . import optimizer as _opt_mod
+
+    _opt_mod.reset_stats()
     if args.previous_state:
         sched.load(args.previous_state)
         # the pickle carries no device state: re-attach this run's device and scorer
@@ -157,6 +160,7 @@ def run_search(args, x=None, y=None, log=print):
         "trained_per_hour": 3600.0 * comm.trials_trained / wall if wall > 0 else None,
         "tail_trials": len(comm.tail),
         "best_fom": state.best_fom, "best_params": state.best_params,
+        "gp": dict(_opt_mod.STATS),     # refits (tell + every cl_min lie), their n, refit / proposal seconds
     }
     log(f"search done: {report['trials_trained']} trials trained ({report['trials_told']} told) in "
         f"{wall:.1f} s; optimizer {report['optimizer_s']:.2f} s, training {report['train_s']:.1f} s; "

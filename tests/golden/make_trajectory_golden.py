@@ -131,11 +131,31 @@ def make_densenet():
             "dn_mm1": np.array(mm)}
 
 
+def make_densenet32():
+    """configs[4]: the sampled members of the 32-member population (init seed
+    500 + member, per-member sample order), 10 steps each on the fp64 oracle."""
+    from mpi_opt_amd.densenet import he_uniform_init
+
+    x, y, _ = T.dn_data()
+    order = T.dn32_order()
+    layers = OD.arch_layers()
+    losses = []
+    for i in T.DN32_PICKS:
+        p, s = he_uniform_init(layers, 500 + i)
+        o = OD.DenseNetOracle(layers, {k: v.astype(np.float64) for k, v in p.items()},
+                              {k: v.astype(np.float64) for k, v in s.items()}, lr=float(T.DN32_LRS[i]))
+        ls = [o.train_step(x[order[i, st * T.BATCH:(st + 1) * T.BATCH]], y[order[i, st * T.BATCH:(st + 1) * T.BATCH]])
+              for st in range(T.DN32_STEPS)]
+        losses.append(ls)
+        print("densenet32 member", i, "lr", T.DN32_LRS[i], ls[0], "->", ls[-1], flush=True)
+    return {"dn32_train_loss": np.array(losses)}
+
+
 if __name__ == "__main__":
-    want = sys.argv[1:] or ["pop", "epoch", "epoch_fp32", "densenet"]
+    want = sys.argv[1:] or ["pop", "epoch", "epoch_fp32", "densenet", "densenet32"]
     data = dict(np.load(OUT)) if os.path.exists(OUT) else {}
     for w in want:
         data.update({"pop": make_pop, "epoch": make_epoch, "epoch_fp32": make_epoch_fp32,
-                     "densenet": make_densenet}[w]())
+                     "densenet": make_densenet, "densenet32": make_densenet32}[w]())
         np.savez(OUT, **data)
     print("wrote", OUT, sorted(data))

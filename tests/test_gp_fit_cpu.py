@@ -52,3 +52,47 @@ def test_lockstep_propagates_objective_errors():
 
     with pytest.raises(RuntimeError, match="device failure"):
         lockstep_lbfgsb(bad, 3, random_state=0)
+
+
+def test_batched_reverse_communication_lbfgsb_is_scipys_path():
+    """lbfgsb_batched (one thread, scipy's setulb in reverse communication, the
+    runs' evaluations batched per round) reproduces scipy.optimize.minimize
+    (L-BFGS-B, the GP refit) and fmin_l_bfgs_b(maxiter=20) (the acquisition
+    polish) bit for bit, run by run."""
+    import scipy.optimize
+    from scipy.optimize import fmin_l_bfgs_b
+
+    from mpi_opt_amd import gp_fit as GF
+
+    assert GF._setulb() is not None
+    X, y = O.synthetic_problem(40, 5, seed=3)
+    d = 5
+    bounds = GF.theta_bounds(d)
+    rng = np.random.RandomState(0)
+    starts = [np.zeros(d + 2)] + [rng.uniform(bounds[:, 0], bounds[:, 1]) for _ in range(2)]
+
+    def ev(T, ids):
+        out = [O.lml_and_grad(X, y, t) for t in T]
+        return np.array([-v for v, _ in out]), np.array([-g for _, g in out])
+
+    got, rounds = GF.lbfgsb_batched(ev, starts, bounds)
+    nfev = []
+    for s0, (x, f) in zip(starts, got):
+        r = scipy.optimize.minimize(lambda t: tuple(-np.asarray(v) for v in O.lml_and_grad(X, y, t)), s0,
+                                    method="L-BFGS-B", jac=True, bounds=bounds)
+        assert np.array_equal(r.x, x) and r.fun == f
+        nfev.append(r.nfev)
+    assert rounds == max(nfev)
+
+    st = O.gp_from_theta(X, y, 1.3, np.full(d, 0.5), 1e-3)
+    ps = [rng.uniform(size=d) for _ in range(5)]
+
+    def ev2(P, ids):
+        out = [O.acquisition_and_grad(st, p, float(y.min()), "EI") for p in P]
+        return np.array([v for v, _ in out]), np.array([g for _, g in out])
+
+    got, _ = GF.lbfgsb_batched(ev2, ps, [(0.0, 1.0)] * d, ftol=GF.FMIN_FTOL, maxiter=20)
+    for p0, (x, f) in zip(ps, got):
+        xr, fr, _ = fmin_l_bfgs_b(lambda v: O.acquisition_and_grad(st, v, float(y.min()), "EI"), p0,
+                                  bounds=[(0.0, 1.0)] * d, approx_grad=False, maxiter=20)
+        assert np.array_equal(xr, x) and fr == f

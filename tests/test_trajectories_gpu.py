@@ -134,3 +134,27 @@ def test_densenet_batch100_trajectory():
     assert np.abs(vc - G["dn_val_correct"]).max() <= 1   # an argmax near-tie may flip in f32
     for i in range(len(T.DN_LRS)):
         np.testing.assert_allclose(pop.get_state(i)["mm1"], G["dn_mm1"][i], rtol=1e-3, atol=1e-5)
+
+
+def test_densenet_32_member_population_configs4():
+    """BASELINE configs[4]: the whole 32-member population (lr 10**U(-5, 1) as the
+    bench draws it) trains together; 4 sampled members spanning the lr range
+    follow their fp64 oracle trajectories for 10 steps within 1e-3 relative."""
+    from mpi_opt_amd.densenet import DenseNetArch, DenseNetPopulation, he_uniform_init
+    from oracle import densenet as OD
+
+    layers = OD.arch_layers()
+    init = [he_uniform_init(layers, 500 + i) for i in range(len(T.DN32_LRS))]
+    pop = DenseNetPopulation(DenseNetArch(), list(T.DN32_LRS), batch=T.BATCH, init=init)
+    x, y, _ = T.dn_data()
+    order = T.dn32_order()
+    xd, yd, od_ = (torch.from_numpy(a).cuda() for a in (x, y, order))
+    got = np.array([pop.train_step(xd, yd, od_, st * T.BATCH).cpu().numpy() for st in range(T.DN32_STEPS)]).T
+    ref = G["dn32_train_loss"]
+    picks = got[T.DN32_PICKS]
+    rel = np.abs(picks - ref) / np.abs(ref)
+    fmt = lambda a: np.array2string(np.asarray(a), formatter={"float_kind": lambda v: "%.2e" % v})  # noqa: E731
+    print("DenseNet 32-member population, members", T.DN32_PICKS, "lr", fmt(T.DN32_LRS[T.DN32_PICKS]),
+          "10 steps: max rel train-loss drift", fmt(rel.max(1)))
+    assert np.isfinite(got[:, 0]).all()
+    assert rel.max() < 1e-3

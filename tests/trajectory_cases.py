@@ -101,6 +101,20 @@ def dn_data():
     return x, y, order
 
 
+# ---------------------------------------------------------------------------
+# DenseNet, BASELINE configs[4]: a 32-member population (the bench's lr draw
+# 10**U(-5, 1)), 4 sampled members checked for 10 steps
+# ---------------------------------------------------------------------------
+DN32_LRS = 10.0 ** np.random.RandomState(2024).uniform(-5, 1, size=32)
+DN32_STEPS = 10
+DN32_PICKS = [int(np.argmin(np.abs(np.log10(DN32_LRS) - np.log10(t)))) for t in (1e-5, 2e-3, 4e-2, 0.4)]
+
+
+def dn32_order():
+    rng = np.random.RandomState(24)
+    return np.stack([rng.permutation(DN_SAMPLES).astype(np.int32) for _ in DN32_LRS])
+
+
 def glorot_init(F, k, p, dense, seed):
     """Same draw as mpi_opt_amd.population.glorot_uniform_init (Keras order)."""
     H2 = 28 - 2 * (k - 1)
