@@ -594,14 +594,14 @@ def bench_search(args, torch, dist, ws, rank, dev):
     return out
 
 
-SEARCH3_ARGV = ["--world-size", "129", "--block-size", "2", "--n-fold", "5", "--num-iterations", "80",
+SEARCH3_ARGV = ["--world-size", "129", "--block-size", "2", "--n-fold", "5", "--num-iterations", "128",
                 "--epochs", "1", "--n-samples", "60000"]
 
 
 def bench_search_gp(args, torch, dist, ws, rank, dev):
     """BASELINE configs[3]'s layout with the GP in the loop (the north_star search):
     64 blocks (``-n 129 --block-size 2``), 5-fold CV, cl_min batches of
-    ``--num-iterations``.  Reduced to fit a bench run: 80 iterations instead of
+    ``--num-iterations``.  Reduced to fit a bench run: 128 iterations instead of
     256 and 1 epoch instead of 10 (stated in ``config.workload``).  The first 64
     trials train as one population and are told one at a time; each of the
     following launches pays the reference's tell + ``ask(num_iterations)`` (a
@@ -636,7 +636,7 @@ def bench_search_gp(args, torch, dist, ws, rank, dev):
            "value": rep["trials_told"] * 3600.0 / wall, "unit": "trials/hour (told)", "n_gpus": ws,
            "wall_s": wall, "scaling": "strong", "dtype": "f32 training, f64 GP",
            "config": {"workload": "option3 search " + " ".join(argv) + " (configs[3]: -n 129 --block-size 2 "
-                                  "--n-fold 5; reduced to 80 iterations and 1 epoch for the bench)",
+                                  "--n-fold 5; reduced to 128 iterations and 1 epoch for the bench)",
                       "num_blocks": rep["num_blocks"], "populations": rep["populations"],
                       "parallelism": f"(trial, fold) units LPT-sharded over {ws} GPU(s); GP on rank 0"},
            "trials_told": rep["trials_told"], "trials_trained": rep["trials_trained"],
@@ -647,6 +647,7 @@ def bench_search_gp(args, torch, dist, ws, rank, dev):
            "gp_refits": gp["refits"], "gp_refit_mean_n": gp["n_sum"] / max(1, gp["refits"]), "gp_refit_max_n": gp["n_max"],
            "ms_per_refit": 1e3 * gp["refit_s"] / max(1, gp["refits"]),
            "ms_per_proposal": 1e3 * gp["propose_s"] / max(1, gp["refits"]),
+           "ms_per_proposal_split": {k: 1e3 * gp[k + "_s"] / max(1, gp["refits"]) for k in ("prepare", "score", "polish")},
            "best_fom": rep["best_fom"]}
     # the rank-0 Amdahl term of the full search: ask(256) after 256 tells
     rng = np.random.RandomState(256)
@@ -663,7 +664,9 @@ def bench_search_gp(args, torch, dist, ws, rank, dev):
     st = dict(OPT.STATS)
     out["ask256"] = {"n_points": args.ask_n, "told": 256, "seconds": t_ask, "refits": st["refits"],
                      "refit_n_range": [256, st["n_max"]], "ms_per_refit": 1e3 * st["refit_s"] / st["refits"],
-                     "ms_per_proposal": 1e3 * st["propose_s"] / st["refits"], "distinct_points": len({tuple(b) for b in batch})}
+                     "ms_per_proposal": 1e3 * st["propose_s"] / st["refits"],
+                     "ms_per_proposal_split": {k: 1e3 * st[k + "_s"] / st["refits"] for k in ("prepare", "score", "polish")},
+                     "distinct_points": len({tuple(b) for b in batch})}
     out["_told_state"] = (pts, ys)
     return out
 

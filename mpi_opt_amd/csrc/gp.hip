@@ -6,9 +6,9 @@
 //
 // Kernels
 //   scale_rows_kernel    xs = X / ls (dims zero-padded to DP)
-//   kernel_matrix_kernel K  = amp * Matern52(|xs_i - xs_j|) + diag
-//   chol_kernel          in-place lower Cholesky (one workgroup)
-//   trsm_kernel          L X = B / L^T X = B, one thread per right-hand side
+//   bc_*_kernel          blocked K = L L^T, W = L^-1, alpha (mpo_gp_prepare)
+//   chol_kernel          in-place lower Cholesky (one workgroup; mpo_chol_f64)
+//   trsm_kernel          L X = B / L^T X = B, one thread per right-hand side (mpo_trsm_f64)
 //   pack_wfrag_kernel    L^-1 -> MFMA B-fragment stream (lower triangle only)
 //   gp_score_kernel      per 16/32/64-candidate block:
 //                          phase 1 (VALU): K*[m][i] = Matern52 into LDS in MFMA
@@ -207,21 +207,6 @@ __global__ __launch_bounds__(256) void xb_check_kernel(const double* __restrict_
     if (threadIdx.x == 0 && bad) flag[0] = 0.0;
 }
 
-__global__ void kernel_matrix_kernel(const double* __restrict__ xs, int n, int dp, double amp,
-                                     double diag_add, double* __restrict__ K, int ldk) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    const int i = blockIdx.y;
-    if (j >= n) return;
-    double r2 = 0.0;
-    for (int c = 0; c < dp; ++c) {
-        const double t = xs[(size_t)i * dp + c] - xs[(size_t)j * dp + c];
-        r2 += t * t;
-    }
-    double v = matern52(sqrt(r2), amp);
-    if (i == j) v += diag_add;
-    K[(size_t)i * ldk + j] = v;
-}
-
 // K from unscaled X (mpo_gp_kernel_matrix has no workspace for xs): divides
 // by ls inline, like sklearn's pdist(X / length_scale).
 __global__ void kernel_matrix_unscaled_kernel(const double* __restrict__ X, int n, int d,
@@ -299,17 +284,6 @@ __global__ __launch_bounds__(64) void trsm_kernel(const double* __restrict__ L, 
             B[(size_t)i * ldb + col] = x;
         }
     }
-}
-
-__global__ void fill_identity_kernel(double* __restrict__ W, int n, int ldw) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    const int i = blockIdx.y;
-    if (j < n) W[(size_t)i * ldw + j] = (i == j) ? 1.0 : 0.0;
-}
-
-__global__ void copy_kernel(const double* __restrict__ src, double* __restrict__ dst, int n) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < n) dst[t] = src[t];
 }
 
 // B-fragment streams of W^T (W = L^-1 lower), one per scoring wave.
@@ -889,6 +863,259 @@ int trsm_launch(const double* L, int n, int lda, double* B, int nrhs, int ldb, i
 }
 
 // ---------------------------------------------------------------------------
+// Blocked factorisation for mpo_gp_prepare: K = L L^T and W = L^-1 over 32-wide
+// blocks on the padded np x np matrix (np = n rounded up to 32, identity on the
+// padding, so padded rows never couple to K).  The one-workgroup right-looking
+// chol_kernel + one-thread-per-column trsm_kernel took ~27 ms at n = 500 (a cl_min
+// batch pays one prepare per lie); here the sequential depth is one 32x32 block
+// per step and everything else is MFMA work over many workgroups:
+//   per block k:  bc_diag_kernel   (one wave) L_kk = chol(A_kk) in registers and
+//                                  D_k = L_kk^-1 (row-wise forward substitution)
+//                 bc_panel_kernel  L_ik = A_ik D_k^T for the 16-row tiles below
+//                 bc_update_kernel A_IJ -= L_Ik L_Jk^T over the trailing lower tiles
+//   per block row I of W:  bc_winv_kernel  W_II = D_I,
+//                                          W_IJ = -D_I sum_{K=J}^{I-1} L_IK W_KJ
+//   alpha = K^-1 y = W^T (W y)   (bc_wy_kernel, bc_wtv_kernel)
+// All sums run in a fixed order: the results do not depend on the launch geometry.
+constexpr int kBc = 32;
+__host__ __device__ inline int bc_np(int n) { return (n + kBc - 1) / kBc * kBc; }
+
+// A (padded, row-major [np][np]): the lower triangle and the full diagonal 32x32 blocks
+__global__ void bc_kmat_kernel(const double* __restrict__ xs, int n, int dp, double amp, double diag_add,
+                               double* __restrict__ A, int np) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y;
+    if (j >= np || j > (i | (kBc - 1))) return;
+    double v;
+    if (i >= n || j >= n) {
+        v = i == j ? 1.0 : 0.0;
+    } else {
+        double r2 = 0.0;
+        for (int c = 0; c < dp; ++c) {
+            const double t = xs[(size_t)i * dp + c] - xs[(size_t)j * dp + c];
+            r2 += t * t;
+        }
+        v = matern52(sqrt(r2), amp);
+        if (i == j) v += diag_add;
+    }
+    A[(size_t)i * np + j] = v;
+}
+
+// One wave: lane l (and l + 32, mirrored) holds row l of the diagonal block.  Column
+// c of the factor is broadcast through the LDS at each step; a non-positive or
+// non-finite pivot records info = first failing column + 1 (sklearn's LinAlgError).
+__global__ __launch_bounds__(64) void bc_diag_kernel(double* __restrict__ A, int np, int k,
+                                                     double* __restrict__ Dinv, double* __restrict__ Wp,
+                                                     int32_t* __restrict__ info) {
+    __shared__ double col[kBc];
+    __shared__ double qrow[kBc];
+    const int lane = threadIdx.x, l = lane & (kBc - 1);
+    const int k0 = k * kBc;
+    double* Akk = A + (size_t)k0 * np + k0;
+    double r[kBc];
+#pragma unroll
+    for (int j = 0; j < kBc; ++j) r[j] = j <= l ? Akk[(size_t)l * np + j] : 0.0;
+    int bad = 0;
+#pragma unroll
+    for (int c = 0; c < kBc; ++c) {
+        if (lane < kBc) col[l] = r[c];
+        __syncthreads();
+        const double d = col[c];
+        if (!(d > 0.0) || !isfinite(d)) bad = bad ? bad : c + 1;
+        const double lcc = sqrt(d);
+        const double inv = 1.0 / lcc;
+        if (l > c) r[c] *= inv;
+        if (l == c) r[c] = lcc;
+#pragma unroll
+        for (int j = c + 1; j < kBc; ++j)
+            if (j <= l) r[j] = fma(-r[c], col[j] * inv, r[j]);
+        __syncthreads();
+    }
+    // D = L_kk^-1: row c = (e_c - sum_{m<c} L[c][m] D[m]) / L[c][c]; lane l keeps its
+    // partial row p and finishes it at step c = l
+    double p[kBc];
+#pragma unroll
+    for (int j = 0; j < kBc; ++j) p[j] = j == l ? 1.0 : 0.0;
+#pragma unroll
+    for (int c = 0; c < kBc; ++c) {
+        if (lane == c) {
+            const double inv = 1.0 / r[c];
+#pragma unroll
+            for (int j = 0; j <= c; ++j) {
+                p[j] *= inv;
+                qrow[j] = p[j];
+            }
+        }
+        __syncthreads();
+        if (l > c) {
+#pragma unroll
+            for (int j = 0; j <= c; ++j) p[j] = fma(-r[c], qrow[j], p[j]);
+        }
+        __syncthreads();
+    }
+    if (lane < kBc) {
+#pragma unroll
+        for (int j = 0; j < kBc; ++j) {
+            if (j <= l) Akk[(size_t)l * np + j] = r[j];
+            Dinv[(size_t)k * kBc * kBc + l * kBc + j] = j <= l ? p[j] : 0.0;
+            Wp[(size_t)(k0 + l) * np + k0 + j] = j <= l ? p[j] : 0.0;
+        }
+    }
+    if (lane == 0 && bad && info[0] == 0) info[0] = k0 + bad;
+}
+
+// L_ik = A_ik D_k^T for the 16-row tiles below block k, one tile per wave
+// (two 16-column MFMA outputs, K = 32).  f64 16x16x4 operands: A[m = lane & 15][kk =
+// lane >> 4], B[kk = lane >> 4][n = lane & 15]; C/D: col = lane & 15, row = (lane >> 4) + 4 q.
+__global__ __launch_bounds__(256) void bc_panel_kernel(double* __restrict__ A, int np, int k,
+                                                       const double* __restrict__ Dinv) {
+    const int lane = threadIdx.x & 63;
+    const int R = (k + 1) * 2 + blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (R >= np / 16) return;
+    const int k0 = k * kBc;
+    const double* D = Dinv + (size_t)k * kBc * kBc;
+    f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    double a[8];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) a[ks] = A[(size_t)(16 * R + (lane & 15)) * np + k0 + 4 * ks + (lane >> 4)];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+        const int kk = 4 * ks + (lane >> 4);
+        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], D[(lane & 15) * kBc + kk], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], D[(16 + (lane & 15)) * kBc + kk], acc1, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        double* row = A + (size_t)(16 * R + (lane >> 4) + 4 * q) * np + k0;
+        row[lane & 15] = acc0[q];
+        row[16 + (lane & 15)] = acc1[q];
+    }
+}
+
+// A_IJ -= L_Ik L_Jk^T over the lower 16x16 tiles of the trailing matrix (I >= J past
+// block k), one tile per wave at a time, K = 32 (8 MFMAs)
+__global__ __launch_bounds__(256) void bc_update_kernel(double* __restrict__ A, int np, int k) {
+    const int lane = threadIdx.x & 63;
+    const int t0 = (k + 1) * 2;                 // first trailing 16-tile
+    const int T = np / 16 - t0;
+    const int ntl = T * (T + 1) / 2;
+    const int k0 = k * kBc;
+    const int gw = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    const int nw = gridDim.x * 4;
+    for (int t = gw; t < ntl; t += nw) {
+        int I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+        while (I * (I + 1) / 2 > t) --I;
+        while ((I + 1) * (I + 2) / 2 <= t) ++I;
+        const int J = t - I * (I + 1) / 2;
+        const int gi = 16 * (t0 + I), gj = 16 * (t0 + J);
+        f64x4 acc;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = A[(size_t)(gi + (lane >> 4) + 4 * q) * np + gj + (lane & 15)];
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            const int kk = k0 + 4 * ks + (lane >> 4);
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-A[(size_t)(gi + (lane & 15)) * np + kk],
+                                                       A[(size_t)(gj + (lane & 15)) * np + kk], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) A[(size_t)(gi + (lane >> 4) + 4 * q) * np + gj + (lane & 15)] = acc[q];
+    }
+}
+
+// Block row I of W = L^-1, block column J = blockIdx.x < I: wave w computes the
+// 16x16 tile (a, b) = (w >> 1, w & 1) of S = sum_{K=J}^{I-1} L_IK W_KJ into the LDS,
+// then W_IJ = -D_I S.
+__global__ __launch_bounds__(256) void bc_winv_kernel(const double* __restrict__ L, double* __restrict__ Wp, int np,
+                                                      int I, const double* __restrict__ Dinv) {
+    __shared__ double S[kBc][kBc + 1];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int a = w >> 1, b = w & 1;
+    const int J = blockIdx.x;
+    const int I0 = I * kBc, J0 = J * kBc;
+    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int K = J; K < I; ++K) {
+        const int K0 = K * kBc;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            const int kk = 4 * ks + (lane >> 4);
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(L[(size_t)(I0 + 16 * a + (lane & 15)) * np + K0 + kk],
+                                                       Wp[(size_t)(K0 + kk) * np + J0 + 16 * b + (lane & 15)], acc,
+                                                       0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) S[16 * a + (lane >> 4) + 4 * q][16 * b + (lane & 15)] = acc[q];
+    __syncthreads();
+    const double* D = Dinv + (size_t)I * kBc * kBc;
+    f64x4 o = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+        const int kk = 4 * ks + (lane >> 4);
+        o = __builtin_amdgcn_mfma_f64_16x16x4f64(D[(16 * a + (lane & 15)) * kBc + kk], S[kk][16 * b + (lane & 15)], o,
+                                                 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Wp[(size_t)(I0 + 16 * a + (lane >> 4) + 4 * q) * np + J0 + 16 * b + (lane & 15)] = -o[q];
+}
+
+// v = W y (one wave per row, fixed butterfly), then alpha = W^T v (one thread per column)
+__global__ __launch_bounds__(256) void bc_wy_kernel(const double* __restrict__ Wp, int np, int n,
+                                                    const double* __restrict__ y, double* __restrict__ v) {
+    const int lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= np) return;
+    double s = 0.0;
+    for (int j = lane; j <= i && j < n; j += 64) s = fma(Wp[(size_t)i * np + j], y[j], s);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+    if (lane == 0) v[i] = s;
+}
+
+__global__ void bc_wtv_kernel(const double* __restrict__ Wp, int np, int n, const double* __restrict__ v,
+                              double* __restrict__ alpha) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    double s = 0.0;
+    for (int i = j; i < np; ++i) s = fma(Wp[(size_t)i * np + j], v[i], s);
+    alpha[j] = s;
+}
+
+// padded factors -> the model's [n][n] L and W (lower triangles, zeros above)
+__global__ void bc_copy_out_kernel(const double* __restrict__ A, const double* __restrict__ Wp, int np, int n,
+                                   double* __restrict__ L, double* __restrict__ W) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y;
+    if (j >= n) return;
+    L[(size_t)i * n + j] = j <= i ? A[(size_t)i * np + j] : 0.0;
+    W[(size_t)i * n + j] = j <= i ? Wp[(size_t)i * np + j] : 0.0;
+}
+
+// The launch sequence of the blocked factorisation (+ alpha) on stream s.
+hipError_t blocked_factor(const double* xs, int n, int dp, double amp, double diag_add, const double* y_norm,
+                          double* A, double* Wp, double* Dinv, double* v, double* L, double* W, double* alpha,
+                          int32_t* info, hipStream_t s) {
+    const int np = bc_np(n), nbk = np / kBc;
+    (void)hipMemsetAsync(info, 0, sizeof(int32_t), s);
+    (void)hipMemsetAsync(Wp, 0, (size_t)np * np * sizeof(double), s);
+    hipLaunchKernelGGL(bc_kmat_kernel, dim3((np + 63) / 64, np), dim3(64), 0, s, xs, n, dp, amp, diag_add, A, np);
+    for (int k = 0; k < nbk; ++k) {
+        hipLaunchKernelGGL(bc_diag_kernel, dim3(1), dim3(64), 0, s, A, np, k, Dinv, Wp, info);
+        const int below = np / 16 - (k + 1) * 2;
+        if (below <= 0) continue;
+        hipLaunchKernelGGL(bc_panel_kernel, dim3((below + 3) / 4), dim3(256), 0, s, A, np, k, Dinv);
+        const int ntl = below * (below + 1) / 2;
+        hipLaunchKernelGGL(bc_update_kernel, dim3(std::max(1, std::min(1024, (ntl + 3) / 4))), dim3(256), 0, s,
+                           A, np, k);
+    }
+    for (int I = 1; I < nbk; ++I)
+        hipLaunchKernelGGL(bc_winv_kernel, dim3(I), dim3(256), 0, s, A, Wp, np, I, Dinv);
+    hipLaunchKernelGGL(bc_wy_kernel, dim3((np + 3) / 4), dim3(256), 0, s, Wp, np, n, y_norm, v);
+    hipLaunchKernelGGL(bc_wtv_kernel, dim3((n + 255) / 256), dim3(256), 0, s, Wp, np, n, v, alpha);
+    hipLaunchKernelGGL(bc_copy_out_kernel, dim3((n + 63) / 64, n), dim3(64), 0, s, A, Wp, np, n, L, W);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Acquisition value + gradient at a few points: the objective of skopt's
 // L-BFGS-B polish of the best n_restarts_optimizer candidates per acquisition
 // (skopt optimizer.py _tell -> fmin_l_bfgs_b(gaussian_acquisition_1D, ...,
@@ -1118,6 +1345,11 @@ size_t mpo_gp_prepare_ws_bytes(int n, int d) {
     c.take<int32_t>(wmeta_elems(np16));    // wmeta
     c.take<double>((size_t)xrows * dp + 8);   // xb + its guard flag
     c.take<double>(4 * (size_t)n);            // xb self-check (mu_n, q) rows, direct and expanded
+    const size_t np = bc_np(n);
+    c.take<double>(np * np);                  // blocked factorisation: padded A -> L
+    c.take<double>(np * np);                  //                        padded W
+    c.take<double>(np * kBc);                 //                        diagonal-block inverses
+    c.take<double>(np);                       //                        W y
     return c.used + 256;
 }
 
@@ -1146,27 +1378,18 @@ int mpo_gp_prepare(const double* X, const double* y_norm, int n, int d, const do
     int32_t* wmeta = c.take<int32_t>(wmeta_elems(np16));
     double* xb = c.take<double>((size_t)xrows * dp + 8);
     double* mqc = c.take<double>(4 * (size_t)n);
+    const size_t npb = bc_np(n);
+    double* Ab = c.take<double>(npb * npb);
+    double* Wb = c.take<double>(npb * npb);
+    double* Db = c.take<double>(npb * kBc);
+    double* vb = c.take<double>(npb);
 
     hipLaunchKernelGGL(scale_rows_kernel, dim3((xrows * dp + 255) / 256), dim3(256), 0, s, X, n, xrows, d, dp, ls, xs,
                        ls_pad);
     MPO_LAUNCH_CHECK();
     hipLaunchKernelGGL(zero_kernel, dim3((xrows + 255) / 256), dim3(256), 0, s, alpha, xrows);
     MPO_LAUNCH_CHECK();
-    hipLaunchKernelGGL(kernel_matrix_kernel, dim3((n + 63) / 64, n), dim3(64), 0, s, xs, n, dp, amp,
-                       noise + kJitter, L, n);
-    MPO_LAUNCH_CHECK();
-    hipLaunchKernelGGL(chol_kernel, dim3(1), dim3(1024), 0, s, L, n, n, info);
-    MPO_LAUNCH_CHECK();
-    hipLaunchKernelGGL(fill_identity_kernel, dim3((n + 63) / 64, n), dim3(64), 0, s, W, n, n);
-    MPO_LAUNCH_CHECK();
-    int rc = trsm_launch(L, n, n, W, n, n, 0, s);
-    if (rc) return rc;
-    hipLaunchKernelGGL(copy_kernel, dim3((n + 255) / 256), dim3(256), 0, s, y_norm, alpha, n);
-    MPO_LAUNCH_CHECK();
-    rc = trsm_launch(L, n, n, alpha, 1, 1, 0, s);
-    if (rc) return rc;
-    rc = trsm_launch(L, n, n, alpha, 1, 1, 1, s);
-    if (rc) return rc;
+    MPO_HIP(blocked_factor(xs, n, dp, amp, noise + kJitter, y_norm, Ab, Wb, Db, vb, L, W, alpha, info, s));
     const int T = np16 / 16;
     const size_t nw = wfrag_elems(np16);
     hipLaunchKernelGGL(zero_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, wfrag, (int)nw);

@@ -120,11 +120,12 @@ def polish_lockstep(model, starts, acqs, y_opt, xi, kappa, bounds, maxiter=20):
 
 #: process-wide accounts of the GP work (bench / search reports): refits, their
 #: observation counts and the seconds spent refitting vs proposing
-STATS = {"refits": 0, "n_sum": 0, "n_max": 0, "refit_s": 0.0, "propose_s": 0.0}
+STATS = {"refits": 0, "n_sum": 0, "n_max": 0, "refit_s": 0.0, "propose_s": 0.0, "prepare_s": 0.0, "score_s": 0.0,
+         "polish_s": 0.0}
 
 
 def reset_stats():
-    STATS.update(refits=0, n_sum=0, n_max=0, refit_s=0.0, propose_s=0.0)
+    STATS.update(refits=0, n_sum=0, n_max=0, refit_s=0.0, propose_s=0.0, prepare_s=0.0, score_s=0.0, polish_s=0.0)
 
 
 class OptimizeResult(dict):
@@ -266,6 +267,9 @@ class Optimizer:
         STATS["n_max"] = max(STATS["n_max"], len(y))
         STATS["refit_s"] += t1 - t0
         est = GPModel(Xt, y, amp, ls, noise, device=self.device)
+        est.dev                                   # the device posterior (mpo_gp_prepare)
+        t2 = time.perf_counter()
+        STATS["prepare_s"] += t2 - t1
         if hasattr(self, "next_xs_") and self.acq_func == "gp_hedge":
             self.gains_ -= est.predict_mean(np.vstack(self.next_xs_))
         if self.model_queue_size is None or self.model_queue_size > 0:
@@ -278,7 +282,10 @@ class Optimizer:
         xi = self.acq_func_kwargs.get("xi", 0.01)
         kappa = self.acq_func_kwargs.get("kappa", 1.96)
         k = 1 if self.acq_optimizer == "sampling" else min(self.n_restarts_optimizer, X.shape[0])
+        t3 = time.perf_counter()
         top = self._score_topk(est, X, y_opt, xi, kappa, k)
+        t4 = time.perf_counter()
+        STATS["score_s"] += t4 - t3
         rec = {"theta": (est.amp, est.length_scale.copy(), est.noise), "top": dict(top), "polished": {}} \
             if self.trace is not None else None
         self.next_xs_ = []
@@ -286,6 +293,7 @@ class Optimizer:
             runs = [(a, i) for a in self.cand_acq_funcs_ for i in top[a]]
             polished = polish_lockstep(est, [X[i] for _, i in runs], [a for a, _ in runs], y_opt, xi, kappa,
                                        self.space.transformed_bounds)
+            STATS["polish_s"] += time.perf_counter() - t4
         for acq in self.cand_acq_funcs_:
             idx = top[acq]
             if self.acq_optimizer == "sampling":
