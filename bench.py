@@ -631,6 +631,7 @@ def bench_search_gp(args, torch, dist, ws, rank, dev):
     if rank != 0:
         return None
     gp = rep["gp"]
+    samples = gp.pop("samples")
     opt_s = rep["ask_s"] + rep["tell_s"]
     out = {"metric": "MNIST-CNN trials/hour, measured search with the GP in the loop (BASELINE configs[3] layout)",
            "value": rep["trials_told"] * 3600.0 / wall, "unit": "trials/hour (told)", "n_gpus": ws,
@@ -668,13 +669,122 @@ def bench_search_gp(args, torch, dist, ws, rank, dev):
                      "ms_per_proposal_split": {k: 1e3 * st[k + "_s"] / st["refits"] for k in ("prepare", "score", "polish")},
                      "distinct_points": len({tuple(b) for b in batch})}
     out["_told_state"] = (pts, ys)
+    out["_samples"] = samples
+    out["_samples_all"] = samples + list(st["samples"])
+    # GPU-seconds per 10-epoch 5-fold trial on one GPU, from this run's populations
+    out["_trial_s_gpu"] = rep["train_s"] / max(1, rep["trials_trained"]) * 10.0
     return out
 
 
-def _oracle_refit_seconds(pts, ys, n, reps=2):
-    """Seconds per skopt refit + proposal on the host (oracle: sklearn fit, einsum
-    posterior over 10 000 candidates, scipy L-BFGS-B polish) at n observations:
-    the copy refit + cl_min lies of ask(reps - 1)."""
+class _CountingOptimizer:
+    """Stand-in optimizer that only counts the GP refits skopt's protocol runs (and
+    at how many observations): a refit per tell once n_initial_points are told,
+    and per ``ask(n, 'cl_min')`` the copy's refit plus one per lie."""
+
+    def __init__(self, dimensions, random_state, n_initial_points=10, **_):
+        self.rng = np.random.RandomState(random_state)
+        self.dims = dimensions
+        self.n0 = n_initial_points
+        self.told = 0
+        self.refits = []
+
+    def _point(self):
+        return [int(self.rng.randint(d.low, d.high + 1)) if type(d).__name__ == "Integer"
+                else float(self.rng.uniform(d.low, d.high)) for d in self.dims]
+
+    def tell(self, xs, ys):
+        from mpi_opt_amd.optimizer import OptimizeResult
+
+        self.told += len(ys)
+        if self.told >= self.n0:
+            self.refits.append(self.told)
+        return OptimizeResult(x=list(xs[0]), fun=float(min(ys)))
+
+    def ask(self, n):
+        if self.told >= self.n0:
+            self.refits.append(self.told)                      # copy(): re-tell, one refit
+        self.refits.extend(self.told + i + 1 for i in range(n) if self.told + i + 1 >= self.n0)
+        return [self._point() for _ in range(n)]
+
+
+def protocol_refits(world_size, block_size, num_iterations):
+    """The refits (their observation counts) and populations the reference's
+    protocol runs for an option3 layout: the build's scheduler and PopulationComm
+    driven with instant random FOMs and a refit-counting optimizer (CPU only)."""
+    import tempfile
+
+    from mpi_opt_amd import scheduler as S
+    from mpi_opt_amd.blocks import PopulationComm
+    from mpi_opt_amd.models import mnist_space
+
+    class _Instant:
+        def __init__(self):
+            self.rng = np.random.RandomState(0)
+
+        def evaluate(self, params):
+            return [float(v) for v in self.rng.rand(len(params))]
+
+    nb = (world_size - 1) // block_size
+    comm = PopulationComm(nb, block_size, _Instant())
+
+    class _Sched(S.AskTellScheduler):
+        optimizer_factory = staticmethod(lambda dims, rs, **kw: _CountingOptimizer(dims, rs))
+
+    with tempfile.TemporaryDirectory() as tmp:
+        sched = _Sched(comm, nb, mnist_space(), checkpoint=os.path.join(tmp, "c.pkl"))
+        sched.run(num_iterations=num_iterations)
+    return sched.optimizer.refits, list(comm.batches)
+
+
+def fit_refit_cost(samples, powers=(0, 1, 2)):
+    """Least-squares t(n) = sum_p c_p n^p over measured (n, seconds) refit +
+    proposal samples; returns [(p, c_p)]."""
+    n = np.array([s[0] for s in samples], dtype=float)
+    t = np.array([s[1] for s in samples], dtype=float)
+    A = np.stack([n ** p for p in powers], 1)
+    coef, *_ = np.linalg.lstsq(A, t, rcond=None)
+    return [(int(p), float(c)) for p, c in zip(powers, coef)]
+
+
+def _price(curve, ns):
+    return float(sum(np.sum(c * ns ** p) for p, c in curve))
+
+
+def project_configs3(samples, trial_s_gpu, gpus=8, cpu=None):
+    """BASELINE configs[3] in full (``-n 129 --block-size 2 --n-fold 5
+    --num-iterations 256 --epochs 10``, 256 trials over 8 GPUs): the protocol's
+    exact refit schedule (protocol_refits) priced by the refit + proposal cost
+    curve measured in this run, plus training at the measured GPU-seconds per
+    10-epoch 5-fold trial (``trial_s_gpu``, one GPU) spread over ``gpus`` GPUs --
+    the optimizer and the populations do not overlap in the population protocol
+    (a population trains once every block is busy).  With ``cpu`` ({"samples":
+    [(n, s)], "trial_s": s}) the same for the reference's host path.  A
+    projection from measured parts, not a measurement."""
+    refits, pops = protocol_refits(129, 2, 256)
+    coef = fit_refit_cost(samples)
+    ns = np.array(refits, dtype=float)
+    t_gp = _price(coef, ns)
+    trials = sum(pops)
+    t_train = trials * trial_s_gpu / gpus
+    out = {"workload": "configs[3] in full: -n 129 --block-size 2 --n-fold 5 --num-iterations 256 --epochs 10, "
+                       f"{gpus} GPUs", "refits": len(refits), "refit_n_mean": float(ns.mean()),
+           "refit_n_max": int(ns.max()), "populations": pops, "trials_trained": trials,
+           "refit_cost_fit_s": coef, "optimizer_s": t_gp, "training_s": t_train,
+           "trials_per_hour": trials * 3600.0 / (t_gp + t_train), "optimizer_share": t_gp / (t_gp + t_train)}
+    if cpu:
+        ccoef = fit_refit_cost(cpu["samples"], powers=(2, 3))
+        t_gp_cpu = _price(ccoef, ns)
+        t_train_cpu = trials * cpu["trial_s"]
+        out["cpu"] = {"refit_cost_fit_s": ccoef, "optimizer_s": t_gp_cpu, "training_s": t_train_cpu,
+                      "trials_per_hour": trials * 3600.0 / (t_gp_cpu + t_train_cpu)}
+        out["speedup_vs_cpu"] = out["trials_per_hour"] / out["cpu"]["trials_per_hour"]
+    return out
+
+
+def _oracle_refit_seconds(pts, ys, n):
+    """Seconds of one skopt refit + proposal on the host at n observations (oracle:
+    sklearn GaussianProcessRegressor.fit, einsum posterior over 10 000 candidates,
+    scipy L-BFGS-B polish)."""
     from oracle.skopt_optimizer import SkoptOracle
 
     from mpi_opt_amd.models import mnist_space
@@ -683,32 +793,35 @@ def _oracle_refit_seconds(pts, ys, n, reps=2):
     ora.Xi, ora.yi = [list(p) for p in pts[:n]], list(ys[:n])
     ora._n_initial_points -= n
     t0 = time.perf_counter()
-    ora.ask(reps - 1)
-    return (time.perf_counter() - t0) / reps
+    ora._fit_and_propose()
+    return time.perf_counter() - t0
 
 
 def cpu_baseline_search_gp(out, cpu_train_trial_s):
     """The same search on the host the way the reference runs it, from bounded
-    samples: the GP side is the oracle's skopt refit + proposal timed at the run's
-    mean observation count and multiplied by the run's refit count; training is
-    the torch-CPU restatement's per-trial time (the train leg's sample, 4 trials at
-    once on every core) for the trials the run trained, at its epochs and folds."""
+    samples: the GP side is the oracle's skopt refit + proposal timed at three
+    observation counts, fitted as a n^2 + b n^3 and summed over the run's refits;
+    training is the torch-CPU restatement's per-trial time (the train leg's
+    sample, 4 trials at once on every core) for the trials the run trained, at
+    its epochs."""
     pts, ys = out.pop("_told_state")
-    n_mean = int(round(out["gp_refit_mean_n"]))
-    s_refit = _oracle_refit_seconds(pts, ys, n_mean)
-    s_refit256 = _oracle_refit_seconds(pts, ys, 256)
+    samples = [(n, _oracle_refit_seconds(pts, ys, n)) for n in (64, 160, 256)]
+    coef = fit_refit_cost(samples, powers=(2, 3))
+    ns = np.array([s_[0] for s_ in out.pop("_samples")], dtype=float)
     epochs = 1
     t_train = out["trials_trained"] * cpu_train_trial_s * epochs / 10.0
-    t_gp = out["gp_refits"] * s_refit
+    t_gp = _price(coef, ns)
     t = t_gp + t_train
-    return {"value": out["trials_told"] * 3600.0 / t, "unit": "trials/hour (told)", "cores": host_cores(),
-            "kind": "port", "seconds_gp": t_gp, "seconds_training": t_train, "s_per_refit_at_mean_n": s_refit,
-            "s_per_refit_n256": s_refit256, "ask256_seconds_est": s_refit256 * (out["ask256"]["refits"]),
-            "sample": f"GP: oracle skopt refit + proposal (sklearn GaussianProcessRegressor.fit, einsum posterior, "
-                      f"L-BFGS-B polish, 10 000 candidates) timed over 2 refits at n={n_mean} ({s_refit:.2f} s each) "
-                      f"and n=256 ({s_refit256:.2f} s) x the run's {out['gp_refits']} refits; training: torch-CPU "
-                      f"fp32 per-trial time of the train leg's sample ({cpu_train_trial_s:.0f} s of all cores per "
-                      f"10-epoch 5-fold trial, 4 at once) x {out['trials_trained']} trials x {epochs}/10 epochs"}
+    res = {"value": out["trials_told"] * 3600.0 / t, "unit": "trials/hour (told)", "cores": host_cores(),
+           "kind": "port", "seconds_gp": t_gp, "seconds_training": t_train,
+           "refit_samples_s": [[n, t_] for n, t_ in samples], "refit_cost_fit_s": coef,
+           "sample": f"GP: oracle skopt refit + proposal (sklearn GaussianProcessRegressor.fit, einsum posterior, "
+                     f"L-BFGS-B polish, 10 000 candidates) timed once each at n = 64, 160, 256 "
+                     f"({', '.join(f'{t_:.2f}' for _, t_ in samples)} s), fitted a n^2 + b n^3 and summed over the "
+                     f"run's {len(ns)} refits; training: torch-CPU fp32 per-trial time of the train leg's sample "
+                     f"({cpu_train_trial_s:.0f} s of all cores per 10-epoch 5-fold trial, 4 at once) x "
+                     f"{out['trials_trained']} trials x {epochs}/10 epochs"}
+    return res, {"samples": samples, "trial_s": cpu_train_trial_s}
 
 
 def cpu_baseline_search(search_out, concurrent=4):
@@ -819,12 +932,16 @@ def main():
             trials = train.pop("_trials")
             train["cpu_baseline"] = cpu_baseline_train(trials) if cpu else None
         if srch3 is not None:
+            cpu_parts = None
             if cpu:
                 tcpu = (train or {}).get("cpu_baseline") or cpu_baseline_train(sample_trials(32, seed=13579))
-                srch3["cpu_baseline"] = cpu_baseline_search_gp(srch3, 3600.0 / tcpu["value"])
+                srch3["cpu_baseline"], cpu_parts = cpu_baseline_search_gp(srch3, 3600.0 / tcpu["value"])
             else:
                 srch3.pop("_told_state")
+                srch3.pop("_samples")
                 srch3["cpu_baseline"] = None
+            srch3["projection_configs3_8gpu"] = project_configs3(srch3.pop("_samples_all"), srch3.pop("_trial_s_gpu"),
+                                                                 cpu=cpu_parts)
         if dn is not None:
             dn["cpu_baseline"] = cpu_baseline_densenet() if cpu else None
         if res is not None:

@@ -845,7 +845,7 @@ __global__ __launch_bounds__(kFitThreads) void lml_sweep_kernel(LmlArgs a) {
 // arithmetic in the same order as lml_sweep_kernel, so both give the same bits.
 constexpr int kSplitMinN = 48;    // past it the split beats both single-workgroup kernels (0.09 vs 0.20 ms at n = 64)
 constexpr int kUpdThreads = 256;
-constexpr int kUpdTilesPerWave = 4;
+constexpr int kUpdTilesPerWave = 1;   // one lower tile per wave: latency-bound steps want many waves
 
 // per-theta workspace (doubles): xs | alpha | A [np][np] | G [np][32] | C0, C1 [np][32]
 // | P^-1 [32][32] | logdet, fail.  C_k (block column k before sweep k, row-major
@@ -946,6 +946,7 @@ __global__ __launch_bounds__(kFitThreads) void sw_pivot_kernel(LmlArgs a, int k)
     const SsPtrs p = ss_ptrs(a, b);
     __shared__ double Pb[kSwNb * kSwLd];   // pivot block rows of C
     __shared__ double Pi[kSwNb * kSwLd];   // P^-1
+    __shared__ double colb[kSwNb];         // the sweep's column broadcast
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     // C_k: at k = 0 copied from A (row segments for rows >= k0, the block's rows
@@ -978,33 +979,46 @@ __global__ __launch_bounds__(kFitThreads) void sw_pivot_kernel(LmlArgs a, int k)
     __syncthreads();
     if (a.stop == 21) return;   // diagnostics only (MPO_FIT_DEBUG): column copy alone
     if (wave == 0 && a.stop != 22) {
-        const int l = lane & 31;
-        double r[kSwNb];
+        // Gauss-Jordan sweep of the 32x32 pivot block by wave 0: lane l + 32 h holds
+        // columns [16 h, 16 h + 16) of row l.  The swept block stays symmetric, so the
+        // pivot row c is column c: at step c every row writes its column-c entry to the
+        // LDS and every lane reads the half of that column it needs (broadcast reads;
+        // LDS operations of one wave complete in order) -- 16 FMAs per lane and step
+        // instead of a 31-readlane chain per step.
+        const int l = lane & 31, h = lane >> 5;
+        double r[16];
 #pragma unroll
-        for (int j = 0; j < kSwNb; ++j) r[j] = Pb[l * kSwLd + j];
+        for (int jj = 0; jj < 16; ++jj) r[jj] = Pb[l * kSwLd + 16 * h + jj];
         double prod = 1.0;
         int bad = 0;
+        const double* colh = colb + 16 * h;
 #pragma unroll
         for (int c = 0; c < kSwNb; ++c) {
-            const double pv = readlane_f64(r[c], c);
+            const int hc = c >> 4, jc = c & 15;
+            if (h == hc) colb[l] = r[jc];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const double pv = colb[c];
             if (!(pv > 0.0) || !isfinite(pv)) bad = bad ? bad : c + 1;
             prod *= pv;
             const double ip = 1.0 / pv;
             const bool piv = l == c;
-            const double t = r[c] * ip;
+            const double t = colb[l] * ip;
+            double cj[16];
 #pragma unroll
-            for (int j = 0; j < kSwNb; ++j) {
-                if (j == c) continue;
-                const double pj = readlane_f64(r[j], c);
-                r[j] = piv ? r[j] * ip : fma(-t, pj, r[j]);
+            for (int jj = 0; jj < 16; ++jj) cj[jj] = colh[jj];
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) {
+                const double upd = piv ? r[jj] * ip : fma(-t, cj[jj], r[jj]);
+                if (jj == jc) r[jj] = h == hc ? (piv ? -ip : t) : upd;
+                else r[jj] = upd;
             }
-            r[c] = piv ? -ip : t;
+            asm volatile("" ::: "memory");
         }
-        if (lane < kSwNb) {
+        if (lane < 64) {
 #pragma unroll
-            for (int j = 0; j < kSwNb; ++j) {
-                Pi[l * kSwLd + j] = -r[j];
-                p.P[l * kSwNb + j] = -r[j];
+            for (int jj = 0; jj < 16; ++jj) {
+                Pi[l * kSwLd + 16 * h + jj] = -r[jj];
+                p.P[l * kSwNb + 16 * h + jj] = -r[jj];
             }
         }
         if (lane == 0) {

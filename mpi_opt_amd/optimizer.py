@@ -121,11 +121,12 @@ def polish_lockstep(model, starts, acqs, y_opt, xi, kappa, bounds, maxiter=20):
 #: process-wide accounts of the GP work (bench / search reports): refits, their
 #: observation counts and the seconds spent refitting vs proposing
 STATS = {"refits": 0, "n_sum": 0, "n_max": 0, "refit_s": 0.0, "propose_s": 0.0, "prepare_s": 0.0, "score_s": 0.0,
-         "polish_s": 0.0}
+         "polish_s": 0.0, "samples": []}
 
 
 def reset_stats():
-    STATS.update(refits=0, n_sum=0, n_max=0, refit_s=0.0, propose_s=0.0, prepare_s=0.0, score_s=0.0, polish_s=0.0)
+    STATS.update(refits=0, n_sum=0, n_max=0, refit_s=0.0, propose_s=0.0, prepare_s=0.0, score_s=0.0, polish_s=0.0,
+                 samples=[])
 
 
 class OptimizeResult(dict):
@@ -319,7 +320,9 @@ class Optimizer:
             rec["gains"] = np.copy(getattr(self, "gains_", np.zeros(0)))
             self.trace.append(rec)
         self._next_x = self.space.inverse_transform(next_x.reshape(1, -1))[0]
-        STATS["propose_s"] += time.perf_counter() - t1
+        t5 = time.perf_counter()
+        STATS["propose_s"] += t5 - t1
+        STATS["samples"].append((len(y), t5 - t0))      # (n, seconds of refit + proposal)
 
     def _score_topk(self, est, X, y_opt, xi, kappa, k):
         """skopt's ``np.argsort(values)[:k]`` per acquisition (lowest index first on

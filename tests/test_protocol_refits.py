@@ -1,0 +1,41 @@
+"""The refit schedule the reference's protocol implies (bench.protocol_refits):
+the build's scheduler + PopulationComm driven with instant FOMs and a
+refit-counting optimizer.  The counting rule is skopt's (a refit per tell once
+n_initial_points = 10 are told; per ask(n, "cl_min") the copy's refit plus one
+per lie, coordinator.py:46-50 / 63-79) -- the same rule the device Optimizer
+follows (17 refits for 20 tells + ask(5) in tests/test_optimizer_parity_gpu.py)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def test_configs0_and_configs3_refit_schedules():
+    import bench
+
+    refits, pops = bench.protocol_refits(21, 5, 10)          # configs[0]: -n 21 --block-size 5, 10 iterations
+    assert pops == [4, 4, 2] and len(refits) == 21 and min(refits) == 10
+    refits, pops = bench.protocol_refits(129, 2, 128)        # configs[3] layout, 128 iterations
+    assert pops == [64, 64] and len(refits) == 8255 and max(refits) == 191
+
+
+def test_counting_optimizer_matches_the_device_rule():
+    import bench
+    from mpi_opt_amd.models import mnist_space
+
+    o = bench._CountingOptimizer(mnist_space(), 0)
+    for i in range(20):
+        o.tell([o._point()], [float(i)])
+    assert len(o.refits) == 11                              # tells 10 .. 20
+    o.ask(5)
+    assert len(o.refits) == 17 and o.refits[11:] == [20, 21, 22, 23, 24, 25]
+
+
+def test_refit_cost_fit_recovers_a_polynomial():
+    import numpy as np
+
+    import bench
+
+    samples = [(n, 0.002 + 1e-5 * n + 3e-8 * n * n) for n in range(10, 500, 7)]
+    coef = dict(bench.fit_refit_cost(samples))
+    assert np.allclose([coef[0], coef[1], coef[2]], [0.002, 1e-5, 3e-8], rtol=1e-6)
