@@ -100,7 +100,7 @@ def live_pmc(train_trials):
     GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs).  Runs before this process touches the
     GPU.  Returns {"ei": ..., "train": ...}; a failed pass leaves its entry None
     with the reason."""
-    out = {"ei": None, "train": None, "errors": []}
+    out = {"ei": None, "train": None, "densenet": None, "errors": []}
     ei_prog = [os.path.join(ROOT, "scripts", "ei_probe.py"), "3"]
     try:
         # one acquisition pass = gp_score_kernel + score_finish_kernel (the (mu_n, q)
@@ -137,6 +137,18 @@ def live_pmc(train_trials):
                         "per_kernel_mfma_busy": per}
     except Exception as e:  # noqa: BLE001
         out["errors"].append(f"train: {e}")
+    # DenseNet (configs[4]): 2 warmup + 3 train steps of the 32-member population
+    dn_prog = [os.path.join(ROOT, "scripts", "dn_probe.py"), "--steps", "3", "--no-eval"]
+    try:
+        ours = lambda k: "anonymous namespace" in k     # noqa: E731
+        f = _per_dispatch(pmc_pass(["FETCH_SIZE"], dn_prog), "FETCH_SIZE", ours)
+        w = _per_dispatch(pmc_pass(["WRITE_SIZE"], dn_prog), "WRITE_SIZE", ours)
+        fetch = 1024.0 * sum(f.values()) / 5
+        write = 1024.0 * sum(w.values()) / 5
+        out["densenet"] = {"hbm_bytes_per_train_step": 2.0 * fetch + write, "fetch_size_bytes_raw": fetch,
+                           "write_size_bytes": write, "steps": 5}
+    except Exception as e:  # noqa: BLE001
+        out["errors"].append(f"densenet: {e}")
     return out
 
 
@@ -485,7 +497,7 @@ def bench_densenet(args, torch, dist, ws, rank, dev):
     CIFAR-10-shape data; each trial trains 10 epochs on the option3 70/30 split of
     50 000 samples (350 train + 150 validation batches of 100 per epoch)."""
     from mpi_opt_amd.densenet import DenseNetArch, DenseNetPopulation, flops_per_sample_fwd, \
-        flops_per_sample_train, synthetic_cifar
+        flops_per_sample_train, hbm_bytes_train, synthetic_cifar
     from mpi_opt_amd.population import kfold_split
 
     n_trials, B = args.dn_trials, 100
@@ -536,6 +548,8 @@ def bench_densenet(args, torch, dist, ws, rank, dev):
     trials_per_hour = ws * n_trials * 3600.0 / (t_macro * 50 * 10)
     flops = n_trials * B * (7 * flops_per_sample_train(pop.layers) + 3 * flops_per_sample_fwd(pop.layers))
     achieved = flops / (t_gpu / args.train_steps) / 1e12
+    algo_bytes = n_trials * hbm_bytes_train(pop.layers, B, pop.n_params)      # per train step
+    pmc = (args.pmc or {}).get("densenet") if n_trials == 32 else None
     return {
         "metric": "DenseNet trials/hour (CIFAR-10 shape, 10 epochs, 70/30 split of 50k samples)",
         "value": trials_per_hour, "unit": "trials/hour", "n_gpus": ws, "steps": args.train_steps,
@@ -547,7 +561,11 @@ def bench_densenet(args, torch, dist, ws, rank, dev):
                    "parallelism": f"trials sharded, {ws} GPU(s), all-gather of validation losses"},
         "roofline": {"kernel": "population step (all DenseNet kernels)", "bound": "mfma",
                      "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None, "algorithmic_flops_per_step": flops},
+                     "frac": achieved / FP32_PEAK_TFLOPS,
+                     "traffic": pmc["hbm_bytes_per_train_step"] if pmc else None,
+                     "traffic_unit": "HBM bytes per train step (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, this run)",
+                     "algorithmic_hbm_bytes_per_train_step": algo_bytes, "pmc": pmc,
+                     "algorithmic_flops_per_step": flops},
     }
 
 
@@ -890,7 +908,7 @@ def main():
         sys.exit(relaunch_distributed(args.gpus))
     ws, rank, local = dist_env()
     args.pmc = None
-    if ws == 1 and not args.no_pmc and args.workload in ("ei", "train", "all") and shutil.which("rocprofv3"):
+    if ws == 1 and not args.no_pmc and args.workload in ("ei", "train", "densenet", "all") and shutil.which("rocprofv3"):
         t0 = time.perf_counter()
         args.pmc = live_pmc(args.train_trials)      # child processes, before this one touches the GPU
         args.pmc["wall_s"] = time.perf_counter() - t0

@@ -126,6 +126,19 @@ int mpo_gp_lml_grad(const double* X, const double* y_norm, int n, int d,
                     const double* theta, int batch, double* lml, double* grad,
                     int32_t* info, void* ws, size_t ws_bytes, void* stream);
 
+/* Bytes of the device buffer mpo_gp_lml_grad_host stages through (d dims, batch thetas). */
+size_t mpo_gp_lml_io_bytes(int d, int batch);
+
+/* mpo_gp_lml_grad for one L-BFGS-B round of the refit with host-side input and
+ * output: theta_host [batch][d+2] is copied into dev_io, the objective runs, and
+ * out_host receives lml [batch] | grad [batch][d+2] | info (int32 [batch]) --
+ * one call and one stream synchronisation per round instead of separate copies
+ * (the refit runs ~100-200 rounds per fit, sklearn _gpr.py:296-337).  Pinned host
+ * buffers avoid a staging copy.  Synchronises `stream`. */
+int mpo_gp_lml_grad_host(const double* X, const double* y_norm, int n, int d,
+                         const double* theta_host, int batch, double* out_host,
+                         void* dev_io, size_t io_bytes, void* ws, size_t ws_bytes, void* stream);
+
 /* Workspace bytes for mpo_gp_acq_score over m candidates. */
 size_t mpo_gp_score_ws_bytes(const MpoGpModel* model, int64_t m, int k);
 

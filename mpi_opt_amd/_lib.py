@@ -76,6 +76,8 @@ SIGNATURES = {
     "mpo_gp_prepare": (_I, [_P, _P, _I, _I, _P, _D, _D, _D, _D, ctypes.POINTER(MpoGpModel), _P, _SZ, _P]),
     "mpo_gp_lml_ws_bytes": (_SZ, [_I, _I, _I]),
     "mpo_gp_lml_grad": (_I, [_P, _P, _I, _I, _P, _I, _P, _P, _P, _P, _SZ, _P]),
+    "mpo_gp_lml_io_bytes": (_SZ, [_I, _I]),
+    "mpo_gp_lml_grad_host": (_I, [_P, _P, _I, _I, _P, _I, _P, _P, _SZ, _P, _SZ, _P]),
     "mpo_gp_score_ws_bytes": (_SZ, [ctypes.POINTER(MpoGpModel), _I64, _I]),
     "mpo_gp_acq_score": (_I, [ctypes.POINTER(MpoGpModel), _P, _I64, _D, _D, _D, _U, _P, _P, _P, _I, _P, _P,
                               _P, _SZ, _P]),

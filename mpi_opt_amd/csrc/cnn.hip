@@ -90,7 +90,22 @@ struct StepArgs {
     int* correct;            // [n_members] running correct count (eval)
     long long zero_off;      // 64 zero floats in the activation arena (DMA source past row ends)
     int debug;               // diagnostics only (env MPO_POP_DEBUG): 1 skip conv MMA loops, 2 skip conv staging
+    int xcd;                 // 1: XCD-grouped work-item order (xcd_item); env MPO_XCD_SWIZZLE=0 turns it off
 };
+
+// Work item of this workgroup.  Items are member-major; workgroups are dealt
+// round-robin over the 8 XCDs (blocks b and b + 8 share one: MI355X_MICROARCH.md,
+// "Workgroup dispatch"), so the identity order spreads every member's items --
+// and the L2 fetches of its weights and activations -- over all 8 XCD L2s.  The
+// bijective remap gives XCD group x a contiguous run of items instead (guide T1),
+// so a member's items share one L2.  Placement is a speed choice only: any
+// permutation computes the same results.
+__device__ __forceinline__ int xcd_item(int on) {
+    const int b = blockIdx.x;
+    if (!on) return b;
+    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, x = b & 7, slot = b >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + slot;
+}
 
 // ---- dropout counter hash (identical in oracle/cnn.py) ---------------------
 __device__ __forceinline__ unsigned lowbias32(unsigned x) {
@@ -229,7 +244,7 @@ __device__ __forceinline__ void conv_fwd_loop(const float* __restrict__ img, con
 template <int OP, int NT>
 __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvItem* __restrict__ items) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const ConvItem it = items[blockIdx.x];
+    const ConvItem it = items[xcd_item(a.xcd)];
     const Member& mb = a.mem[it.member];
     const int k = mb.k, F = mb.F;
     int Hin, Cin, Ho;
@@ -350,7 +365,7 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
 template <int NT>
 __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvItem* __restrict__ items) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const ConvItem it = items[blockIdx.x];
+    const ConvItem it = items[xcd_item(a.xcd)];
     const Member& mb = a.mem[it.member];
     const int k = mb.k, F = mb.F, H2 = mb.H2, Ho = mb.H1;
     const int pad = k - 1;
@@ -588,7 +603,7 @@ __device__ __forceinline__ void wgrad_row(const float* __restrict__ img, const f
 template <int OP, int NT, int MT>
 __global__ __launch_bounds__(kWgThreads) void conv_wgrad_kernel(StepArgs a, const WgItem* __restrict__ items) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const WgItem it = items[blockIdx.x];
+    const WgItem it = items[xcd_item(a.xcd)];
     const Member& mb = a.mem[it.member];
     const int k = mb.k, F = mb.F;
     int Hin, Cin, Ho;
@@ -738,7 +753,7 @@ __host__ __device__ constexpr inline int w1_lds_floats(int nb, int mt, int nt) {
 template <int NT, int MT>
 __global__ __launch_bounds__(kW1Waves * 64) void conv1_wgrad_kernel(StepArgs a, const WgItem* __restrict__ items) {
     extern __shared__ __attribute__((aligned(16))) float sh[];   // images | slack | {0, 1}; then the reduction
-    const WgItem it = items[blockIdx.x];
+    const WgItem it = items[xcd_item(a.xcd)];
     const Member& mb = a.mem[it.member];
     const int k = mb.k, F = mb.F, Ho = mb.H1, Kw = k * k;
     const int tid = threadIdx.x, lane = tid & 63, krow = lane >> 4, kcol = lane & 15;
@@ -1326,6 +1341,7 @@ struct Plan {
     bool timer_detail = false;
     long long zero_off = 0;
     int debug = 0;
+    int xcd = 1;
     std::vector<Member> mem;
     long long n_params = 0, act_floats = 0;
     std::vector<ConvItem> conv1, conv2, dgrad;
@@ -1698,6 +1714,7 @@ StepArgs make_args(const Plan& P, const float* x, const int* labels, const int* 
     a.loss_sum = nullptr;
     a.correct = nullptr;
     a.debug = P.debug;
+    a.xcd = P.xcd;
     a.zero_off = P.zero_off;
     return a;
 }
@@ -1736,6 +1753,7 @@ int mpo_pop_create(const MpoCnnSpec* specs, int n_members, int batch, void** han
     auto P = std::make_unique<Plan>();
     P->timer.on = env_int("MPO_POP_PROFILE", 0) != 0;
     P->debug = env_int("MPO_POP_DEBUG", 0);
+    P->xcd = env_int("MPO_XCD_SWIZZLE", 1) != 0;
     P->timer_detail = env_int("MPO_POP_PROFILE", 0) > 1;
     int rc = build_plan(*P, specs, n_members, batch);
     if (rc) return rc;

@@ -946,7 +946,7 @@ __global__ __launch_bounds__(kFitThreads) void sw_pivot_kernel(LmlArgs a, int k)
     const SsPtrs p = ss_ptrs(a, b);
     __shared__ double Pb[kSwNb * kSwLd];   // pivot block rows of C
     __shared__ double Pi[kSwNb * kSwLd];   // P^-1
-    __shared__ double colb[kSwNb];         // the sweep's column broadcast
+    __shared__ double rowb[kSwNb];         // the sweep's pivot-row broadcast
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     // C_k: at k = 0 copied from A (row segments for rows >= k0, the block's rows
@@ -980,35 +980,41 @@ __global__ __launch_bounds__(kFitThreads) void sw_pivot_kernel(LmlArgs a, int k)
     if (a.stop == 21) return;   // diagnostics only (MPO_FIT_DEBUG): column copy alone
     if (wave == 0 && a.stop != 22) {
         // Gauss-Jordan sweep of the 32x32 pivot block by wave 0: lane l + 32 h holds
-        // columns [16 h, 16 h + 16) of row l.  The swept block stays symmetric, so the
-        // pivot row c is column c: at step c every row writes its column-c entry to the
-        // LDS and every lane reads the half of that column it needs (broadcast reads;
-        // LDS operations of one wave complete in order) -- 16 FMAs per lane and step
-        // instead of a 31-readlane chain per step.
+        // columns [16 h, 16 h + 16) of row l.  At step c the pivot row (lanes c and
+        // c + 32) goes through the LDS and every lane reads the half it needs
+        // (broadcast reads; LDS operations of one wave complete in order); a row's
+        // column-c entry comes from its other half-lane by a lane permute.  The same
+        // arithmetic in the same order as the readlane form (the pivot row, not the
+        // symmetric column: eliminating with the column's rounding measured 10-100x
+        // less accurate at cond(K) ~ 1e5), 16 FMAs per lane and step.
         const int l = lane & 31, h = lane >> 5;
         double r[16];
 #pragma unroll
         for (int jj = 0; jj < 16; ++jj) r[jj] = Pb[l * kSwLd + 16 * h + jj];
         double prod = 1.0;
         int bad = 0;
-        const double* colh = colb + 16 * h;
+        const double* rowh = rowb + 16 * h;
 #pragma unroll
         for (int c = 0; c < kSwNb; ++c) {
             const int hc = c >> 4, jc = c & 15;
-            if (h == hc) colb[l] = r[jc];
+            if (l == c) {
+#pragma unroll
+                for (int jj = 0; jj < 16; ++jj) rowb[16 * h + jj] = r[jj];
+            }
+            const double colv = __shfl(r[jc], l + 32 * hc);   // A[l][c], held by the half-lane of column c
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            const double pv = colb[c];
+            const double pv = rowb[c];
             if (!(pv > 0.0) || !isfinite(pv)) bad = bad ? bad : c + 1;
             prod *= pv;
             const double ip = 1.0 / pv;
             const bool piv = l == c;
-            const double t = colb[l] * ip;
-            double cj[16];
+            const double t = colv * ip;
+            double pj[16];
 #pragma unroll
-            for (int jj = 0; jj < 16; ++jj) cj[jj] = colh[jj];
+            for (int jj = 0; jj < 16; ++jj) pj[jj] = rowh[jj];
 #pragma unroll
             for (int jj = 0; jj < 16; ++jj) {
-                const double upd = piv ? r[jj] * ip : fma(-t, cj[jj], r[jj]);
+                const double upd = piv ? r[jj] * ip : fma(-t, pj[jj], r[jj]);
                 if (jj == jc) r[jj] = h == hc ? (piv ? -ip : t) : upd;
                 else r[jj] = upd;
             }
@@ -1361,6 +1367,36 @@ int mpo_gp_lml_grad(const double* X, const double* y_norm, int n, int d, const d
         case 16: return launch_lml<false, 16>(a, batch, s);
         default: return launch_lml<false, 32>(a, batch, s);
     }
+    MPO_GUARD_END
+}
+
+size_t mpo_gp_lml_io_bytes(int d, int batch) {
+    if (d <= 0 || batch <= 0) return 0;
+    const size_t k = (size_t)d + 2;
+    return ((size_t)batch * k + (size_t)batch + (size_t)batch * k + ((size_t)batch + 1) / 2) * sizeof(double);
+}
+
+int mpo_gp_lml_grad_host(const double* X, const double* y_norm, int n, int d, const double* theta_host, int batch,
+                         double* out_host, void* dev_io, size_t io_bytes, void* ws, size_t ws_bytes, void* stream) {
+    MPO_GUARD_BEGIN
+    MPO_CHECK_ARG(theta_host && out_host && dev_io, "mpo_gp_lml_grad_host: null pointer");
+    MPO_CHECK_ARG(d > 0 && batch > 0, "mpo_gp_lml_grad_host: bad shape d=%d batch=%d", d, batch);
+    MPO_CHECK_ARG(io_bytes >= mpo_gp_lml_io_bytes(d, batch), "mpo_gp_lml_grad_host: io buffer too small (%zu < %zu)",
+                  io_bytes, mpo_gp_lml_io_bytes(d, batch));
+    const size_t k = (size_t)d + 2;
+    double* th = static_cast<double*>(dev_io);
+    double* out = th + (size_t)batch * k;                  // lml | grad | info, as out_host
+    double* lml = out;
+    double* grad = out + batch;
+    int32_t* info = reinterpret_cast<int32_t*>(grad + (size_t)batch * k);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    MPO_HIP(hipMemcpyAsync(th, theta_host, (size_t)batch * k * sizeof(double), hipMemcpyHostToDevice, s));
+    const int rc = mpo_gp_lml_grad(X, y_norm, n, d, th, batch, lml, grad, info, ws, ws_bytes, stream);
+    if (rc != MPO_OK) return rc;
+    const size_t out_bytes = ((size_t)batch + (size_t)batch * k + ((size_t)batch + 1) / 2) * sizeof(double);
+    MPO_HIP(hipMemcpyAsync(out_host, out, out_bytes, hipMemcpyDeviceToHost, s));
+    MPO_HIP(hipStreamSynchronize(s));
+    return MPO_OK;
     MPO_GUARD_END
 }
 

@@ -136,6 +136,33 @@ def flops_per_sample_train(layers):
     return 3 * flops_per_sample_fwd(layers) - 2 * 9 * c0["cin"] * c0["cout"] * c0["H"] * c0["W"]
 
 
+def hbm_bytes_train(layers, batch, n_params):
+    """Algorithmic HBM bytes of one train step of one member over ``batch``
+    samples (f32), every tensor written once and read once per consuming kernel:
+    forward -- each layer reads its input channels (BN + ELU folded into the
+    consumer) and writes its output channels, the transition's AvgPool reads the
+    conv output and writes the pooled stage; backward -- each layer reads its
+    output gradient and its input (for the weight gradient and the BN / ELU
+    derivative), writes its input gradient (not for the initial conv), the pool
+    reads / writes the gradient once; per member the parameters are read twice
+    (forward, backward), the gradient written and read, Adam's m and v read and
+    written and the parameters written (8 passes)."""
+    per_sample = 0
+    for ly in layers:
+        hw = ly["H"] * ly["W"]
+        if ly["kind"] == "head":
+            per_sample += hw * ly["cin"] * 2 + hw * ly["cin"] * 2      # GAP read fwd; dGAP fold + input read bwd
+            continue
+        per_sample += hw * (ly["cin"] + ly["cout"])                    # forward
+        per_sample += hw * (ly["cout"] + ly["cin"])                    # backward: dOut, input for wgrad / BN
+        if ly["kind"] != "conv0":
+            per_sample += hw * ly["cin"]                               # input gradient
+        if ly["kind"] == "trans":
+            q = (ly["H"] // 2) * (ly["W"] // 2) * ly["cout"]
+            per_sample += 2 * (hw * ly["cout"] + q)                    # AvgPool2 forward + backward
+    return 4 * (batch * per_sample + 8 * n_params)
+
+
 class DenseNetPopulation:
     """``n`` same-architecture DenseNet members resident on one GPU."""
 

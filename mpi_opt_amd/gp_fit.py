@@ -57,6 +57,7 @@ class DeviceLML:
         self.n, self.d = X.shape
         self.X = torch.from_numpy(X).to(self.device)
         self.y = torch.from_numpy(np.ascontiguousarray(y_norm, dtype=np.float64)).to(self.device)
+        self._stream = _lib.stream_handle(self.device)
         self._cap = 0
 
     def _ensure(self, batch):
@@ -67,39 +68,37 @@ class DeviceLML:
         if self.ws_bytes == 0:
             raise _lib.MpoError(f"mpo_gp_lml_grad: n={self.n} d={self.d} unsupported")
         self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
-        self.theta_d = torch.empty((batch, self.d + 2), dtype=torch.float64, device=self.device)
-        # lml | grad | info in ONE device buffer: one device-to-host copy (one sync)
-        # per L-BFGS iteration instead of three
+        self.io_bytes = int(L.mpo_gp_lml_io_bytes(self.d, batch))
+        self.io = torch.empty(self.io_bytes, dtype=torch.uint8, device=self.device)
         k = self.d + 2
-        self.out_d = torch.empty(batch * (k + 2), dtype=torch.float64, device=self.device)
-        self.lml_d = self.out_d[:batch]
-        self.grad_d = self.out_d[batch:batch * (k + 1)].view(batch, k)
-        self.info_d = self.out_d[batch * (k + 1):].view(torch.int32)[:batch]
+        # device views of the io buffer at full capacity (direct mpo_gp_lml_grad timing in bench / probes)
+        io = self.io.view(torch.float64)
+        self.theta_d = io[:batch * k].view(batch, k)
+        self.lml_d = io[batch * k:batch * (k + 1)]
+        self.grad_d = io[batch * (k + 1):batch * (2 * k + 1)].view(batch, k)
+        self.info_d = io[batch * (2 * k + 1):].view(torch.int32)[:batch]
+        # host side of one round: theta in, lml | grad | info out (pinned)
         self.theta_h = torch.empty((batch, k), dtype=torch.float64).pin_memory()
-        self.out_h = torch.empty(batch * (k + 2), dtype=torch.float64).pin_memory()
+        self.out_h = torch.empty(batch * (k + 1) + (batch + 1) // 2, dtype=torch.float64).pin_memory()
         self._cap = batch
 
     def evaluate(self, thetas):
-        """thetas [B, d+2] (log space) -> (lml [B], grad [B, d+2], info [B]) as numpy."""
+        """thetas [B, d+2] (log space) -> (lml [B], grad [B, d+2], info [B]) as numpy:
+        one ``mpo_gp_lml_grad_host`` call (copy in, objective, copy out, sync)."""
         thetas = np.ascontiguousarray(np.atleast_2d(np.asarray(thetas, dtype=np.float64)))
         B = thetas.shape[0]
         if thetas.shape[1] != self.d + 2:
             raise ValueError(f"theta has {thetas.shape[1]} entries, expected d+2={self.d + 2}")
-        # runs on the lockstep worker threads, whose current HIP device is the
-        # thread-local default: pin this objective's device for the launch
-        with torch.cuda.device(self.device):
-            self._ensure(B)
-            k, cap = self.d + 2, self._cap
-            self.theta_h[:B].numpy()[:] = thetas
-            self.theta_d[:B].copy_(self.theta_h[:B], non_blocking=True)
-            _lib.check(_lib.lib().mpo_gp_lml_grad(
-                _lib.ptr(self.X), _lib.ptr(self.y), self.n, self.d, _lib.ptr(self.theta_d), B,
-                _lib.ptr(self.lml_d), _lib.ptr(self.grad_d), _lib.ptr(self.info_d),
-                _lib.ptr(self.ws), self.ws_bytes, _lib.stream_handle(self.device)), "mpo_gp_lml_grad")
-            self.out_h.copy_(self.out_d)          # synchronising copy of all outputs
-            h = self.out_h.numpy()
-            return (h[:B].copy(), h[cap:cap + B * k].reshape(B, k).copy(),
-                    h[cap * (k + 1):].view(np.int32)[:B].copy())
+        self._ensure(B)
+        k = self.d + 2
+        th = self.theta_h.numpy()
+        th[:B] = thetas
+        _lib.check(_lib.lib().mpo_gp_lml_grad_host(
+            _lib.ptr(self.X), _lib.ptr(self.y), self.n, self.d, self.theta_h.data_ptr(), B,
+            self.out_h.data_ptr(), _lib.ptr(self.io), self.io_bytes, _lib.ptr(self.ws), self.ws_bytes,
+            self._stream), "mpo_gp_lml_grad_host")
+        h = self.out_h.numpy()
+        return (h[:B].copy(), h[B:B + B * k].reshape(B, k).copy(), h[B + B * k:].view(np.int32)[:B].copy())
 
 
 # scipy's L-BFGS-B defaults as ``minimize(method="L-BFGS-B")`` and ``fmin_l_bfgs_b`` pass them

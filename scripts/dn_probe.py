@@ -15,6 +15,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--members", type=int, default=32)
 ap.add_argument("--batch", type=int, default=100)
 ap.add_argument("--steps", type=int, default=10)
+ap.add_argument("--no-eval", action="store_true", help="train steps only (the bench's PMC traffic passes)")
 args = ap.parse_args()
 
 x, y = synthetic_cifar(n=5000, seed=0)
@@ -29,6 +30,9 @@ for s in range(args.steps):
     pop.train_step(x, y, order, (s % 40) * args.batch)
 torch.cuda.synchronize()
 tt = (time.time() - t0) / args.steps
+if args.no_eval:
+    print(f"members {args.members} batch {args.batch}: train {tt*1e3:.2f} ms", flush=True)
+    sys.exit(0)
 t0 = time.time()
 for s in range(args.steps):
     pop.eval_step(x, y, order, (s % 40) * args.batch)
