@@ -90,7 +90,7 @@ struct StepArgs {
     int* correct;            // [n_members] running correct count (eval)
     long long zero_off;      // 64 zero floats in the activation arena (DMA source past row ends)
     int debug;               // diagnostics only (env MPO_POP_DEBUG): 1 skip conv MMA loops, 2 skip conv staging
-    int xcd;                 // 1: XCD-grouped work-item order (xcd_item); env MPO_XCD_SWIZZLE=0 turns it off
+    int xcd;                 // 1: XCD-grouped work-item order (xcd_item, env MPO_XCD_SWIZZLE=1); off by default
 };
 
 // Work item of this workgroup.  Items are member-major; workgroups are dealt
@@ -1341,7 +1341,7 @@ struct Plan {
     bool timer_detail = false;
     long long zero_off = 0;
     int debug = 0;
-    int xcd = 1;
+    int xcd = 0;
     std::vector<Member> mem;
     long long n_params = 0, act_floats = 0;
     std::vector<ConvItem> conv1, conv2, dgrad;
@@ -1753,7 +1753,7 @@ int mpo_pop_create(const MpoCnnSpec* specs, int n_members, int batch, void** han
     auto P = std::make_unique<Plan>();
     P->timer.on = env_int("MPO_POP_PROFILE", 0) != 0;
     P->debug = env_int("MPO_POP_DEBUG", 0);
-    P->xcd = env_int("MPO_XCD_SWIZZLE", 1) != 0;
+    P->xcd = env_int("MPO_XCD_SWIZZLE", 0) != 0;   // measured 21% slower on (profiles/r03/train_xcd*_e.json)
     P->timer_detail = env_int("MPO_POP_PROFILE", 0) > 1;
     int rc = build_plan(*P, specs, n_members, batch);
     if (rc) return rc;

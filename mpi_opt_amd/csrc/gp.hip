@@ -1127,10 +1127,12 @@ hipError_t blocked_factor(const double* xs, int n, int dp, double amp, double di
 //   dk_i/dx_j  = c_i (x_j - X_ij) / ls_j^2,  c_i = -(5/3) amp (1 + t_i) e^-t_i
 //   dmu/dx     = y_std dk^T alpha
 //   dsd/dx     = -y_std dk^T (W^T W k*) / sd_n,  W = L^-1
-// LDS: k*, c (n each), v = W k* (n), four per-wave partials of W^T v (4 n).
-constexpr int kGradThreads = 256;
-
-__global__ __launch_bounds__(kGradThreads) void acq_grad_kernel(
+// LDS: k*, c (n each), v = W k* (n), one per-wave partial of W^T v per wave (NW n).
+// NW = 16 waves per point while (3 + NW) n doubles fit the LDS (n <= ~1000; the
+// 4-wave form past it): the two triangular mat-vecs are the kernel's serial work,
+// 16 waves cut them 4x (n = 512: 214 -> see DESIGN §3.1b round trip per launch).
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void acq_grad_kernel(
         int n, int d, int dp, double amp, double y_mean, double y_std, const double* __restrict__ xs,
         const double* __restrict__ ls, const double* __restrict__ alpha, const double* __restrict__ W,
         const double* __restrict__ x, const int32_t* __restrict__ acq, double y_opt, double xi, double kappa,
@@ -1139,10 +1141,11 @@ __global__ __launch_bounds__(kGradThreads) void acq_grad_kernel(
     double* kk = sm;              // [n]
     double* cc = kk + n;          // [n]
     double* vv = cc + n;          // [n]
-    double* up = vv + n;          // [4][n]
+    double* up = vv + n;          // [NW][n]
     __shared__ double xp[32];     // x / ls
+    constexpr int kGradThreads = NW * 64, kGroups = kGradThreads / 32;
     __shared__ double red[kGradThreads];
-    __shared__ double ga[8][32], gu[8][32];
+    __shared__ double ga[kGroups][32], gu[kGroups][32];
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid < 32) xp[tid] = tid < d ? x[(size_t)b * d + tid] / ls[tid] : 0.0;
     __syncthreads();
@@ -1162,12 +1165,12 @@ __global__ __launch_bounds__(kGradThreads) void acq_grad_kernel(
         cc[i] = (-5.0 / 3.0) * amp * (1.0 + t) * e;
         mu_part = fma(k, alpha[i], mu_part);
     }
-    for (int i = tid; i < 4 * n; i += kGradThreads) up[i] = 0.0;
+    for (int i = tid; i < NW * n; i += kGradThreads) up[i] = 0.0;
     __syncthreads();
 
     // v = W k* (rows per wave, lanes across the row), q = ||v||^2
     double q_part = 0.0;
-    for (int r = wave; r < n; r += 4) {
+    for (int r = wave; r < n; r += NW) {
         double s = 0.0;
         for (int c = lane; c <= r; c += 64) s = fma(W[(size_t)r * n + c], kk[c], s);
 #pragma unroll
@@ -1178,14 +1181,19 @@ __global__ __launch_bounds__(kGradThreads) void acq_grad_kernel(
     if (lane != 0) q_part = 0.0;
     __syncthreads();
 
-    // u = W^T v: wave w accumulates rows r = w (mod 4) into its own partial
+    // u = W^T v: wave w accumulates rows r = w (mod NW) into its own partial
     double* uw = up + (size_t)wave * n;
-    for (int r = wave; r < n; r += 4) {
+    for (int r = wave; r < n; r += NW) {
         const double vr = vv[r];
         for (int c = lane; c <= r; c += 64) uw[c] = fma(W[(size_t)r * n + c], vr, uw[c]);
     }
     __syncthreads();
-    for (int i = tid; i < n; i += kGradThreads) up[i] = (up[i] + up[n + i]) + (up[2 * n + i] + up[3 * n + i]);
+    for (int i = tid; i < n; i += kGradThreads) {
+        double u = up[i];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) u += up[(size_t)w * n + i];
+        up[i] = u;
+    }
 
     // block sums of mu_n and q
     red[tid] = mu_part;
@@ -1204,12 +1212,12 @@ __global__ __launch_bounds__(kGradThreads) void acq_grad_kernel(
     }
     const double q = red[0];
 
-    // dk^T alpha and dk^T u per dimension: thread (grp, j) sums observations grp (mod 8)
+    // dk^T alpha and dk^T u per dimension: thread (grp, j) sums observations grp (mod kGroups)
     {
         const int j = tid & 31, grp = tid >> 5;
         double sa = 0.0, su = 0.0;
         if (j < d) {
-            for (int i = grp; i < n; i += 8) {
+            for (int i = grp; i < n; i += kGroups) {
                 const double t = cc[i] * (xp[j] - xs[(size_t)i * dp + j]);
                 sa = fma(t, alpha[i], sa);
                 su = fma(t, up[i], su);
@@ -1223,7 +1231,7 @@ __global__ __launch_bounds__(kGradThreads) void acq_grad_kernel(
     if (tid < d) {
         const int j = tid;
         double sa = 0.0, su = 0.0;
-        for (int grp = 0; grp < 8; ++grp) {
+        for (int grp = 0; grp < kGroups; ++grp) {
             sa += ga[grp][j];
             su += gu[grp][j];
         }
@@ -1571,11 +1579,14 @@ int mpo_gp_acq_grad(const MpoGpModel* model, const double* x, int batch, const i
     MPO_CHECK_ARG(model && x && acq && f && g, "mpo_gp_acq_grad: null pointer");
     MPO_CHECK_ARG(batch > 0 && batch <= 65535, "mpo_gp_acq_grad: batch=%d outside [1, 65535]", batch);
     MPO_CHECK_ARG(model->n > 0 && model->d > 0 && model->d <= 32 && model->W, "mpo_gp_acq_grad: model not prepared");
-    const size_t lds = (size_t)7 * model->n * sizeof(double);
-    if (lds > kMaxLds - 8192) { mpo::set_error("mpo_gp_acq_grad: n=%d too large", model->n); return MPO_ENOTSUP; }
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(acq_grad_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(acq_grad_kernel, dim3(batch), dim3(kGradThreads), lds, static_cast<hipStream_t>(stream),
+    // static LDS of the 16-wave form: red[1024] + ga / gu [32][32] doubles = 24 KiB
+    const size_t lds16 = (size_t)19 * model->n * sizeof(double), lds4 = (size_t)7 * model->n * sizeof(double);
+    const bool wide = lds16 + (24 << 10) <= kMaxLds;
+    const size_t lds = wide ? lds16 : lds4;
+    if (lds4 > kMaxLds - 8192) { mpo::set_error("mpo_gp_acq_grad: n=%d too large", model->n); return MPO_ENOTSUP; }
+    auto kern = wide ? acq_grad_kernel<16> : acq_grad_kernel<4>;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(batch), dim3(wide ? 1024 : 256), lds, static_cast<hipStream_t>(stream),
                        model->n, model->d, model->dp, model->amp, model->y_mean, model->y_std, model->xs, model->ls,
                        model->alpha, model->W, x, acq, y_opt, xi, kappa, f, g);
     MPO_LAUNCH_CHECK();

@@ -87,6 +87,7 @@ int main() {
             (void)mpo_gp_lml_ws_bytes(n, d, 3);
         }
     EXPECT(mpo_gp_lml_ws_bytes(0, 10, 3) == 0 && mpo_gp_lml_ws_bytes(10, 40, 3) == 0);
+    EXPECT(mpo_gp_lml_io_bytes(5, 3) == (3 * 7 + 3 + 3 * 7 + 2) * sizeof(double) && mpo_gp_lml_io_bytes(0, 3) == 0);
     MpoGpModel gm{};
     gm.n = 200; gm.d = 10; gm.dp = 12; gm.np16 = 208;
     EXPECT(mpo_gp_score_ws_bytes(&gm, 1000000, 5) > 0);
@@ -96,6 +97,8 @@ int main() {
     int32_t info = 0;
     EXPECT(mpo_gp_prepare(nullptr, dummy, 1, 1, dummy, 1.0, 0.1, 0.0, 1.0, &gm, dummy, 8, nullptr) != 0);
     EXPECT(mpo_gp_lml_grad(dummy, dummy, 0, 1, dummy, 1, dummy, dummy, &info, dummy, 8, nullptr) != 0);
+    EXPECT(mpo_gp_lml_grad_host(dummy, dummy, 4, 1, nullptr, 1, dummy, dummy, 8, dummy, 8, nullptr) != 0);
+    EXPECT(mpo_gp_lml_grad_host(dummy, dummy, 4, 1, dummy, 1, dummy, dummy, 8, dummy, 8, nullptr) != 0);  // io too small
     EXPECT(mpo_gp_acq_score(&gm, dummy, 10, 0.0, 0.01, 1.96, 1, nullptr, nullptr, nullptr, MPO_TOPK_MAX + 1,
                             nullptr, nullptr, dummy, 8, nullptr) != 0);
     EXPECT(mpo_gp_acq_grad(&gm, dummy, 0, nullptr, 0.0, 0.01, 1.96, dummy, dummy, nullptr) != 0);
