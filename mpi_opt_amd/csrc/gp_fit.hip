@@ -834,12 +834,12 @@ __global__ __launch_bounds__(kFitThreads) void lml_sweep_kernel(LmlArgs a) {
 // over the device.  The single-workgroup kernel runs every rank-32 trailing update
 // on ONE CU (2.45 ms per launch at n = 500: the n^3 MFMA work of a theta on 4
 // SIMDs); here each sweep step is two launches --
-//   sw_pivot_kernel   (one workgroup per theta) old block column C -> global,
-//                     pivot block swept by wave 0 (log det, failure flag
-//                     accumulate in the workspace), G = C P^-1 -> global;
+//   sw_pivot_kernel   (one wave per theta) pivot block of C_k swept in
+//                     registers, P^-1 -> global (log det, failure flag
+//                     accumulate in the workspace);
 //   sw_update_kernel  (many workgroups per theta, one 16x16 lower tile per wave
-//                     at a time) A_IJ -= G_I C_J^T outside block k, block
-//                     column k <- G, pivot block <- -P^-1
+//                     at a time) G_I = C_I P^-1 per wave, A_IJ -= G_I C_J^T
+//                     outside block k, block column k <- G, pivot block <- -P^-1
 // -- bracketed by sw_build_kernel (xs, K; many workgroups) and sw_finish_kernel
 // (alpha, the pair/gradient phase and the LML; one workgroup per theta).  Same
 // arithmetic in the same order as lml_sweep_kernel, so both give the same bits.
@@ -847,18 +847,18 @@ constexpr int kSplitMinN = 48;    // past it the split beats both single-workgro
 constexpr int kUpdThreads = 256;
 constexpr int kUpdTilesPerWave = 1;   // one lower tile per wave: latency-bound steps want many waves
 
-// per-theta workspace (doubles): xs | alpha | A [np][np] | G [np][32] | C0, C1 [np][32]
+// per-theta workspace (doubles): xs | alpha | A [np][np] | C0, C1 [np][32]
 // | P^-1 [32][32] | logdet, fail.  C_k (block column k before sweep k, row-major
 // [np][32]) lives in C[k & 1]: the update kernel of step k writes C_{k+1} as it
 // produces those entries, so the pivot kernel never re-reads a block column of A.
 __host__ __device__ inline long long ss_ws_doubles(int n, int d) {
     auto al = [](long long x) { return (x + 31) & ~31LL; };
     const long long np = sw_np(n);
-    return al((long long)n * d) + al(np) + np * np + 3 * np * kSwNb + kSwNb * kSwNb + 32;
+    return al((long long)n * d) + al(np) + np * np + 2 * np * kSwNb + kSwNb * kSwNb + 32;
 }
 
 struct SsPtrs {
-    double *xs, *alpha, *A, *G, *C0, *C1, *P, *acc;   // acc[0] = log det, acc[1] = failure column (as double)
+    double *xs, *alpha, *A, *C0, *C1, *P, *acc;   // acc[0] = log det, acc[1] = failure column (as double)
     __device__ double* C(int k) const { return (k & 1) ? C1 : C0; }
 };
 
@@ -869,8 +869,7 @@ __device__ __forceinline__ SsPtrs ss_ptrs(const LmlArgs& a, int b) {
     p.xs = a.ws + (long long)b * a.ws_stride;
     p.alpha = p.xs + al((long long)a.n * a.d);
     p.A = p.alpha + al(np);
-    p.G = p.A + np * np;
-    p.C0 = p.G + np * kSwNb;
+    p.C0 = p.A + np * np;
     p.C1 = p.C0 + np * kSwNb;
     p.P = p.C1 + np * kSwNb;
     p.acc = p.P + kSwNb * kSwNb;
@@ -936,151 +935,163 @@ __global__ __launch_bounds__(256) void sw_build_kernel(LmlArgs a) {
                 v = amp * ((1.0 + k + k * k / 3.0) * exp(-k));
             }
             p.A[(long long)i * np + j] = v;
+            // C_0 (block column 0 before sweep 0, row-major [np][32]) from the lower
+            // entries, as the pivot kernel once copied it out of A
+            if (j < kSwNb && j <= i) {
+                p.C0[(long long)i * kSwNb + j] = v;
+                if (i < kSwNb) p.C0[(long long)j * kSwNb + i] = v;
+            }
         }
     }
 }
 
-// grid (1, B), kFitThreads: steps a-c of sweep step k (see lml_sweep_kernel)
-__global__ __launch_bounds__(kFitThreads) void sw_pivot_kernel(LmlArgs a, int k) {
-    const int b = blockIdx.y, np = (int)sw_np(a.n), ntile = np / 16, k0 = k * kSwNb;
+// grid (1, B), one wave: steps a-b of sweep step k (see lml_sweep_kernel) -- the
+// 32x32 pivot block of C_k (written by the build kernel for k = 0, by the previous
+// update kernel after) swept in registers, P^-1 to the workspace.  A single wave
+// keeps the whole register file (r02's 1024-thread pivot kernel capped the sweep
+// at 128 VGPRs and spilled its rows to scratch); G = C P^-1 is formed per tile by
+// sw_update_kernel.
+__global__ __launch_bounds__(64) void sw_pivot_kernel(LmlArgs a, int k) {
+    const int b = blockIdx.y, k0 = k * kSwNb;
     const SsPtrs p = ss_ptrs(a, b);
-    __shared__ double Pb[kSwNb * kSwLd];   // pivot block rows of C
-    __shared__ double Pi[kSwNb * kSwLd];   // P^-1
     __shared__ double rowb[kSwNb];         // the sweep's pivot-row broadcast
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // C_k: at k = 0 copied from A (row segments for rows >= k0, the block's rows
-    // transposed for rows < k0; all of a thread's reads before its stores); for
-    // k > 0 the previous update kernel wrote it.  The pivot rows go to the LDS.
-    double* C = p.C(k);
-    if (k == 0) {
-        constexpr int kCopyBatch = 16;
-        for (int e0 = 0; e0 < np * kSwNb; e0 += kCopyBatch * kFitThreads) {
-            double v[kCopyBatch];
-            int dst[kCopyBatch];
+    const int lane = threadIdx.x;
+    const double* C = p.C(k);
+    if (a.stop == 21 || a.stop == 22) return;   // diagnostics only (MPO_FIT_DEBUG)
+    // Gauss-Jordan sweep of the 32x32 pivot block: lane l + 32 h holds columns
+    // [16 h, 16 h + 16) of row l.  At step c the pivot row (lanes c and c + 32) goes
+    // through the LDS and every lane reads the half it needs (broadcast reads; LDS
+    // operations of one wave complete in order); a row's column-c entry comes from
+    // its other half-lane by a lane permute.  The same arithmetic in the same order
+    // as the readlane form (the pivot row, not the symmetric column: eliminating
+    // with the column's rounding measured 10-100x less accurate at cond(K) ~ 1e5),
+    // 16 FMAs per lane and step.
+    const int l = lane & 31, h = lane >> 5;
+    double r[16];
 #pragma unroll
-            for (int u = 0; u < kCopyBatch; ++u) {
-                const int e = e0 + u * kFitThreads + tid;
-                dst[u] = -1;
-                if (e < np * kSwNb) {
-                    const int i = e >> 5, c = e & 31;
-                    v[u] = i >= c ? p.A[(long long)i * np + c] : p.A[(long long)c * np + i];
-                    dst[u] = e;
-                }
-            }
+    for (int jj = 0; jj < 16; ++jj) r[jj] = C[(long long)(k0 + l) * kSwNb + 16 * h + jj];
+    double prod = 1.0;
+    int bad = 0;
+    const double* rowh = rowb + 16 * h;
 #pragma unroll
-            for (int u = 0; u < kCopyBatch; ++u)
-                if (dst[u] >= 0) C[dst[u]] = v[u];
-        }
-        __threadfence_block();
-        __syncthreads();
-    }
-    for (int e = tid; e < kSwNb * kSwNb; e += kFitThreads) Pb[(e >> 5) * kSwLd + (e & 31)] = C[(long long)k0 * kSwNb + e];
-    __syncthreads();
-    if (a.stop == 21) return;   // diagnostics only (MPO_FIT_DEBUG): column copy alone
-    if (wave == 0 && a.stop != 22) {
-        // Gauss-Jordan sweep of the 32x32 pivot block by wave 0: lane l + 32 h holds
-        // columns [16 h, 16 h + 16) of row l.  At step c the pivot row (lanes c and
-        // c + 32) goes through the LDS and every lane reads the half it needs
-        // (broadcast reads; LDS operations of one wave complete in order); a row's
-        // column-c entry comes from its other half-lane by a lane permute.  The same
-        // arithmetic in the same order as the readlane form (the pivot row, not the
-        // symmetric column: eliminating with the column's rounding measured 10-100x
-        // less accurate at cond(K) ~ 1e5), 16 FMAs per lane and step.
-        const int l = lane & 31, h = lane >> 5;
-        double r[16];
-#pragma unroll
-        for (int jj = 0; jj < 16; ++jj) r[jj] = Pb[l * kSwLd + 16 * h + jj];
-        double prod = 1.0;
-        int bad = 0;
-        const double* rowh = rowb + 16 * h;
-#pragma unroll
-        for (int c = 0; c < kSwNb; ++c) {
-            const int hc = c >> 4, jc = c & 15;
-            if (l == c) {
-#pragma unroll
-                for (int jj = 0; jj < 16; ++jj) rowb[16 * h + jj] = r[jj];
-            }
-            const double colv = __shfl(r[jc], l + 32 * hc);   // A[l][c], held by the half-lane of column c
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            const double pv = rowb[c];
-            if (!(pv > 0.0) || !isfinite(pv)) bad = bad ? bad : c + 1;
-            prod *= pv;
-            const double ip = 1.0 / pv;
-            const bool piv = l == c;
-            const double t = colv * ip;
-            double pj[16];
-#pragma unroll
-            for (int jj = 0; jj < 16; ++jj) pj[jj] = rowh[jj];
+    for (int c = 0; c < kSwNb; ++c) {
+        const int hc = c >> 4, jc = c & 15;
+        const double colv = __shfl(r[jc], l + 32 * hc);   // A[l][c], held by the half-lane of column c
+        const bool piv = l == c;
+        if (piv) {
+            // the pivot row goes to the LDS and its registers to zero, so that the
+            // one update form below gives r * ip on the pivot lanes (fma(ip, pj, 0)
+            // rounds the same product) and fma(-t, pj, r) elsewhere -- no per-element
+            // lane select (r02's form spent two v_cndmask per double on it)
 #pragma unroll
             for (int jj = 0; jj < 16; ++jj) {
-                const double upd = piv ? r[jj] * ip : fma(-t, pj[jj], r[jj]);
-                if (jj == jc) r[jj] = h == hc ? (piv ? -ip : t) : upd;
-                else r[jj] = upd;
+                rowb[16 * h + jj] = r[jj];
+                r[jj] = 0.0;
             }
-            asm volatile("" ::: "memory");
         }
-        if (lane < 64) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const double pv = rowb[c];
+        if (!(pv > 0.0) || !isfinite(pv)) bad = bad ? bad : c + 1;
+        prod *= pv;
+        const double ip = 1.0 / pv;
+        const double t = colv * ip;
+        const double f = piv ? ip : -t;
+        double pj[16];
 #pragma unroll
-            for (int jj = 0; jj < 16; ++jj) {
-                Pi[l * kSwLd + 16 * h + jj] = -r[jj];
-                p.P[l * kSwNb + 16 * h + jj] = -r[jj];
-            }
+        for (int jj = 0; jj < 16; ++jj) pj[jj] = rowh[jj];
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            const double upd = fma(f, pj[jj], r[jj]);
+            if (jj == jc) r[jj] = h == hc ? (piv ? -ip : t) : upd;
+            else r[jj] = upd;
         }
-        if (lane == 0) {
-            p.acc[0] += log(prod);
-            if (bad && p.acc[1] == 0.0) p.acc[1] = (double)(k0 + bad);
-        }
+        asm volatile("" ::: "memory");
     }
-    __syncthreads();
-    if (a.stop == 23) return;   // diagnostics only: no G phase
-    for (int R = wave; R < ntile; R += kFitWaves) {
-        if ((R >> 1) == k) continue;
-        f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-        const double* ar = C + (long long)(16 * R + (lane & 15)) * kSwNb + (lane >> 4);
-        const int br = (lane >> 4) * kSwLd + (lane & 15);
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks) {
-            const double av = ar[4 * ks];
-            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, Pi[br + 4 * ks * kSwLd], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, Pi[br + 4 * ks * kSwLd + 16], acc1, 0, 0, 0);
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int rr = (lane >> 4) + 4 * q, c0 = lane & 15, c1 = 16 + c0;
-            p.G[((long long)R * 8 + (c0 >> 2)) * 64 + rr + 16 * (c0 & 3)] = acc0[q];
-            p.G[((long long)R * 8 + (c1 >> 2)) * 64 + rr + 16 * (c1 & 3)] = acc1[q];
-        }
+    for (int jj = 0; jj < 16; ++jj) p.P[l * kSwNb + 16 * h + jj] = -r[jj];
+    if (lane == 0) {
+        p.acc[0] += log(prod);
+        if (bad && p.acc[1] == 0.0) p.acc[1] = (double)(k0 + bad);
     }
 }
 
-// grid (nwg, B), kUpdThreads: step d of sweep step k over this workgroup's waves
+// grid (nwg, B), kUpdThreads: steps c-d of sweep step k over this workgroup's
+// waves, one lower 16x16 tile (I, J) per wave at a time.  The wave forms its own
+// G_I = C_I P^-1 (16 MFMAs, the MFMA output turned into the A-operand layout
+// through the wave's LDS slice) instead of reading it from a separate G launch:
+// the same MFMA sequence, so the same bits, one launch per step fewer.  The
+// diagonal tile (I, I) also writes G_I into block column k of A (and row I's
+// entries of C_{k+1}); tile (I, I) of block k writes -P^-1 there.
 __global__ __launch_bounds__(kUpdThreads) void sw_update_kernel(LmlArgs a, int k) {
     const int b = blockIdx.y, np = (int)sw_np(a.n), ntile = np / 16, k0 = k * kSwNb;
     const SsPtrs p = ss_ptrs(a, b);
     const double* Cc = p.C(k);
+    __shared__ double gl[kUpdThreads / 64][16 * kSwNb];   // per wave: G_I, A-operand order
     // C_{k+1} (next block column, rows i, columns k1 .. k1+32) as its entries are
-    // produced: from the lower entries only (the pivot kernel's copy reads lower
-    // storage for both halves of a diagonal tile), so the bits match that copy
+    // produced: from the lower entries only (the build kernel's copy of C_0 reads
+    // lower storage for both halves of a diagonal tile), so the bits match that copy
     const int k1 = k0 + kSwNb;
     double* Cn = k1 < np ? p.C(k + 1) : nullptr;
     const int lane = threadIdx.x & 63;
-    const int gw = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kUpdThreads / 64) + (threadIdx.x >> 6)));
+    const int wv = threadIdx.x >> 6;
+    const int gw = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kUpdThreads / 64) + wv));
     const int nw = gridDim.x * (kUpdThreads / 64);
     const int nt_low = ntile * (ntile + 1) / 2;
+    double* g = gl[wv];
     for (int t = gw; t < nt_low; t += nw) {
         int I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
         while (I * (I + 1) / 2 > t) --I;
         while ((I + 1) * (I + 2) / 2 <= t) ++I;
         const int J = t - I * (I + 1) / 2;
-        if ((I >> 1) == k || (J >> 1) == k) continue;
+        if ((I >> 1) == k) {
+            if (I == J) {   // rows of block k: -P^-1
+#pragma unroll
+                for (int e = lane; e < 16 * kSwNb; e += 64) {
+                    const int i = 16 * I + (e >> 5), c = e & 31;
+                    p.A[(long long)i * np + k0 + c] = -p.P[(i - k0) * kSwNb + c];
+                }
+            }
+            continue;
+        }
+        if ((J >> 1) == k) continue;
+        // G_I = C_I P^-1 (r02's pivot-kernel G phase, per wave)
+        {
+            double av[8], b0[8], b1[8];
+            const double* ar = Cc + (long long)(16 * I + (lane & 15)) * kSwNb + (lane >> 4);
+            const double* br = p.P + (lane >> 4) * kSwNb + (lane & 15);
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) {
+                av[ks] = ar[4 * ks];
+                b0[ks] = br[4 * ks * kSwNb];
+                b1[ks] = br[4 * ks * kSwNb + 16];
+            }
+            f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) {
+                acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ks], b0[ks], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ks], b1[ks], acc1, 0, 0, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int rr = (lane >> 4) + 4 * q, c0 = lane & 15, c1 = 16 + c0;
+                g[(c0 >> 2) * 64 + rr + 16 * (c0 & 3)] = acc0[q];
+                g[(c1 >> 2) * 64 + rr + 16 * (c1 & 3)] = acc1[q];
+            }
+        }
         f64x4 acc;
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc[q] = p.A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)];
-        const double* cb = Cc + (long long)(16 * J + (lane & 15)) * kSwNb + (lane >> 4);
+        double cb[8];
+        const double* cr = Cc + (long long)(16 * J + (lane & 15)) * kSwNb + (lane >> 4);
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) cb[ks] = cr[4 * ks];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's G_I stores (LDS ops of one wave complete in order)
+        double ga[8];
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) ga[ks] = g[ks * 64 + lane];
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks)
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-p.G[((long long)I * 8 + ks) * 64 + lane], cb[4 * ks], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-ga[ks], cb[ks], acc, 0, 0, 0);
 #pragma unroll
         for (int q = 0; q < 4; ++q) p.A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)] = acc[q];
         if (Cn && ((J >> 1) == k + 1 || (I >> 1) == k + 1)) {
@@ -1092,18 +1103,20 @@ __global__ __launch_bounds__(kUpdThreads) void sw_update_kernel(LmlArgs a, int k
                 if ((i >> 5) == k + 1) Cn[(long long)j * kSwNb + (i - k1)] = acc[q];
             }
         }
-    }
-    for (long long e = (long long)blockIdx.x * kUpdThreads + threadIdx.x; e < (long long)np * kSwNb;
-         e += (long long)gridDim.x * kUpdThreads) {
-        const int i = (int)(e >> 5), c = (int)(e & 31), j = k0 + c;
-        if ((i >> 5) == k) {
-            p.A[(long long)i * np + j] = -p.P[(i - k0) * kSwNb + c];
-        } else {
-            const double gv = p.G[((long long)(i >> 4) * 8 + (c >> 2)) * 64 + (i & 15) + 16 * (c & 3)];
-            if (i > j) p.A[(long long)i * np + j] = gv;
-            else p.A[(long long)j * np + i] = gv;
-            if (Cn && (i >> 5) == k + 1) Cn[(long long)j * kSwNb + (i - k1)] = gv;   // row j < k1 of C_{k+1}
+        if (I == J) {
+            // block column k, rows 16 I .. 16 I + 15, <- G_I (lower storage: below
+            // block k at A[i][j], above it transposed at A[j][i]); a row of block k+1
+            // also gives row j of C_{k+1}
+#pragma unroll
+            for (int e = lane; e < 16 * kSwNb; e += 64) {
+                const int ri = e >> 5, c = e & 31, i = 16 * I + ri, j = k0 + c;
+                const double gv = g[(c >> 2) * 64 + ri + 16 * (c & 3)];
+                if (i > j) p.A[(long long)i * np + j] = gv;
+                else p.A[(long long)j * np + i] = gv;
+                if (Cn && (i >> 5) == k + 1) Cn[(long long)j * kSwNb + (i - k1)] = gv;
+            }
         }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the G_I reads before the next tile's stores
     }
 }
 
@@ -1236,7 +1249,7 @@ int launch_split(const LmlArgs& a, int B, hipStream_t s) {
     hipLaunchKernelGGL(sw_build_kernel<DP>, dim3(ntile, B), dim3(256), 0, s, a);
     MPO_LAUNCH_CHECK();
     for (int k = 0; k < nbk; ++k) {
-        hipLaunchKernelGGL(sw_pivot_kernel, dim3(1, B), dim3(kFitThreads), 0, s, a, k);
+        hipLaunchKernelGGL(sw_pivot_kernel, dim3(1, B), dim3(64), 0, s, a, k);
         MPO_LAUNCH_CHECK();
         hipLaunchKernelGGL(sw_update_kernel, dim3(nwg, B), dim3(kUpdThreads), 0, s, a, k);
         MPO_LAUNCH_CHECK();
