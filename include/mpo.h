@@ -71,8 +71,8 @@ typedef struct MpoGpModel {
     const int32_t* wmeta;  /* per-wave B-stream plan of wfrag (scoring kernel) */
     const double* xb;      /* [np16+32][dp] (-2 xs, 1, |xs|^2, 0..) + a guard flag, or NULL:
                               the MFMA form of the candidate-observation distance,
-                              set by mpo_gp_prepare when d + 2 <= dp and its
-                              rounding bound holds (see mpo_gp_prepare) */
+                              set by mpo_gp_prepare when d + 2 <= dp; the flag is
+                              the self-check's verdict (see mpo_gp_prepare) */
 } MpoGpModel;
 
 /* K(i,j) = amp * Matern52(|X_i/ls - X_j/ls|) + (i==j ? diag_add : 0).
@@ -95,11 +95,18 @@ size_t mpo_gp_prepare_ws_bytes(int n, int d);
 /* Build a GP posterior from observations and fitted hyper-parameters:
  *   xs = X/ls;  K = amp*Matern52 + (noise + 1e-10 jitter) I;  L = chol(K);
  *   W = L^-1;  alpha = L^-T L^-1 y_norm;  pack W for the scoring kernel.
- * When d + 2 <= dp and 16 eps (|c|^2 + |x|^2 <= 4) sqrt(n) (5/3) amp^1.5 / noise^1.5
- * <= 1e-9 (the worst-case relative error of sd^2 from the expanded distance),
- * model->xb is set and the scoring kernel forms |c - x|^2 = |c|^2 + |x|^2 - 2 c.x
- * on fp64 MFMA for candidate tiles with every |c|^2 <= 2 (observations: a device
- * flag for every |x|^2 <= 2); other tiles and models take the direct differences.
+ * When d + 2 <= dp, model->xb is set and the scoring kernel may form
+ * |c - x|^2 = |c|^2 + |x|^2 - 2 c.x on fp64 MFMA (absolute rounding error of a few
+ * eps (|c|^2 + |x|^2) instead of the direct form's eps |c - x|^2).  The guard is
+ * empirical, not a closed-form bound: (1) a device flag requires every |x/ls|^2 <= 2;
+ * (2) a prepare-time self-check scores the model's own observations both ways --
+ * r^2 = 0 on each one's own row and the smallest sd, the expansion's worst case --
+ * and clears the flag unless (mu_n, q) agree within 1e-10 (q relative to
+ * sd^2 = amp - q, mu_n relative to amp sum |alpha|); (3) per 16-candidate tile, the
+ * expanded form is used only when every |c/ls|^2 <= 2.  Any other tile or model
+ * takes the direct differences.  tests/test_gp_gpu.py checks the expanded path
+ * against the exact posterior at 1e-9 on the fixtures and on a small-noise,
+ * near-duplicate-observation problem.  MPO_GP_DIST=0 disables it.
  * X [n][d], y_norm [n], ls [d]: device.  `model` (host struct) receives
  * device pointers into `ws`, which must stay alive while the model is used.
  * Replaces GaussianProcessRegressor.fit's tail (sklearn _gpr.py:345-365) and

@@ -813,8 +813,8 @@ hipError_t launch_score_occ_md(const ScoreArgs& a, int nblocks, size_t lds, hipS
     }
 }
 
-// MD = 1 (the MFMA distance) when the model carries xb (d + 2 <= dp and the
-// rounding bound of mpo_gp_prepare holds); MPO_GP_DIST=0 forces the direct form
+// MD = 1 (the MFMA distance) when the model carries xb (d + 2 <= dp; the kernel
+// reads the self-check's device flag); MPO_GP_DIST=0 forces the direct form
 template <int DP, int D>
 hipError_t launch_score_occ(const ScoreArgs& a, int nblocks, size_t lds, hipStream_t s) {
     if constexpr (D + 2 <= DP) {

@@ -224,6 +224,47 @@ def test_expanded_distance_matches_direct(path, monkeypatch):
     assert np.array_equal(o0["topk"]["EI"][0].cpu().numpy(), o1["topk"]["EI"][0].cpu().numpy())
 
 
+@pytest.mark.parametrize("noise", [1e-3, 1e-5])
+def test_expanded_distance_small_noise_near_duplicates(noise, monkeypatch):
+    """the expanded distance is guarded empirically (observation norms,
+    the prepare-time self-check at the observations, candidate-tile norms), not by a
+    closed-form bound.  Stress it where W = L^-1 is large: small fitted noise (down
+    to skopt's WhiteKernel lower bound 1e-5) and pairs of near-duplicate
+    observations 1e-4 apart (cond(K) ~ 1e7), with candidates on, next to and
+    between the observations.  Whatever the self-check decides, the expanded path
+    is no worse than the direct one (within 2x + 1e-10), the direct one meets the
+    1e-9 bar or 4x what a plain fp64 evaluation achieves (at cond 1e7 fp64 itself
+    carries ~4e-10), and the top-5 agree."""
+    from mpi_opt_amd.gp import DeviceGP
+
+    rng = np.random.RandomState(11)
+    n, d = 120, 10
+    base = rng.uniform(size=(n // 2, d))
+    X = np.concatenate([base, base + 1e-4 * rng.randn(n // 2, d)])
+    y = np.sin(X @ rng.randn(d)) + 0.05 * rng.randn(n)
+    amp, ls = 2.3, np.linspace(0.5, 1.6, d)
+    C = np.concatenate([X[:40], X[:40] + 1e-3 * rng.randn(40, d), 0.5 * (X[:40] + X[40:80]),
+                        rng.uniform(size=(200, d))])
+    st = O.gp_from_theta(X, y, amp, ls, noise)
+    mu_x, sd_x = O.posterior_exact(st, C)
+    V = O.matern52(C, X, ls, amp) @ np.linalg.inv(st.L).T          # plain fp64 norm form
+    sd64 = np.sqrt(np.maximum(amp - (V * V).sum(1), 0.0)) * st.y_std
+    bar = max(1e-9, 4.0 * float(np.max(np.abs(sd64 - sd_x) / sd_x)))
+    out, err = {}, {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MPO_GP_DIST", mode)
+        g = DeviceGP(X, y, amp, ls, noise)
+        out[mode] = g.score(torch.from_numpy(C).cuda(), float(np.min(y)), acqs=("EI",), k=5)
+        if mode == "1":
+            assert g.model.xb and _xb_flag(g) in (0.0, 1.0)
+        sd = out[mode]["sd"].cpu().numpy()
+        mu = out[mode]["mu"].cpu().numpy()
+        err[mode] = (float(np.max(np.abs(sd - sd_x) / sd_x)), float(np.max(np.abs(mu - mu_x) / mu_scale(st, C))))
+    assert err["0"][0] < bar and err["0"][1] < 1e-9, err
+    assert err["1"][0] <= 2 * err["0"][0] + 1e-10 and err["1"][1] <= 2 * err["0"][1] + 1e-10, err
+    assert np.array_equal(out["0"]["topk"]["EI"][0].cpu().numpy(), out["1"]["topk"]["EI"][0].cpu().numpy())
+
+
 def test_expanded_distance_far_candidates_fall_back(monkeypatch):
     """Candidate tiles with |c/ls|^2 > kDistNorm take the direct form: candidates far
     outside [0,1]^d (where the expansion would lose digits) still match the exact
