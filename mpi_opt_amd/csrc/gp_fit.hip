@@ -945,33 +945,91 @@ __global__ __launch_bounds__(256) void sw_build_kernel(LmlArgs a) {
     }
 }
 
+// grid (np/16, B), 1024 threads, dynamic LDS (16 bx + 16) x DP doubles: sw_xs_kernel
+// and sw_build_kernel in one launch.  The workgroup divides the X rows its K rows
+// need into the LDS (the same X / ls division as sw_xs_kernel), writes its own 16
+// rows of xs for the pair kernel, and builds K rows [16 bx, 16 bx + 16) one row per
+// wave with sw_build_kernel's arithmetic (the same bits).  Workgroup 0 resets the
+// log det / failure accumulators and the pair kernel's arrival counter.
+template <int DP>
+__global__ __launch_bounds__(1024) void sw_xs_build_kernel(LmlArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double xsl[];   // [rows][DP]
+    const int b = blockIdx.y, n = a.n, d = a.d, np = (int)sw_np(n);
+    const SsPtrs p = ss_ptrs(a, b);
+    double amp, noise, ls[DP];
+    ss_theta<DP>(a, b, amp, noise, ls);
+    const int rows = min(n, 16 * (int)blockIdx.x + 16);
+    for (int e = threadIdx.x; e < rows * d; e += blockDim.x) {
+        const int i = e / d, c = e % d;
+        double lc = 1.0;
+#pragma unroll
+        for (int q = 0; q < DP; ++q)
+            if (q == c) lc = ls[q];
+        const double v = a.X[e] / lc;
+        xsl[i * DP + c] = v;
+        if (i >= 16 * (int)blockIdx.x) p.xs[e] = v;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        p.acc[0] = 0.0;
+        p.acc[1] = 0.0;
+        *reinterpret_cast<unsigned*>(p.acc + 2) = 0u;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int i = 16 * blockIdx.x + wave;
+    double xi[DP];
+#pragma unroll
+    for (int c = 0; c < DP; ++c) xi[c] = (c < d && i < n) ? xsl[i * DP + c] : 0.0;
+    const int jend = (i | 15) + 1;
+    for (int j = lane; j < jend && j < np; j += 64) {
+        double v;
+        if (i >= n || j >= n) {
+            v = i == j ? 1.0 : 0.0;
+        } else if (i == j) {
+            v = amp * 1.0 + noise + kFitJitter;
+        } else {
+            double r2 = 0.0;
+#pragma unroll
+            for (int c = 0; c < DP; ++c)
+                if (c < d) {
+                    const double t = xi[c] - xsl[j * DP + c];
+                    r2 += t * t;
+                }
+            const double k = sqrt(r2) * kSqrt5;
+            v = amp * ((1.0 + k + k * k / 3.0) * exp(-k));
+        }
+        p.A[(long long)i * np + j] = v;
+        if (j < kSwNb && j <= i) {
+            p.C0[(long long)i * kSwNb + j] = v;
+            if (i < kSwNb) p.C0[(long long)j * kSwNb + i] = v;
+        }
+    }
+}
+
 // grid (1, B), one wave: steps a-b of sweep step k (see lml_sweep_kernel) -- the
 // 32x32 pivot block of C_k (written by the build kernel for k = 0, by the previous
 // update kernel after) swept in registers, P^-1 to the workspace.  A single wave
 // keeps the whole register file (r02's 1024-thread pivot kernel capped the sweep
 // at 128 VGPRs and spilled its rows to scratch); G = C P^-1 is formed per tile by
 // sw_update_kernel.
-__global__ __launch_bounds__(64) void sw_pivot_kernel(LmlArgs a, int k) {
-    const int b = blockIdx.y, k0 = k * kSwNb;
-    const SsPtrs p = ss_ptrs(a, b);
-    __shared__ double rowb[kSwNb];         // the sweep's pivot-row broadcast
-    const int lane = threadIdx.x;
-    const double* C = p.C(k);
-    if (a.stop == 21 || a.stop == 22) return;   // diagnostics only (MPO_FIT_DEBUG)
-    // Gauss-Jordan sweep of the 32x32 pivot block: lane l + 32 h holds columns
-    // [16 h, 16 h + 16) of row l.  At step c the pivot row (lanes c and c + 32) goes
-    // through the LDS and every lane reads the half it needs (broadcast reads; LDS
-    // operations of one wave complete in order); a row's column-c entry comes from
-    // its other half-lane by a lane permute.  The same arithmetic in the same order
-    // as the readlane form (the pivot row, not the symmetric column: eliminating
-    // with the column's rounding measured 10-100x less accurate at cond(K) ~ 1e5),
-    // 16 FMAs per lane and step.
+// Gauss-Jordan sweep of the 32x32 pivot block rows k0 .. k0+31 of C (row-major
+// [np][32]) by one wave: lane l + 32 h holds columns [16 h, 16 h + 16) of row l.
+// At step c the pivot row (lanes c and c + 32) goes through the LDS (rowb, 32
+// doubles) and every lane reads the half it needs (broadcast reads; LDS operations
+// of one wave complete in order); a row's column-c entry comes from its other
+// half-lane by a lane permute.  The same arithmetic in the same order as the
+// readlane form (the pivot row, not the symmetric column: eliminating with the
+// column's rounding measured 10-100x less accurate at cond(K) ~ 1e5), 16 FMAs per
+// lane and step.  On return r holds -P^-1 (lane's half row), prod the product of
+// the pivots, bad the first non-positive pivot (1-based) or 0.
+__device__ __forceinline__ void pivot_block_sweep(const double* __restrict__ C, int k0, double* rowb,
+                                                  double (&r)[16], double& prod, int& bad) {
+    const int lane = threadIdx.x & 63;
     const int l = lane & 31, h = lane >> 5;
-    double r[16];
 #pragma unroll
     for (int jj = 0; jj < 16; ++jj) r[jj] = C[(long long)(k0 + l) * kSwNb + 16 * h + jj];
-    double prod = 1.0;
-    int bad = 0;
+    prod = 1.0;
+    bad = 0;
     const double* rowh = rowb + 16 * h;
 #pragma unroll
     for (int c = 0; c < kSwNb; ++c) {
@@ -1007,6 +1065,24 @@ __global__ __launch_bounds__(64) void sw_pivot_kernel(LmlArgs a, int k) {
         }
         asm volatile("" ::: "memory");
     }
+}
+
+// grid (1, B), one wave: steps a-b of sweep step k (see lml_sweep_kernel) -- the
+// 32x32 pivot block of C_k (written by the build kernel for k = 0, by the previous
+// update kernel after) swept in registers, P^-1 to the workspace.  A single wave
+// keeps the whole register file (r02's 1024-thread pivot kernel capped the sweep
+// at 128 VGPRs and spilled its rows to scratch); G = C P^-1 is formed per tile by
+// sw_update_kernel.  (MPO_FIT_FUSE=0 path; sw_step_kernel folds it into the update.)
+__global__ __launch_bounds__(64) void sw_pivot_kernel(LmlArgs a, int k) {
+    const int b = blockIdx.y, k0 = k * kSwNb;
+    const SsPtrs p = ss_ptrs(a, b);
+    __shared__ double rowb[kSwNb];         // the sweep's pivot-row broadcast
+    const int lane = threadIdx.x;
+    if (a.stop == 21 || a.stop == 22) return;   // diagnostics only (MPO_FIT_DEBUG)
+    const int l = lane & 31, h = lane >> 5;
+    double r[16], prod;
+    int bad;
+    pivot_block_sweep(p.C(k), k0, rowb, r, prod, bad);
 #pragma unroll
     for (int jj = 0; jj < 16; ++jj) p.P[l * kSwNb + 16 * h + jj] = -r[jj];
     if (lane == 0) {
@@ -1117,6 +1193,129 @@ __global__ __launch_bounds__(kUpdThreads) void sw_update_kernel(LmlArgs a, int k
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the G_I reads before the next tile's stores
+    }
+}
+
+// grid (nwg, B), kUpdThreads, nwg * 4 >= the lower tile count (one tile per wave):
+// the whole sweep step k in one launch.  Every workgroup sweeps the 32x32 pivot
+// block of C_k itself (wave 0, pivot_block_sweep: the same instructions on the same
+// data, so the same P^-1 bits in every workgroup) into its LDS while the other waves
+// load their tile's operands; then each wave forms G_I = C_I P^-1 and updates its
+// tile exactly as sw_update_kernel does.  Replaces the one-wave sw_pivot_kernel
+// launch and the P round trip through global memory; workgroup 0 keeps the log det
+// and the failure column.
+__global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlArgs a, int k) {
+    const int b = blockIdx.y, np = (int)sw_np(a.n), ntile = np / 16, k0 = k * kSwNb;
+    const SsPtrs p = ss_ptrs(a, b);
+    const double* Cc = p.C(k);
+    __shared__ double gl[kUpdThreads / 64][16 * kSwNb];   // per wave: G_I, A-operand order
+    __shared__ double Pl[kSwNb * kSwNb];                  // P^-1 of this step
+    __shared__ double rowb[kSwNb];
+    const int k1 = k0 + kSwNb;
+    double* Cn = k1 < np ? p.C(k + 1) : nullptr;
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const int t = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kUpdThreads / 64) + wv));
+    const int nt_low = ntile * (ntile + 1) / 2;
+    int I = 0, J = 0, kind = 0;   // 0: nothing, 1: rows of block k <- -P^-1, 2: update tile (I, J)
+    if (t < nt_low) {
+        I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+        while (I * (I + 1) / 2 > t) --I;
+        while ((I + 1) * (I + 2) / 2 <= t) ++I;
+        J = t - I * (I + 1) / 2;
+        kind = (I >> 1) == k ? (I == J ? 1 : 0) : ((J >> 1) == k ? 0 : 2);
+    }
+    I = __builtin_amdgcn_readfirstlane(I);
+    J = __builtin_amdgcn_readfirstlane(J);
+    kind = __builtin_amdgcn_readfirstlane(kind);
+    // the tile's operands that do not depend on P^-1, loaded before the sweep
+    double av[8], cb[8];
+    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+    if (kind == 2) {
+        const double* ar = Cc + (long long)(16 * I + (lane & 15)) * kSwNb + (lane >> 4);
+        const double* cr = Cc + (long long)(16 * J + (lane & 15)) * kSwNb + (lane >> 4);
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            av[ks] = ar[4 * ks];
+            cb[ks] = cr[4 * ks];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = p.A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)];
+    }
+    if (wv == 0) {
+        const int l = lane & 31, h = lane >> 5;
+        double r[16], prod;
+        int bad;
+        pivot_block_sweep(Cc, k0, rowb, r, prod, bad);
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) Pl[l * kSwNb + 16 * h + jj] = -r[jj];
+        if (blockIdx.x == 0 && lane == 0) {
+            p.acc[0] += log(prod);
+            if (bad && p.acc[1] == 0.0) p.acc[1] = (double)(k0 + bad);
+        }
+    }
+    __syncthreads();
+    if (kind == 1) {
+#pragma unroll
+        for (int e = lane; e < 16 * kSwNb; e += 64) {
+            const int i = 16 * I + (e >> 5), c = e & 31;
+            p.A[(long long)i * np + k0 + c] = -Pl[(i - k0) * kSwNb + c];
+        }
+        return;
+    }
+    if (kind != 2) return;
+    double* g = gl[wv];
+    {
+        double b0[8], b1[8];
+        const double* br = Pl + (lane >> 4) * kSwNb + (lane & 15);
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            b0[ks] = br[4 * ks * kSwNb];
+            b1[ks] = br[4 * ks * kSwNb + 16];
+        }
+        f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ks], b0[ks], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ks], b1[ks], acc1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int rr = (lane >> 4) + 4 * q, c0 = lane & 15, c1 = 16 + c0;
+            g[(c0 >> 2) * 64 + rr + 16 * (c0 & 3)] = acc0[q];
+            g[(c1 >> 2) * 64 + rr + 16 * (c1 & 3)] = acc1[q];
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's G_I stores (LDS ops of one wave complete in order)
+    double ga[8];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) ga[ks] = g[ks * 64 + lane];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-ga[ks], cb[ks], acc, 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) p.A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)] = acc[q];
+    if (Cn && ((J >> 1) == k + 1 || (I >> 1) == k + 1)) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = 16 * I + (lane >> 4) + 4 * q, j = 16 * J + (lane & 15);
+            if (i < j) continue;                                    // upper half of a diagonal tile
+            if ((j >> 5) == k + 1) Cn[(long long)i * kSwNb + (j - k1)] = acc[q];
+            if ((i >> 5) == k + 1) Cn[(long long)j * kSwNb + (i - k1)] = acc[q];
+        }
+    }
+    if (I == J) {
+        // block column k, rows 16 I .. 16 I + 15, <- G_I (lower storage: below
+        // block k at A[i][j], above it transposed at A[j][i]); a row of block k+1
+        // also gives row j of C_{k+1}
+#pragma unroll
+        for (int e = lane; e < 16 * kSwNb; e += 64) {
+            const int ri = e >> 5, c = e & 31, i = 16 * I + ri, j = k0 + c;
+            const double gv = g[(c >> 2) * 64 + ri + 16 * (c & 3)];
+            if (i > j) p.A[(long long)i * np + j] = gv;
+            else p.A[(long long)j * np + i] = gv;
+            if (Cn && (i >> 5) == k + 1) Cn[(long long)j * kSwNb + (i - k1)] = gv;
+        }
     }
 }
 
@@ -1239,28 +1438,146 @@ __global__ __launch_bounds__(64) void sw_final_kernel(LmlArgs a, const double* _
     }
 }
 
+// sw_pairs_kernel + sw_final_kernel in one launch: every workgroup stores its
+// partial, then the last one to arrive (a device-scope counter per theta, reset by
+// sw_xs_build_kernel) sums the partials -- loaded in parallel into the LDS, then
+// added in sw_final_kernel's fixed order -- and writes y.alpha, the LML and the
+// gradient (the same bits as the two-launch form).
+template <int DP>
+__global__ __launch_bounds__(256) void sw_pairs_final_kernel(LmlArgs a, double* __restrict__ partials) {
+    __shared__ double red[4][DP + 2];
+    __shared__ double pl[kPairGroups * (DP + 2)];
+    __shared__ int last;
+    const int b = blockIdx.y, n = a.n, d = a.d, np = (int)sw_np(n);
+    const SsPtrs p = ss_ptrs(a, b);
+    double amp, noise, ls[DP];
+    ss_theta<DP>(a, b, amp, noise, ls);
+    (void)ls;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int gw = blockIdx.x * 4 + wave, nw = gridDim.x * 4;
+    const bool failed = p.acc[1] != 0.0;
+    double g[DP + 2];
+#pragma unroll
+    for (int c = 0; c < DP + 2; ++c) g[c] = 0.0;
+    if (!failed) {
+        for (int i = gw; i < n; i += nw) {
+            const double ai = p.alpha[i];
+            double xi[DP];
+#pragma unroll
+            for (int c = 0; c < DP; ++c) xi[c] = c < d ? p.xs[i * d + c] : 0.0;
+            for (int j = lane; j <= i; j += 64) {
+                const double W = (ai * p.alpha[j] + p.A[(long long)i * np + j]) * (i == j ? 1.0 : 2.0);
+                const double* xj = p.xs + j * d;
+                double r2 = 0.0;
+#pragma unroll
+                for (int c = 0; c < DP; ++c)
+                    if (c < d) {
+                        const double t = xi[c] - xj[c];
+                        r2 += t * t;
+                    }
+                const double sq = sqrt(5.0 * r2);
+                const double e = exp(-sq);
+                const double Mij = i == j ? 1.0 : (1.0 + sq + sq * sq / 3.0) * e;
+                g[0] += W * (amp * Mij);
+                const double f = W * amp * (5.0 / 3.0) * (sq + 1.0) * e;
+#pragma unroll
+                for (int c = 0; c < DP; ++c)
+                    if (c < d) {
+                        const double t = xi[c] - xj[c];
+                        g[1 + c] += f * (t * t);
+                    }
+                if (i == j) g[DP + 1] += W * noise;
+            }
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < DP + 2; ++c) {
+        const double v = wave_sum_bcast(g[c]);
+        if (lane == 0) red[wave][c] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < DP + 2) {
+        const int c = threadIdx.x;
+        partials[((long long)b * gridDim.x + blockIdx.x) * (DP + 2) + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+        __threadfence();
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last = atomicAdd(reinterpret_cast<unsigned*>(p.acc + 2), 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    const int groups = gridDim.x;
+    double* out = a.grad + (long long)b * (d + 2);
+    if (failed) {
+        if (threadIdx.x == 0) { a.lml[b] = -INFINITY; a.info[b] = (int)p.acc[1]; }
+        for (int c = threadIdx.x; c < d + 2; c += 256) out[c] = 0.0;
+        return;
+    }
+    for (int e = threadIdx.x; e < groups * (DP + 2); e += 256)
+        pl[e] = partials[(long long)b * groups * (DP + 2) + e];
+    __syncthreads();
+    if (wave != 0) return;
+    double ya = 0.0;
+    for (int i = lane; i < n; i += 64) ya = fma(a.y[i], p.alpha[i], ya);
+    ya = wave_sum_bcast(ya);
+    if (lane == 0) {
+        a.lml[b] = -0.5 * ya - 0.5 * p.acc[0] - 0.5 * n * kLog2Pi;
+        a.info[b] = 0;
+    }
+    if (lane < d + 2) {
+        const int src = lane == 0 ? 0 : (lane == d + 1 ? DP + 1 : lane);
+        double sum = 0.0;
+        for (int w = 0; w < groups; ++w) sum += pl[w * (DP + 2) + src];
+        out[lane] = 0.5 * sum;
+    }
+}
+
 template <int DP>
 int launch_split(const LmlArgs& a, int B, hipStream_t s) {
     const int np = (int)sw_np(a.n), nbk = np / kSwNb, ntile = np / 16;
     const int nt_low = ntile * (ntile + 1) / 2;
     const int nwg = std::max(1, (nt_low + 4 * kUpdTilesPerWave - 1) / (4 * kUpdTilesPerWave));
-    hipLaunchKernelGGL(sw_xs_kernel<DP>, dim3(1, B), dim3(256), 0, s, a);
-    MPO_LAUNCH_CHECK();
-    hipLaunchKernelGGL(sw_build_kernel<DP>, dim3(ntile, B), dim3(256), 0, s, a);
-    MPO_LAUNCH_CHECK();
-    for (int k = 0; k < nbk; ++k) {
-        hipLaunchKernelGGL(sw_pivot_kernel, dim3(1, B), dim3(64), 0, s, a, k);
+    // MPO_FIT_FUSE=0: the r03 launch sequence (separate xs / pivot / final kernels)
+    const char* fe = getenv("MPO_FIT_FUSE");
+    const bool fuse = !(fe && fe[0] == '0');
+    const size_t xs_lds = (size_t)np * DP * sizeof(double);
+    const bool fuse_build = fuse && xs_lds <= 64 * 1024;
+    double* partials = a.ws + (long long)B * a.ws_stride;   // [B][kPairGroups][DP + 2]
+    if (fuse_build) {
+        auto kb = sw_xs_build_kernel<DP>;
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kb), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)xs_lds);
+        hipLaunchKernelGGL(kb, dim3(ntile, B), dim3(1024), xs_lds, s, a);
         MPO_LAUNCH_CHECK();
-        hipLaunchKernelGGL(sw_update_kernel, dim3(nwg, B), dim3(kUpdThreads), 0, s, a, k);
+    } else {
+        hipLaunchKernelGGL(sw_xs_kernel<DP>, dim3(1, B), dim3(256), 0, s, a);
+        MPO_LAUNCH_CHECK();
+        hipLaunchKernelGGL(sw_build_kernel<DP>, dim3(ntile, B), dim3(256), 0, s, a);
         MPO_LAUNCH_CHECK();
     }
-    double* partials = a.ws + (long long)B * a.ws_stride;   // [B][kPairGroups][DP + 2]
+    for (int k = 0; k < nbk; ++k) {
+        if (fuse) {
+            hipLaunchKernelGGL(sw_step_kernel, dim3(nwg, B), dim3(kUpdThreads), 0, s, a, k);
+            MPO_LAUNCH_CHECK();
+        } else {
+            hipLaunchKernelGGL(sw_pivot_kernel, dim3(1, B), dim3(64), 0, s, a, k);
+            MPO_LAUNCH_CHECK();
+            hipLaunchKernelGGL(sw_update_kernel, dim3(nwg, B), dim3(kUpdThreads), 0, s, a, k);
+            MPO_LAUNCH_CHECK();
+        }
+    }
     hipLaunchKernelGGL(sw_alpha_kernel, dim3(ntile, B), dim3(256), 0, s, a);
     MPO_LAUNCH_CHECK();
-    hipLaunchKernelGGL(sw_pairs_kernel<DP>, dim3(kPairGroups, B), dim3(256), 0, s, a, partials);
-    MPO_LAUNCH_CHECK();
-    hipLaunchKernelGGL(sw_final_kernel<DP>, dim3(1, B), dim3(64), 0, s, a, partials, kPairGroups);
-    MPO_LAUNCH_CHECK();
+    if (fuse_build) {   // the arrival counter is reset by sw_xs_build_kernel
+        hipLaunchKernelGGL(sw_pairs_final_kernel<DP>, dim3(kPairGroups, B), dim3(256), 0, s, a, partials);
+        MPO_LAUNCH_CHECK();
+    } else {
+        hipLaunchKernelGGL(sw_pairs_kernel<DP>, dim3(kPairGroups, B), dim3(256), 0, s, a, partials);
+        MPO_LAUNCH_CHECK();
+        hipLaunchKernelGGL(sw_final_kernel<DP>, dim3(1, B), dim3(64), 0, s, a, partials, kPairGroups);
+        MPO_LAUNCH_CHECK();
+    }
     return MPO_OK;
 }
 

@@ -145,3 +145,31 @@ def test_device_fit_matches_sklearn_fit(name):
     # the LML at the optimum agrees tightly; theta within the optimiser's resolution
     assert abs(det["lml"] - float(G[name + "_fit_lml"])) <= 1e-7 * abs(float(G[name + "_fit_lml"]))
     assert np.max(np.abs(theta - ref)) <= 1e-3, (theta, ref)
+
+
+@pytest.mark.parametrize("name", ["n57_d3", "n130_d6", "n230_d4", "n256_d10", "n500_d10"])
+def test_fused_split_sweep_is_bit_identical_to_the_launch_sequence(name, monkeypatch):
+    """r03: sw_step_kernel (every workgroup sweeps the pivot block itself),
+    sw_xs_build_kernel and sw_pairs_final_kernel (last-arriving workgroup sums the
+    partials) reproduce the separate xs / build / pivot / update / pairs / final
+    launches bit for bit; repeated calls re-arm the arrival counter."""
+    dev, _ = _lml(name)
+    T = G[name + "_theta"]
+    monkeypatch.setenv("MPO_FIT_FUSE", "0")
+    l0, g0, i0 = dev.evaluate(T)
+    monkeypatch.setenv("MPO_FIT_FUSE", "1")
+    for _ in range(3):
+        l1, g1, i1 = dev.evaluate(T)
+        assert np.array_equal(i0, i1) and np.array_equal(l0, l1) and np.array_equal(g0, g1)
+
+
+def test_fused_split_sweep_reports_failure(monkeypatch):
+    monkeypatch.setenv("MPO_FIT_FUSE", "1")
+    dev, _ = _lml("n230_d4")
+    T = G["n230_d4_theta"][:3].copy()
+    T[1, 0] = np.nan
+    lml, grad, info = dev.evaluate(T)
+    assert info[0] == 0 and info[1] >= 1 and info[2] == 0
+    assert lml[1] == -np.inf and np.all(grad[1] == 0.0)
+    l2, g2, _ = dev.evaluate(T[2:3])
+    assert l2[0] == lml[2] and np.array_equal(g2[0], grad[2])
