@@ -103,8 +103,9 @@ def live_pmc(train_trials):
     out = {"ei": None, "train": None, "densenet": None, "errors": []}
     ei_prog = [os.path.join(ROOT, "scripts", "ei_probe.py"), "3"]
     try:
-        # one acquisition pass = gp_score_kernel + score_finish_kernel (the (mu_n, q)
-        # rows between them are the only non-algorithmic traffic)
+        # one acquisition pass = gp_score_kernel (r03: the posterior / acquisition /
+        # top-k finish runs inside it over the workgroup's own (mu_n, q) rows, the only
+        # non-algorithmic traffic; score_finish_kernel of earlier rounds kept matching)
         acq = lambda k: "gp_score_kernel" in k or "score_finish_kernel" in k   # noqa: E731
         f = _per_dispatch(pmc_pass(["FETCH_SIZE"], ei_prog), "FETCH_SIZE", acq)
         w = _per_dispatch(pmc_pass(["WRITE_SIZE"], ei_prog), "WRITE_SIZE", acq)
@@ -272,7 +273,7 @@ def bench_ei(args, torch, dist, ws, rank, dev):
                                f"{m} candidates per GPU, top-{k} (skopt argsort[:n_restarts])",
                    "n_obs": n, "dims": d, "candidates_per_gpu": m,
                    "parallelism": f"candidates sharded, {ws} GPU(s), all-gather of (value,index)"},
-        "roofline": {"kernel": "gp_score_kernel + score_finish_kernel (one acquisition pass)", "bound": "mfma",
+        "roofline": {"kernel": "gp_score_kernel (one acquisition pass, finish fused)", "bound": "mfma",
                      "achieved": achieved,
                      "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
                      "traffic": ((args.pmc or {}).get("ei") or {}).get("hbm_bytes_per_launch"),

@@ -17,7 +17,7 @@
 //                                          only the lower-triangular k-steps,
 //                                          ||V_row||^2 accumulated in registers
 //                          phase 3:        sd, mu, -EI/-PI/LCB, block top-k
-//   topk_merge_kernel    block top-k partials -> global top-k (lowest index ties)
+//   topk_merge_kernel    workgroup top-k lists -> global top-k (lowest index ties)
 //
 // Why the triangular form: skopt evaluates sd^2 = amp - k^T K_inv k with an
 // explicit K_inv (86 kFLOP/candidate at N=200, catastrophic cancellation);
@@ -371,24 +371,19 @@ struct ScoreArgs {
     int k;
     long long* part_idx;  // [nparts][3][k]
     double* part_val;
-    double* mq;           // [m][2] (mu_n, q): scoring kernel -> score_finish_kernel
+    double* mq;           // [m][2] raw (mu_n, q) rows (FIN = 0 only: the prepare-time self-check)
 };
 
-// Posterior, acquisitions and per-wave top-k from the scoring kernel's
-// (mu_n = amp K'.alpha, q = amp^2 ||L^-1 K'||^2) per candidate: one candidate per
-// thread, every lane live (the scoring kernel's 16-candidate tiles would leave
-// 48 of 64 lanes idle here).  Wave w of block b writes part list b*4 + w.
-constexpr int kFinishThreads = 256;
-constexpr int kFinishCands = 64;   // candidates per partial top-k list (one wave)
-
-__global__ __launch_bounds__(kFinishThreads) void score_finish_kernel(ScoreArgs a, const double* __restrict__ mq) {
-    const int lane = threadIdx.x & 63;
-    const long long gm = (long long)blockIdx.x * kFinishThreads + threadIdx.x;
-    const long long part = gm >> 6;
-    const bool valid = gm < a.m;
+// One wave, 64 candidates (lane = candidate; invalid lanes contribute nothing): the
+// posterior and acquisitions as score_finish_kernel computes them, the requested
+// output rows, then the candidates merged into the workgroup's running top-k lists
+// (tk_val / tk_idx [3][MPO_TOPK_MAX], sorted, LDS).  A lane takes part only while its
+// (value, index) beats the list's k-th entry; each round inserts the group minimum
+// among those lanes (lane 0 shifts the list), so at most k rounds run and usually none.
+__device__ __attribute__((noinline)) void score_finish_group(const ScoreArgs& a, bool valid, long long gm, double mu_n,
+                                                   double q, int lane, double* tk_val, long long* tk_idx) {
     double mu = 0.0, sd = 0.0, vei = 0.0, vpi = 0.0, vlcb = 0.0;
     if (valid) {
-        const double mu_n = mq[2 * gm], q = mq[2 * gm + 1];
         double var = a.amp - q;
         if (var < 0.0) var = 0.0;
         sd = sqrt(var) * a.y_std;
@@ -412,22 +407,34 @@ __global__ __launch_bounds__(kFinishThreads) void score_finish_kernel(ScoreArgs 
             if (a.flags & MPO_ACQ_LCB) a.vals[2 * a.m + gm] = vlcb;
         }
     }
-    if (a.k <= 0 || (a.dbg & 4) || (long long)blockIdx.x * kFinishThreads + (threadIdx.x & ~63) >= a.m) return;
+    if (a.k <= 0 || (a.dbg & 4)) return;
     const double inf = __builtin_huge_val();
     const long long big = 0x7fffffffffffffffLL;
+    const int k = a.k;
 #pragma unroll
     for (int acq = 0; acq < 3; ++acq) {
         if (!(a.flags & (1u << acq))) continue;
-        double v = valid ? (acq == 0 ? vei : (acq == 1 ? vpi : vlcb)) : inf;
-        long long idx = valid ? gm : big;
-        long long* pi = a.part_idx + ((size_t)part * 3 + acq) * a.k;
-        double* pv = a.part_val + ((size_t)part * 3 + acq) * a.k;
-        for (int r = 0; r < a.k; ++r) {
-            double bv = v;
-            long long bi = idx;
+        const double v = valid ? (acq == 0 ? vei : (acq == 1 ? vpi : vlcb)) : inf;
+        const long long idx = valid ? gm : big;
+        double* lv = tk_val + acq * MPO_TOPK_MAX;
+        long long* li = tk_idx + acq * MPO_TOPK_MAX;
+        bool cand = valid && lex_less(v, idx, lv[k - 1], li[k - 1]);
+        while (__any(cand)) {
+            double bv = cand ? v : inf;
+            long long bi = cand ? idx : big;
             wave_lex_min(bv, bi);
-            if (lane == 0) { pv[r] = bv; pi[r] = bi; }
-            if (idx == bi) { v = inf; idx = big; }
+            if (lane == 0) {
+                int pos = k - 1;
+                while (pos > 0 && lex_less(bv, bi, lv[pos - 1], li[pos - 1])) {
+                    lv[pos] = lv[pos - 1];
+                    li[pos] = li[pos - 1];
+                    --pos;
+                }
+                lv[pos] = bv;
+                li[pos] = bi;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // lane 0's list stores before every lane's reads
+            cand = cand && idx != bi && lex_less(v, idx, lv[k - 1], li[k - 1]);
         }
     }
 }
@@ -435,7 +442,15 @@ __global__ __launch_bounds__(kFinishThreads) void score_finish_kernel(ScoreArgs 
 // One workgroup = 4 waves looping over 16-candidate tiles (kBM) tile = blockIdx.x,
 // += gridDim.x (the grid is sized to the resident capacity); the next tile's
 // candidate rows are loaded while the current one is scored.
-template <int DP, int D, int OCC, int MD>
+// FIN = 1 (every scoring launch): after its tile loop the workgroup finishes its own
+// candidates -- the (mu_n, q) rows it wrote (still largely in this XCD's L2) read
+// back 64 per wave with every lane live, the posterior and acquisitions as
+// score_finish_group computes them, one running top-k list per wave -- instead of a
+// separate finish launch over rows written by workgroups on every XCD.  (An in-loop
+// finish was built first: the loop already holds 101 SGPRs and 96 VGPRs at
+// occupancy 5, and the finish's invariants spilled it.)  FIN = 0 stops at the rows
+// (mpo_gp_prepare's self-check of the expanded form).
+template <int DP, int D, int OCC, int MD, int FIN>
 __global__ __launch_bounds__(256, OCC) void gp_score_kernel(ScoreArgs a) {
     static_assert(!MD || D + 2 <= DP, "the MFMA distance needs two spare columns");
     constexpr int BM = kBM;
@@ -453,6 +468,7 @@ __global__ __launch_bounds__(256, OCC) void gp_score_kernel(ScoreArgs a) {
     const long long ntiles = (a.m + BM - 1) / BM;
 
     for (int e = tid; e < 4 * (a.T + 4); e += 256) mls[e] = a.wmeta[e];
+
     const bool xb_ok = MD && *a.xb_ok != 0.0;   // read once: the model-level guard of the expanded distance
     // thread tid owns elements tid + 256 u of the [BM][DP] candidate tile
     double raw[EPT], ls_e[EPT];
@@ -465,10 +481,19 @@ __global__ __launch_bounds__(256, OCC) void gp_score_kernel(ScoreArgs a) {
     _Pragma("unroll") for (int u = 0; u < EPT; ++u) {                                          \
         const int e = tid + 256 * u, r = e / DP, c = e % DP;                                   \
         const long long gm = (TILE) * BM + r;                                                  \
-        raw[u] = (e < BM * DP && gm < a.m && c < a.d) ? a.cand[gm * a.d + c] : 0.0;            \
+        raw[u] = (e < BM * DP && gm < a.m && c < a.d) ? __builtin_nontemporal_load(a.cand + gm * a.d + c) : 0.0; \
     }
     MPO_LOAD_TILE((long long)blockIdx.x)
     __syncthreads();
+    // the finishing wave (mu fold, phase 3, FIN's group finish): the wave whose phase-2
+    // B stream (sw = (wave + blockIdx.x) & 3, below) carries the fewest groups
+    int fw = 0;
+    {
+        int lw = 0;
+        for (int q = 1; q < 4; ++q)
+            if (mls[q * (a.T + 4) + 1] < mls[lw * (a.T + 4) + 1]) lw = q;
+        fw = __builtin_amdgcn_readfirstlane((lw - (int)blockIdx.x) & 3);
+    }
 
     // Phase-2 B-fragment stream of this wave (rotated by block so the heaviest one
     // does not always land on the same SIMD).  B fragments arrive through asm loads
@@ -587,9 +612,9 @@ __global__ __launch_bounds__(256, OCC) void gp_score_kernel(ScoreArgs a) {
     }
     __syncthreads();
     double mu_n = 0.0;
-    if (tid < BM) {
+    if (wave == fw && lane < BM) {
 #pragma unroll
-        for (int s = 0; s < S; ++s) mu_n += red[s * BM + tid];
+        for (int s = 0; s < S; ++s) mu_n += red[s * BM + lane];
         mu_n *= a.amp;
     }
     __syncthreads();  // red is reused for the q partials below
@@ -651,14 +676,49 @@ __global__ __launch_bounds__(256, OCC) void gp_score_kernel(ScoreArgs a) {
     }
     __syncthreads();
 
-    // ---- phase 3: (mu_n, q) out (wave 0; the other waves go on to the next tile's
-    // phase 0 and meet wave 0 at its barrier, after which red may be rewritten)
-    if (tid < BM && m0 + tid < a.m) {
-        const double q = (red[0 * BM + tid] + red[1 * BM + tid] + red[2 * BM + tid] + red[3 * BM + tid]) *
+    // ---- phase 3: (mu_n, q) rows out (wave fw; the other waves go on to the next
+    // tile's phase 0 and meet wave fw at its barrier, after which red may be rewritten)
+    if (wave == fw && lane < BM && m0 + lane < a.m) {
+        const double q = (red[0 * BM + lane] + red[1 * BM + lane] + red[2 * BM + lane] + red[3 * BM + lane]) *
                          (a.amp * a.amp);
-        *reinterpret_cast<double2*>(a.mq + 2 * (m0 + tid)) = double2{mu_n, q};
+        *reinterpret_cast<double2*>(a.mq + 2 * (m0 + lane)) = double2{mu_n, q};
     }
     }  // tile loop
+    if constexpr (FIN) {
+        // ---- finish: this workgroup's own (mu_n, q) rows (written above, mostly still
+        // in this XCD's L2), 64 candidates per wave at a time with every lane live;
+        // one running top-k list per wave in the (now free) K* LDS region
+        __syncthreads();   // the rows of wave fw (global writes, workgroup-scope visibility)
+        // the finish reads its arguments through a pointer to the kernarg segment: the
+        // out-of-line score_finish_group given `a` itself would copy the by-value
+        // struct to the stack (and the scoring variants must stay scratch-free, see
+        // launch_score); the asm keeps the loads out of the tile loop
+        const ScoreArgs* ap = (const ScoreArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(ap));
+        const ScoreArgs& f = *ap;
+        double* tk_val = kc + wave * 3 * MPO_TOPK_MAX;
+        long long* tk_idx = reinterpret_cast<long long*>(kc + 4 * 3 * MPO_TOPK_MAX) + wave * 3 * MPO_TOPK_MAX;
+        if (lane < 3 * MPO_TOPK_MAX) {
+            tk_val[lane] = __builtin_huge_val();
+            tk_idx[lane] = 0x7fffffffffffffffLL;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const long long ntl = ((f.m + BM - 1) / BM - blockIdx.x + gridDim.x - 1) / gridDim.x;   // this workgroup's tiles
+        for (long long c0 = (long long)wave * 64; c0 < ntl * BM; c0 += 256) {
+            const long long cl = c0 + lane;
+            const long long gm = (blockIdx.x + (cl >> 4) * (long long)gridDim.x) * BM + (cl & 15);
+            const bool valid = cl < ntl * BM && gm < f.m;
+            double2 v = {0.0, 0.0};
+            if (valid) v = *reinterpret_cast<const double2*>(f.mq + 2 * gm);
+            score_finish_group(f, valid, gm, v.x, v.y, lane, tk_val, tk_idx);
+        }
+        if (f.k > 0 && lane < 3 * f.k) {
+            const int acq = lane / f.k, r = lane - acq * f.k;
+            const size_t part = (size_t)blockIdx.x * 4 + wave;
+            f.part_val[(part * 3 + acq) * f.k + r] = tk_val[acq * MPO_TOPK_MAX + r];
+            f.part_idx[(part * 3 + acq) * f.k + r] = tk_idx[acq * MPO_TOPK_MAX + r];
+        }
+    }
 #undef MPO_LD4
 #undef MPO_LD
 #undef MPO_LOAD_TILE
@@ -758,15 +818,18 @@ constexpr int kMergeGroups = 256;  // stage-1 top-k merge groups
 
 size_t score_lds_bytes(int dp, int np16) {
     const int T = np16 / 16;
+    // kc (after the tile loop: FIN's per-wave top-k lists, 4 x 3 x MPO_TOPK_MAX x 16 B <= np16 x kBM x 8 B),
+    // cs, red | wave records
     return ((size_t)np16 * kBM + (size_t)kBM * dp + 16 * kBM) * sizeof(double) + (size_t)4 * (T + 4) * sizeof(int32_t);
 }
 
 bool score_fits(int dp, int np16) { return score_lds_bytes(dp, np16) <= kMaxLds; }
 
-// grid = the device's resident capacity for this variant (tiles are looped over)
-template <int DP, int D, int OCC, int MD>
-hipError_t launch_score(const ScoreArgs& a, int ntiles, size_t lds, hipStream_t s) {
-    auto kern = gp_score_kernel<DP, D, OCC, MD>;
+// grid = the device's resident capacity for this variant (tiles are looped over);
+// *grid_out receives it (FIN: one top-k list per workgroup)
+template <int DP, int D, int OCC, int MD, int FIN>
+hipError_t launch_score(const ScoreArgs& a, int ntiles, size_t lds, hipStream_t s, int* grid_out) {
+    auto kern = gp_score_kernel<DP, D, OCC, MD, FIN>;
     // The B ring's asm loads are invisible to the compiler: a spill of a ring
     // register would store it before its load lands.  A variant whose register
     // cap forces spills is refused instead of run.
@@ -782,16 +845,18 @@ hipError_t launch_score(const ScoreArgs& a, int ntiles, size_t lds, hipStream_t 
     int grid = std::max(1, std::min(ntiles, std::max(1, per_cu) * std::max(1, cus)));
     const char* g = getenv("MPO_GP_GRID");   // experiments: "tiles" = one tile per workgroup
     if (g && g[0] == 't') grid = ntiles;
+    if (grid_out) *grid_out = grid;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, a);
     return hipGetLastError();
 }
 
-template <int DP, int D, int OCC, int MD>
+template <int DP, int D, int OCC, int MD, int FIN>
 bool spill_free() {
     static int ok = -1;
     if (ok < 0) {
         hipFuncAttributes fa;
-        ok = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(gp_score_kernel<DP, D, OCC, MD>)) == hipSuccess &&
+        ok = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(gp_score_kernel<DP, D, OCC, MD, FIN>)) ==
+                 hipSuccess &&
              fa.localSizeBytes == 0;
     }
     return ok == 1;
@@ -799,42 +864,50 @@ bool spill_free() {
 
 // occupancy hint (min waves per SIMD -> VGPR cap): the highest spill-free one;
 // MPO_GP_OCC (2, 4, 5, 6) forces one for experiments
-template <int DP, int D, int MD>
-hipError_t launch_score_occ_md(const ScoreArgs& a, int nblocks, size_t lds, hipStream_t s) {
+template <int DP, int D, int MD, int FIN>
+hipError_t launch_score_occ_md(const ScoreArgs& a, int nblocks, size_t lds, hipStream_t s, int* grid_out) {
     const char* e = getenv("MPO_GP_OCC");
     int occ = e ? atoi(e) : 0;
     if (occ != 2 && occ != 4 && occ != 5 && occ != 6)
-        occ = spill_free<DP, D, 6, MD>() ? 6 : spill_free<DP, D, 5, MD>() ? 5 : spill_free<DP, D, 4, MD>() ? 4 : 2;
+        occ = spill_free<DP, D, 6, MD, FIN>()   ? 6
+              : spill_free<DP, D, 5, MD, FIN>() ? 5
+              : spill_free<DP, D, 4, MD, FIN>() ? 4
+                                                : 2;
     switch (occ) {
-        case 6: return launch_score<DP, D, 6, MD>(a, nblocks, lds, s);
-        case 5: return launch_score<DP, D, 5, MD>(a, nblocks, lds, s);
-        case 4: return launch_score<DP, D, 4, MD>(a, nblocks, lds, s);
-        default: return launch_score<DP, D, 2, MD>(a, nblocks, lds, s);
+        case 6: return launch_score<DP, D, 6, MD, FIN>(a, nblocks, lds, s, grid_out);
+        case 5: return launch_score<DP, D, 5, MD, FIN>(a, nblocks, lds, s, grid_out);
+        case 4: return launch_score<DP, D, 4, MD, FIN>(a, nblocks, lds, s, grid_out);
+        default: return launch_score<DP, D, 2, MD, FIN>(a, nblocks, lds, s, grid_out);
     }
 }
 
 // MD = 1 (the MFMA distance) when the model carries xb (d + 2 <= dp; the kernel
-// reads the self-check's device flag); MPO_GP_DIST=0 forces the direct form
+// reads the self-check's device flag); MPO_GP_DIST=0 forces the direct form.
+// fin = false: raw (mu_n, q) rows only.
 template <int DP, int D>
-hipError_t launch_score_occ(const ScoreArgs& a, int nblocks, size_t lds, hipStream_t s) {
+hipError_t launch_score_occ(const ScoreArgs& a, int nblocks, size_t lds, hipStream_t s, bool fin, int* grid_out) {
     if constexpr (D + 2 <= DP) {
         const char* e = getenv("MPO_GP_DIST");
-        if (a.xb && a.xb_ok && !(e && e[0] == '0')) return launch_score_occ_md<DP, D, 1>(a, nblocks, lds, s);
+        if (a.xb && a.xb_ok && !(e && e[0] == '0'))
+            return fin ? launch_score_occ_md<DP, D, 1, 1>(a, nblocks, lds, s, grid_out)
+                       : launch_score_occ_md<DP, D, 1, 0>(a, nblocks, lds, s, grid_out);
     }
-    return launch_score_occ_md<DP, D, 0>(a, nblocks, lds, s);
+    return fin ? launch_score_occ_md<DP, D, 0, 1>(a, nblocks, lds, s, grid_out)
+               : launch_score_occ_md<DP, D, 0, 0>(a, nblocks, lds, s, grid_out);
 }
 
 // (padded row width DP, distance dims D): d = 5 and d = 10 (the reference's mnist
 // space and the BASELINE config) get exact-width distance loops
-hipError_t launch_score_dp(int dp, int d, const ScoreArgs& a, int nblocks, size_t lds, hipStream_t s) {
+hipError_t launch_score_dp(int dp, int d, const ScoreArgs& a, int nblocks, size_t lds, hipStream_t s, bool fin,
+                           int* grid_out = nullptr) {
     switch (dp) {
-        case 4: return launch_score_occ<4, 4>(a, nblocks, lds, s);
-        case 8: return d == 5 ? launch_score_occ<8, 5>(a, nblocks, lds, s)
-                              : launch_score_occ<8, 8>(a, nblocks, lds, s);
-        case 12: return d == 10 ? launch_score_occ<12, 10>(a, nblocks, lds, s)
-                                : launch_score_occ<12, 12>(a, nblocks, lds, s);
-        case 16: return launch_score_occ<16, 16>(a, nblocks, lds, s);
-        case 32: return launch_score_occ<32, 32>(a, nblocks, lds, s);
+        case 4: return launch_score_occ<4, 4>(a, nblocks, lds, s, fin, grid_out);
+        case 8: return d == 5 ? launch_score_occ<8, 5>(a, nblocks, lds, s, fin, grid_out)
+                              : launch_score_occ<8, 8>(a, nblocks, lds, s, fin, grid_out);
+        case 12: return d == 10 ? launch_score_occ<12, 10>(a, nblocks, lds, s, fin, grid_out)
+                                : launch_score_occ<12, 12>(a, nblocks, lds, s, fin, grid_out);
+        case 16: return launch_score_occ<16, 16>(a, nblocks, lds, s, fin, grid_out);
+        case 32: return launch_score_occ<32, 32>(a, nblocks, lds, s, fin, grid_out);
     }
     return hipErrorInvalidValue;
 }
@@ -1283,7 +1356,8 @@ struct ScoreWs {
     double* mq;
 };
 
-inline int64_t score_nparts(int64_t m) { return (m + kFinishCands - 1) / kFinishCands; }
+// top-k lists: 4 per workgroup (one per wave), and a workgroup has at least one tile
+inline int64_t score_nparts(int64_t m) { return 4 * ((m + kBM - 1) / kBM); }
 
 inline ScoreWs carve_score_ws(void* ws, int64_t m, int k, size_t* used) {
     const int64_t nparts = score_nparts(m);
@@ -1427,12 +1501,12 @@ int mpo_gp_prepare(const double* X, const double* y_norm, int n, int d, const do
         const int nt = (n + kBM - 1) / kBM;
         const size_t lds = score_lds_bytes(dp, np16);
         sa.mq = mqc;                                   // direct form
-        bool ok = launch_score_dp(dp, d, sa, nt, lds, s) == hipSuccess;
+        bool ok = launch_score_dp(dp, d, sa, nt, lds, s, false) == hipSuccess;
         sa.mq = mqc + 2 * (size_t)n;                   // expanded form
         sa.xb = xb;
         sa.xb_ok = flag;
         // a refused variant (MPO_GP_OCC forcing a spilling one) just leaves xb out
-        ok = ok && launch_score_dp(dp, d, sa, nt, lds, s) == hipSuccess;
+        ok = ok && launch_score_dp(dp, d, sa, nt, lds, s, false) == hipSuccess;
         if (ok) {
             hipLaunchKernelGGL(xb_check_kernel, dim3(1), dim3(256), 0, s, mqc, mqc + 2 * (size_t)n, alpha, n, amp,
                                flag);
@@ -1484,7 +1558,6 @@ static int gp_score_impl(const MpoGpModel* model, const double* cand, int64_t m,
     const int64_t ntiles64 = (m + kBM - 1) / kBM;
     MPO_CHECK_ARG(ntiles64 < (1LL << 31), "mpo_gp_acq_score: too many candidates");
     const int ntiles = (int)ntiles64;
-    const int nparts = (int)score_nparts(m);
     const ScoreWs w = carve_score_ws(ws, m, k, nullptr);
     long long* part_idx = w.part_idx;
     double* part_val = w.part_val;
@@ -1523,12 +1596,11 @@ static int gp_score_impl(const MpoGpModel* model, const double* cand, int64_t m,
     a.k = k;
     a.part_idx = part_idx;
     a.part_val = part_val;
-    a.mq = w.mq;
+    a.mq = w.mq;   // FIN: the workgroup's own rows, finished inside the scoring kernel
     const size_t lds = score_lds_bytes(model->dp, model->np16);
-    MPO_HIP(launch_score_dp(model->dp, model->d, a, ntiles, lds, s));
-    hipLaunchKernelGGL(score_finish_kernel, dim3((unsigned)((m + kFinishThreads - 1) / kFinishThreads)),
-                       dim3(kFinishThreads), 0, s, a, w.mq);
-    MPO_LAUNCH_CHECK();
+    int grid = 0;
+    MPO_HIP(launch_score_dp(model->dp, model->d, a, ntiles, lds, s, /*fin=*/true, &grid));
+    const int nparts = 4 * grid;
     if (k > 0) {
         // stage 1: G groups of ~64 wave-lists each; stage 2: one list
         const int chunk = std::max(64, (nparts + kMergeGroups - 1) / kMergeGroups);

@@ -58,6 +58,7 @@ struct LmlArgs {
     double* ws;           // per theta: ws_stride doubles
     long long ws_stride;
     int stop;             // diagnostics only (env MPO_FIT_DEBUG): return after phase 1/2/3/4
+    int pair;             // split sweep: pivot_block_sweep2 (two steps per LDS round, MPO_FIT_PAIR != 0)
 };
 
 __host__ __device__ inline long long fit_tri(long long n) { return n * (n + 1) / 2; }
@@ -1006,6 +1007,86 @@ __global__ __launch_bounds__(1024) void sw_xs_build_kernel(LmlArgs a) {
     }
 }
 
+// pivot_block_sweep with two steps per LDS round: the pivot rows c and c + 1 are
+// broadcast together, and every lane forms row c + 1 after step c itself
+// (row2' = fma(-t21, row1, row2), its column c = t21, pv2 = row2'[c + 1]) and the
+// column-(c+1) entry of its own row after step c (colv2' = fma(f1, row1[c+1], colv2),
+// 0 for the zeroed pivot row) with exactly the operations the lanes owning them
+// perform in pivot_block_sweep -- so the result is the same bits with half the LDS
+// round trips (and half the serial latency chains) at 16 more FMAs per two steps.
+// rowb: 64 doubles.
+__device__ __forceinline__ void pivot_block_sweep2(const double* __restrict__ C, int k0, double* rowb,
+                                                   double (&r)[16], double& prod, int& bad) {
+    const int lane = threadIdx.x & 63;
+    const int l = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) r[jj] = C[(long long)(k0 + l) * kSwNb + 16 * h + jj];
+    prod = 1.0;
+    bad = 0;
+#pragma unroll
+    for (int c = 0; c < kSwNb; c += 2) {
+        const int hc = c >> 4, jc = c & 15;       // columns c, c + 1: same half, jc even
+        const double colv1 = __shfl(r[jc], l + 32 * hc);       // A[l][c]
+        const double colv2 = __shfl(r[jc + 1], l + 32 * hc);   // A[l][c+1], before step c
+        const bool piv1 = l == c, piv2 = l == c + 1;
+        if (piv1 || piv2) {
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) rowb[32 * (l - c) + 16 * h + jj] = r[jj];
+        }
+        if (piv1) {
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) r[jj] = 0.0;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // ---- step c
+        const double pv1 = rowb[c];
+        if (!(pv1 > 0.0) || !isfinite(pv1)) bad = bad ? bad : c + 1;
+        prod *= pv1;
+        const double ip1 = 1.0 / pv1;
+        const double t1 = colv1 * ip1;
+        const double f1 = piv1 ? ip1 : -t1;
+        const double p1c1 = rowb[c + 1], p2c = rowb[32 + c], p2c1 = rowb[32 + c + 1];
+        double q1[16], q2[16];
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            q1[jj] = rowb[16 * h + jj];
+            q2[jj] = rowb[32 + 16 * h + jj];
+        }
+        // row c + 1 after step c, as its own lanes form it (t21 = their t1)
+        const double t21 = p2c * ip1;
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            const double u = fma(-t21, q1[jj], q2[jj]);
+            q2[jj] = (jj == jc && h == hc) ? t21 : u;
+        }
+        const double pv2 = fma(-t21, p1c1, p2c1);
+        const double colv2p = fma(f1, p1c1, piv1 ? 0.0 : colv2);
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            const double upd = fma(f1, q1[jj], r[jj]);
+            if (jj == jc) r[jj] = h == hc ? (piv1 ? -ip1 : t1) : upd;
+            else r[jj] = upd;
+        }
+        // ---- step c + 1 (pivot row = q2)
+        if (!(pv2 > 0.0) || !isfinite(pv2)) bad = bad ? bad : c + 2;
+        prod *= pv2;
+        const double ip2 = 1.0 / pv2;
+        const double t2 = colv2p * ip2;
+        const double f2 = piv2 ? ip2 : -t2;
+        if (piv2) {
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) r[jj] = 0.0;
+        }
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            const double upd = fma(f2, q2[jj], r[jj]);
+            if (jj == jc + 1) r[jj] = h == hc ? (piv2 ? -ip2 : t2) : upd;
+            else r[jj] = upd;
+        }
+        asm volatile("" ::: "memory");
+    }
+}
+
 // grid (1, B), one wave: steps a-b of sweep step k (see lml_sweep_kernel) -- the
 // 32x32 pivot block of C_k (written by the build kernel for k = 0, by the previous
 // update kernel after) swept in registers, P^-1 to the workspace.  A single wave
@@ -1076,13 +1157,14 @@ __device__ __forceinline__ void pivot_block_sweep(const double* __restrict__ C, 
 __global__ __launch_bounds__(64) void sw_pivot_kernel(LmlArgs a, int k) {
     const int b = blockIdx.y, k0 = k * kSwNb;
     const SsPtrs p = ss_ptrs(a, b);
-    __shared__ double rowb[kSwNb];         // the sweep's pivot-row broadcast
+    __shared__ double rowb[2 * kSwNb];     // the sweep's pivot-row broadcast
     const int lane = threadIdx.x;
     if (a.stop == 21 || a.stop == 22) return;   // diagnostics only (MPO_FIT_DEBUG)
     const int l = lane & 31, h = lane >> 5;
     double r[16], prod;
     int bad;
-    pivot_block_sweep(p.C(k), k0, rowb, r, prod, bad);
+    if (a.pair) pivot_block_sweep2(p.C(k), k0, rowb, r, prod, bad);
+    else pivot_block_sweep(p.C(k), k0, rowb, r, prod, bad);
 #pragma unroll
     for (int jj = 0; jj < 16; ++jj) p.P[l * kSwNb + 16 * h + jj] = -r[jj];
     if (lane == 0) {
@@ -1204,13 +1286,14 @@ __global__ __launch_bounds__(kUpdThreads) void sw_update_kernel(LmlArgs a, int k
 // tile exactly as sw_update_kernel does.  Replaces the one-wave sw_pivot_kernel
 // launch and the P round trip through global memory; workgroup 0 keeps the log det
 // and the failure column.
+template <bool PAIR>
 __global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlArgs a, int k) {
     const int b = blockIdx.y, np = (int)sw_np(a.n), ntile = np / 16, k0 = k * kSwNb;
     const SsPtrs p = ss_ptrs(a, b);
     const double* Cc = p.C(k);
     __shared__ double gl[kUpdThreads / 64][16 * kSwNb];   // per wave: G_I, A-operand order
     __shared__ double Pl[kSwNb * kSwNb];                  // P^-1 of this step
-    __shared__ double rowb[kSwNb];
+    __shared__ double rowb[2 * kSwNb];
     const int k1 = k0 + kSwNb;
     double* Cn = k1 < np ? p.C(k + 1) : nullptr;
     const int lane = threadIdx.x & 63;
@@ -1228,10 +1311,12 @@ __global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlArgs a, int k) 
     I = __builtin_amdgcn_readfirstlane(I);
     J = __builtin_amdgcn_readfirstlane(J);
     kind = __builtin_amdgcn_readfirstlane(kind);
-    // the tile's operands that do not depend on P^-1, loaded before the sweep
+    // the tile's operands that do not depend on P^-1: waves 1-3 load them while wave 0
+    // sweeps (if / else, so that they are not live across the sweep's registers)
     double av[8], cb[8];
     f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-    if (kind == 2) {
+    auto load_tile = [&]() {
+        if (kind != 2) return;
         const double* ar = Cc + (long long)(16 * I + (lane & 15)) * kSwNb + (lane >> 4);
         const double* cr = Cc + (long long)(16 * J + (lane & 15)) * kSwNb + (lane >> 4);
 #pragma unroll
@@ -1241,18 +1326,22 @@ __global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlArgs a, int k) 
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc[q] = p.A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)];
-    }
+    };
     if (wv == 0) {
         const int l = lane & 31, h = lane >> 5;
         double r[16], prod;
         int bad;
-        pivot_block_sweep(Cc, k0, rowb, r, prod, bad);
+        if constexpr (PAIR) pivot_block_sweep2(Cc, k0, rowb, r, prod, bad);
+        else pivot_block_sweep(Cc, k0, rowb, r, prod, bad);
 #pragma unroll
         for (int jj = 0; jj < 16; ++jj) Pl[l * kSwNb + 16 * h + jj] = -r[jj];
         if (blockIdx.x == 0 && lane == 0) {
             p.acc[0] += log(prod);
             if (bad && p.acc[1] == 0.0) p.acc[1] = (double)(k0 + bad);
         }
+        load_tile();
+    } else {
+        load_tile();
     }
     __syncthreads();
     if (kind == 1) {
@@ -1558,7 +1647,8 @@ int launch_split(const LmlArgs& a, int B, hipStream_t s) {
     }
     for (int k = 0; k < nbk; ++k) {
         if (fuse) {
-            hipLaunchKernelGGL(sw_step_kernel, dim3(nwg, B), dim3(kUpdThreads), 0, s, a, k);
+            if (a.pair) hipLaunchKernelGGL(sw_step_kernel<true>, dim3(nwg, B), dim3(kUpdThreads), 0, s, a, k);
+            else hipLaunchKernelGGL(sw_step_kernel<false>, dim3(nwg, B), dim3(kUpdThreads), 0, s, a, k);
             MPO_LAUNCH_CHECK();
         } else {
             hipLaunchKernelGGL(sw_pivot_kernel, dim3(1, B), dim3(64), 0, s, a, k);
@@ -1661,6 +1751,10 @@ int mpo_gp_lml_grad(const double* X, const double* y_norm, int n, int d, const d
               reinterpret_cast<double*>(mpo::align_up(reinterpret_cast<uintptr_t>(ws), 256)),
               split ? ss_ws_doubles(n, d) : sweep ? sw_ws_doubles(n, d) : fit_ws_doubles(n, d, use_lds), 0};
     if (const char* e = getenv("MPO_FIT_DEBUG")) a.stop = atoi(e);
+    {
+        const char* e = getenv("MPO_FIT_PAIR");
+        a.pair = !(e && e[0] == '0');
+    }
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (split) {
         MPO_CHECK_ARG(batch <= 65535, "mpo_gp_lml_grad: batch %d too large", batch);

@@ -173,3 +173,20 @@ def test_fused_split_sweep_reports_failure(monkeypatch):
     assert lml[1] == -np.inf and np.all(grad[1] == 0.0)
     l2, g2, _ = dev.evaluate(T[2:3])
     assert l2[0] == lml[2] and np.array_equal(g2[0], grad[2])
+
+
+@pytest.mark.parametrize("fuse", ["0", "1"])
+@pytest.mark.parametrize("name", ["n57_d3", "n130_d6", "n230_d4", "n256_d10", "n500_d10"])
+def test_paired_pivot_sweep_is_bit_identical(name, fuse, monkeypatch):
+    """r03: pivot_block_sweep2 (two sweep steps per LDS broadcast round, every lane
+    forming row c + 1 after step c and its own column-(c+1) entry itself) runs the
+    one-step sweep's operations on the same operands: the same bits (MPO_FIT_PAIR=0
+    is the one-step sweep), in both the fused and the launch-sequence forms."""
+    monkeypatch.setenv("MPO_FIT_FUSE", fuse)
+    dev, _ = _lml(name)
+    T = G[name + "_theta"]
+    monkeypatch.setenv("MPO_FIT_PAIR", "0")
+    l0, g0, i0 = dev.evaluate(T)
+    monkeypatch.setenv("MPO_FIT_PAIR", "1")
+    l1, g1, i1 = dev.evaluate(T)
+    assert np.array_equal(i0, i1) and np.array_equal(l0, l1) and np.array_equal(g0, g1)
