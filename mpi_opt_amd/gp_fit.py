@@ -81,23 +81,30 @@ class DeviceLML:
         self.theta_h = torch.empty((batch, k), dtype=torch.float64).pin_memory()
         self.out_h = torch.empty(batch * (k + 1) + (batch + 1) // 2, dtype=torch.float64).pin_memory()
         self._cap = batch
+        # one round's call, its pointers resolved once (a round is ~100-400 us of
+        # device time; ctypes argument packing and tensor data_ptr lookups were ~10 us of it)
+        self._th_np, self._out_np = self.theta_h.numpy(), self.out_h.numpy()
+        fn = L.mpo_gp_lml_grad_host
+        args = (_lib.ptr(self.X), _lib.ptr(self.y), self.n, self.d, self.theta_h.data_ptr())
+        tail = (self.out_h.data_ptr(), _lib.ptr(self.io), self.io_bytes, _lib.ptr(self.ws), self.ws_bytes, self._stream)
+        self._call = lambda B: fn(*args, B, *tail)
 
     def evaluate(self, thetas):
         """thetas [B, d+2] (log space) -> (lml [B], grad [B, d+2], info [B]) as numpy:
         one ``mpo_gp_lml_grad_host`` call (copy in, objective, copy out, sync)."""
-        thetas = np.ascontiguousarray(np.atleast_2d(np.asarray(thetas, dtype=np.float64)))
+        thetas = np.asarray(thetas, dtype=np.float64)
+        if thetas.ndim == 1:
+            thetas = thetas[None, :]
         B = thetas.shape[0]
         if thetas.shape[1] != self.d + 2:
             raise ValueError(f"theta has {thetas.shape[1]} entries, expected d+2={self.d + 2}")
         self._ensure(B)
         k = self.d + 2
-        th = self.theta_h.numpy()
-        th[:B] = thetas
-        _lib.check(_lib.lib().mpo_gp_lml_grad_host(
-            _lib.ptr(self.X), _lib.ptr(self.y), self.n, self.d, self.theta_h.data_ptr(), B,
-            self.out_h.data_ptr(), _lib.ptr(self.io), self.io_bytes, _lib.ptr(self.ws), self.ws_bytes,
-            self._stream), "mpo_gp_lml_grad_host")
-        h = self.out_h.numpy()
+        self._th_np[:B] = thetas
+        rc = self._call(B)
+        if rc != 0:
+            _lib.check(rc, "mpo_gp_lml_grad_host")
+        h = self._out_np
         return (h[:B].copy(), h[B:B + B * k].reshape(B, k).copy(), h[B + B * k:].view(np.int32)[:B].copy())
 
 
@@ -160,21 +167,25 @@ class _LbfgsbRun:
     def advance(self, setulb):
         """Run setulb until it needs f, g at a new point (returns that point) or
         stops (returns None)."""
+        task = self.task
         while True:
-            self.g = self.g.astype(np.float64)
+            if self.g.dtype != np.float64:     # scipy's g.astype(np.float64); deliver() hands float64 already
+                self.g = self.g.astype(np.float64)
             setulb(self.m, self.x, self.low, self.up, self.nbd, self.f, self.g, self.factr, self.pgtol, self.wa,
-                   self.iwa, self.task, self.lsave, self.isave, self.dsave, self.maxls, self.ln_task)
-            if self.task[0] == 3:
-                if np.array_equal(self.x, self.sf_x):
+                   self.iwa, task, self.lsave, self.isave, self.dsave, self.maxls, self.ln_task)
+            t0 = task[0]
+            if t0 == 3:
+                # ScalarFunction's cache: the same x (np.array_equal of same-shape float arrays)
+                if self.sf_x is not None and bool((self.x == self.sf_x).all()):
                     self.f, self.g = self.sf_f, self.sf_g
                     continue
                 return self.x.copy()
-            if self.task[0] == 1:
+            if t0 == 1:
                 self.nit += 1
                 if self.nit >= self.maxiter:
-                    self.task[0], self.task[1] = 5, 504
+                    task[0], task[1] = 5, 504
                 elif self.nfev > self.maxfun:
-                    self.task[0], self.task[1] = 5, 502
+                    task[0], task[1] = 5, 502
                 continue
             self.done = True
             return None
@@ -196,8 +207,9 @@ def lbfgsb_batched(evaluate, starts, bounds, ftol=MINIMIZE_FTOL, gtol=1e-5, maxi
         ids = sorted(want)
         f, g = evaluate(np.stack([want[i] for i in ids]), ids)
         rounds += 1
+        g = np.asarray(g, dtype=np.float64)
         for k, i in enumerate(ids):
-            runs[i].deliver(want[i], float(f[k]), np.array(g[k], dtype=np.float64))
+            runs[i].deliver(want[i], float(f[k]), g[k].copy())
         nxt = {}
         for i in ids:
             x = runs[i].advance(setulb)
