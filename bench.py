@@ -756,13 +756,18 @@ def protocol_refits(world_size, block_size, num_iterations):
 
 
 def fit_refit_cost(samples, powers=(0, 1, 2)):
-    """Least-squares t(n) = sum_p c_p n^p over measured (n, seconds) refit +
-    proposal samples; returns [(p, c_p)]."""
+    """Non-negative least-squares t(n) = sum_p c_p n^p over measured (n, seconds)
+    refit + proposal samples; returns [(p, c_p)].  Non-negative: a refit never gets
+    cheaper with more observations, and a free fit through three noisy host samples
+    gave a negative cubic term (t < 0 past n ~ 350) that under-priced the host path."""
+    from scipy.optimize import nnls
+
     n = np.array([s[0] for s in samples], dtype=float)
     t = np.array([s[1] for s in samples], dtype=float)
     A = np.stack([n ** p for p in powers], 1)
-    coef, *_ = np.linalg.lstsq(A, t, rcond=None)
-    return [(int(p), float(c)) for p, c in zip(powers, coef)]
+    scale = np.abs(A).max(0)
+    coef, _ = nnls(A / scale, t)
+    return [(int(p), float(c / sc)) for p, c, sc in zip(powers, coef, scale)]
 
 
 def _price(curve, ns):
