@@ -59,6 +59,8 @@ struct LmlArgs {
     long long ws_stride;
     int stop;             // diagnostics only (env MPO_FIT_DEBUG): return after phase 1/2/3/4
     int pair;             // split sweep: pivot_block_sweep2 (two steps per LDS round, MPO_FIT_PAIR != 0)
+    const double* theta_src;  // fused split sweep, host-staged call: theta in pinned host memory (device
+                              // view), read by sw_xs_build_kernel and copied to `theta`; else nullptr
 };
 
 __host__ __device__ inline long long fit_tri(long long n) { return n * (n + 1) / 2; }
@@ -878,8 +880,9 @@ __device__ __forceinline__ SsPtrs ss_ptrs(const LmlArgs& a, int b) {
 }
 
 template <int DP>
-__device__ __forceinline__ void ss_theta(const LmlArgs& a, int b, double& amp, double& noise, double (&ls)[DP]) {
-    const double* th = a.theta + (long long)b * (a.d + 2);
+__device__ __forceinline__ void ss_theta(const LmlArgs& a, int b, double& amp, double& noise, double (&ls)[DP],
+                                         const double* src = nullptr) {
+    const double* th = (src ? src : a.theta) + (long long)b * (a.d + 2);
     amp = exp(th[0]);
     noise = exp(th[a.d + 1]);
 #pragma unroll
@@ -958,7 +961,9 @@ __global__ __launch_bounds__(1024) void sw_xs_build_kernel(LmlArgs a) {
     const int b = blockIdx.y, n = a.n, d = a.d, np = (int)sw_np(n);
     const SsPtrs p = ss_ptrs(a, b);
     double amp, noise, ls[DP];
-    ss_theta<DP>(a, b, amp, noise, ls);
+    ss_theta<DP>(a, b, amp, noise, ls, a.theta_src);   // host-staged call: theta straight from pinned memory
+    if (a.theta_src && blockIdx.x == 0 && threadIdx.x < d + 2)   // ... and the device copy the later kernels read
+        const_cast<double*>(a.theta)[(long long)b * (d + 2) + threadIdx.x] = a.theta_src[(long long)b * (d + 2) + threadIdx.x];
     const int rows = min(n, 16 * (int)blockIdx.x + 16);
     for (int e = threadIdx.x; e < rows * d; e += blockDim.x) {
         const int i = e / d, c = e % d;
@@ -1711,6 +1716,13 @@ inline bool use_split(int n) {
     return n > kSplitMinN;
 }
 
+// the fused split sweep (launch_split's fuse_build): the host-staged call may hand it theta
+// and the outputs in pinned host memory
+inline bool fit_fused_split(int n, int dp) {
+    const char* fe = getenv("MPO_FIT_FUSE");
+    return use_split(n) && !(fe && fe[0] == '0') && (size_t)sw_np(n) * dp * sizeof(double) <= 64 * 1024;
+}
+
 template <bool kLds, int DP>
 int launch_lml(const LmlArgs& a, int B, hipStream_t s) {
     auto kern = lml_grad_kernel<kLds, DP>;
@@ -1732,8 +1744,18 @@ size_t mpo_gp_lml_ws_bytes(int n, int d, int batch) {
     return ((size_t)per * batch + (size_t)batch * kPairGroups * 34) * sizeof(double) + 256;   // + pair partials
 }
 
+static int lml_grad_impl(const double* X, const double* y_norm, int n, int d, const double* theta,
+                         const double* theta_src, int batch, double* lml, double* grad, int32_t* info, void* ws,
+                         size_t ws_bytes, void* stream);
+
 int mpo_gp_lml_grad(const double* X, const double* y_norm, int n, int d, const double* theta, int batch,
                     double* lml, double* grad, int32_t* info, void* ws, size_t ws_bytes, void* stream) {
+    return lml_grad_impl(X, y_norm, n, d, theta, nullptr, batch, lml, grad, info, ws, ws_bytes, stream);
+}
+
+static int lml_grad_impl(const double* X, const double* y_norm, int n, int d, const double* theta,
+                         const double* theta_src, int batch, double* lml, double* grad, int32_t* info, void* ws,
+                         size_t ws_bytes, void* stream) {
     MPO_GUARD_BEGIN
     MPO_CHECK_ARG(X && y_norm && theta && lml && grad && info && ws, "mpo_gp_lml_grad: null pointer");
     MPO_CHECK_ARG(n > 0 && d > 0 && batch > 0, "mpo_gp_lml_grad: bad shape n=%d d=%d batch=%d", n, d, batch);
@@ -1755,6 +1777,8 @@ int mpo_gp_lml_grad(const double* X, const double* y_norm, int n, int d, const d
         const char* e = getenv("MPO_FIT_PAIR");
         a.pair = !(e && e[0] == '0');
     }
+    a.theta_src = split && fit_fused_split(n, dp) ? theta_src : nullptr;
+    MPO_CHECK_ARG(!theta_src || a.theta_src, "mpo_gp_lml_grad: a host theta source needs the fused split sweep");
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (split) {
         MPO_CHECK_ARG(batch <= 65535, "mpo_gp_lml_grad: batch %d too large", batch);
@@ -1814,6 +1838,26 @@ int mpo_gp_lml_grad_host(const double* X, const double* y_norm, int n, int d, co
     double* grad = out + batch;
     int32_t* info = reinterpret_cast<int32_t*>(grad + (size_t)batch * k);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    // Pinned host buffers on the fused split sweep: the first kernel reads theta from
+    // the host copy and the last writes lml | grad | info straight into out_host --
+    // no copy launches around the round (two of ~20 launches, ~7 us at n = 256).
+    // MPO_FIT_HOSTIO=0 keeps the copies.
+    const int dp = fit_dp(d);
+    const char* he = getenv("MPO_FIT_HOSTIO");
+    if (dp > 0 && fit_fused_split(n, dp) && !(he && he[0] == '0')) {
+        hipPointerAttribute_t ta{}, oa{};
+        if (hipPointerGetAttributes(&ta, theta_host) == hipSuccess && ta.type == hipMemoryTypeHost && ta.devicePointer &&
+            hipPointerGetAttributes(&oa, out_host) == hipSuccess && oa.type == hipMemoryTypeHost && oa.devicePointer) {
+            double* od = static_cast<double*>(oa.devicePointer);
+            const int rc = lml_grad_impl(X, y_norm, n, d, th, static_cast<const double*>(ta.devicePointer), batch, od,
+                                         od + batch, reinterpret_cast<int32_t*>(od + batch + (size_t)batch * k), ws,
+                                         ws_bytes, stream);
+            if (rc != MPO_OK) return rc;
+            MPO_HIP(hipStreamSynchronize(s));
+            return MPO_OK;
+        }
+        (void)hipGetLastError();   // an unregistered pointer: the copies below
+    }
     MPO_HIP(hipMemcpyAsync(th, theta_host, (size_t)batch * k * sizeof(double), hipMemcpyHostToDevice, s));
     const int rc = mpo_gp_lml_grad(X, y_norm, n, d, th, batch, lml, grad, info, ws, ws_bytes, stream);
     if (rc != MPO_OK) return rc;

@@ -190,3 +190,22 @@ def test_paired_pivot_sweep_is_bit_identical(name, fuse, monkeypatch):
     monkeypatch.setenv("MPO_FIT_PAIR", "1")
     l1, g1, i1 = dev.evaluate(T)
     assert np.array_equal(i0, i1) and np.array_equal(l0, l1) and np.array_equal(g0, g1)
+
+
+@pytest.mark.parametrize("name", ["n130_d6", "n500_d10"])
+def test_host_staged_direct_io_is_bit_identical(name, monkeypatch):
+    """r03: on the fused split sweep the host-staged call hands the kernels theta and
+    the output rows in pinned host memory (no copy launches); MPO_FIT_HOSTIO=0 keeps
+    the copies.  Same bits, repeated calls included, and a failed theta still reports."""
+    dev, _ = _lml(name)
+    T = G[name + "_theta"]
+    monkeypatch.setenv("MPO_FIT_HOSTIO", "0")
+    l0, g0, i0 = dev.evaluate(T)
+    monkeypatch.setenv("MPO_FIT_HOSTIO", "1")
+    for _ in range(3):
+        l1, g1, i1 = dev.evaluate(T)
+        assert np.array_equal(i0, i1) and np.array_equal(l0, l1) and np.array_equal(g0, g1)
+    T2 = T[:2].copy()
+    T2[1, 0] = np.nan
+    l2, g2, i2 = dev.evaluate(T2)
+    assert i2[0] == 0 and i2[1] >= 1 and l2[1] == -np.inf and np.all(g2[1] == 0.0) and l2[0] == l0[0]
