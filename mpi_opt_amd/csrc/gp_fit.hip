@@ -1020,6 +1020,13 @@ __global__ __launch_bounds__(1024) void sw_xs_build_kernel(LmlArgs a) {
 // perform in pivot_block_sweep -- so the result is the same bits with half the LDS
 // round trips (and half the serial latency chains) at 16 more FMAs per two steps.
 // rowb: 64 doubles.
+// r = 0 on the active lanes as 16 exec-masked v_mov_b64 (a branch): written as plain
+// stores the compiler if-converts the branch into two v_cndmask_b32 per double
+__device__ __forceinline__ void zero_row(double (&r)[16]) {
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) asm volatile("v_mov_b64 %0, 0" : "=v"(r[jj]));
+}
+
 __device__ __forceinline__ void pivot_block_sweep2(const double* __restrict__ C, int k0, double* rowb,
                                                    double (&r)[16], double& prod, int& bad) {
     const int lane = threadIdx.x & 63;
@@ -1038,10 +1045,7 @@ __device__ __forceinline__ void pivot_block_sweep2(const double* __restrict__ C,
 #pragma unroll
             for (int jj = 0; jj < 16; ++jj) rowb[32 * (l - c) + 16 * h + jj] = r[jj];
         }
-        if (piv1) {
-#pragma unroll
-            for (int jj = 0; jj < 16; ++jj) r[jj] = 0.0;
-        }
+        if (piv1) zero_row(r);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         // ---- step c
         const double pv1 = rowb[c];
@@ -1078,10 +1082,7 @@ __device__ __forceinline__ void pivot_block_sweep2(const double* __restrict__ C,
         const double ip2 = 1.0 / pv2;
         const double t2 = colv2p * ip2;
         const double f2 = piv2 ? ip2 : -t2;
-        if (piv2) {
-#pragma unroll
-            for (int jj = 0; jj < 16; ++jj) r[jj] = 0.0;
-        }
+        if (piv2) zero_row(r);
 #pragma unroll
         for (int jj = 0; jj < 16; ++jj) {
             const double upd = fma(f2, q2[jj], r[jj]);
@@ -1593,11 +1594,15 @@ __global__ __launch_bounds__(256) void sw_pairs_final_kernel(LmlArgs a, double* 
     if (threadIdx.x < DP + 2) {
         const int c = threadIdx.x;
         partials[((long long)b * gridDim.x + blockIdx.x) * (DP + 2) + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
-        __threadfence();
     }
     __syncthreads();
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0) {
+        // one device-scope release per workgroup (after the barrier it covers the
+        // partial rows written by threads 0 .. DP+1): each fence writes back this
+        // XCD's L2, and one per writing thread cost ~4 us per launch
+        __threadfence();
         last = atomicAdd(reinterpret_cast<unsigned*>(p.acc + 2), 1u) == gridDim.x - 1;
+    }
     __syncthreads();
     if (!last) return;
     __threadfence();
