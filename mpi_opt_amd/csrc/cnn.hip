@@ -535,6 +535,224 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
 }
 
 // ============================================================================
+// Input gradient of conv2 by scatter (r03, MPO_DG_SCATTER):
+//   dz1[b][y+ky][x+kx][c] += sum_f dz2[b][y][x][f] * w2[ky][kx][c][f]
+// input-stationary: every (tap, dz2 pixel) pair contributing to the band is one
+// MFMA row exactly once, so the MFMAs are the algorithmic count (the halo-tap
+// gather above runs 1.16-1.64x of it by k).  One workgroup = (member, sample,
+// output rows [y0, y0+R)); the dz2 rows feeding the band are staged once in the
+// LDS (the gather's layout).  For a tap the feeding dz2 pixels are one contiguous
+// run of flattened (y, x) indices, cut into 16-pixel MFMA tiles (M = pixels, N =
+// 16 channels c, K = F4 channels f); the tile's 16 output pixels are distinct, so
+// its 4 values per lane go to the band with ds_add_f32 on distinct addresses.
+// Determinism: each wave accumulates into its OWN band [R][H1][16] (one channel
+// group, a fixed subset of the taps, taps and tiles in a fixed order), and the
+// bands of a channel group are summed in wave order in the epilogue (ReLU gate of
+// a1 applied there).  Wave w: channel group w % NT, a contiguous tap range.
+// Measured (profiles/r03/scatter_ab.txt, 320 members, one GPU): the band's
+// read-add-write (8 LDS reads + 8 writes per two tiles; ds_add_f32 was ~10x slower
+// still) and the per-workgroup setup outweigh the 1.16-1.64x MFMAs it saves:
+// 48.3 vs 42.0 ms per train batch for all members, 45.2 with only F > 32 on it.
+// Off by default (MPO_DG_SCATTER=1 / 2 select it); kept, tested, for the record.
+// ============================================================================
+// per-wave band stride: [R][H1][16] and 64 floats a lane may write past a tap's run
+__host__ __device__ inline int dgs_band_floats(int R, int H1) { return R * H1 * 16 + 64; }
+
+// The per-wave tap loop of conv_dgrad_scatter_kernel for KS k-steps: B (the tap's
+// weights) in registers, the tap's tiles two at a time (two independent MFMA chains,
+// the next pair's LDS offsets read one pair ahead), results added to the wave's
+// band.  Tile rows past the tap's run (qb) are computed from in-bounds LDS data and
+// discarded.
+template <int NT>
+struct DgsTaps {
+    const float* img;
+    const int* aoff;
+    const int* boff;
+    float* band;
+    const float* W;
+    int k, H1, H2, F4, y0, R, gy_lo, gy_hi, wc, krow, kcol, dump;
+
+    template <int KS>
+    __device__ __forceinline__ void load_b(int t, float (&bw)[KS]) const {
+        constexpr int N16 = NT * 16;
+        const int ky = t / k, kx = t - ky * k;
+        const int rt = (k - 1 - ky) * k + (k - 1 - kx);
+        // w2[ky][kx][c][f] = w2t[rot(t)][f][c] (zero-padded to F4 x N16)
+        const float* wsrc = W + ((long long)rt * F4 + krow) * N16 + wc * 16 + kcol;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) bw[ks] = wsrc[(long long)ks * 4 * N16];
+    }
+
+    // taps [t0, t1) of channel group wc into `band`
+    template <int KS>
+    __device__ __forceinline__ void run(int t0, int t1) {
+        if (t0 >= t1) return;
+        float bw[KS], bn[KS];
+        load_b<KS>(t0, bw);
+        for (int t = t0; t < t1; ++t) {
+            // the next tap's weights load (L2) while this tap's tiles run
+            if (t + 1 < t1) load_b<KS>(t + 1, bn);
+            const int ky = t / k, kx = t - ky * k;
+            const int ylo = max(gy_lo, y0 - ky), yhi = min(gy_hi, y0 + R - ky);
+            const int qa = (ylo - gy_lo) * H2, qb = (yhi - gy_lo) * H2;
+            const int tapoff = (ky * H1 + kx) * 16;
+            // tile row m is pixel q0 + perm(m), perm(m) = 4 (m & 3) + (m >> 2): output row
+            // krow * 4 + r is then pixel q0 + 4 r + krow, so the 4 lane groups of one
+            // read-add-write instruction hit consecutive pixels (alternate 16-bank
+            // halves of the [pix][16] band: 2-way instead of 4-way bank conflicts)
+            const int pm = 4 * (kcol & 3) + (kcol >> 2);
+            int ab0 = aoff[qa + pm] + krow, ab1 = aoff[qa + 16 + pm] + krow;
+            for (int q0 = qa; q0 < qb; q0 += 32) {
+                float a0[KS], a1[KS];
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) {
+                    a0[ks] = img[ab0 + 4 * ks];
+                    a1[ks] = img[ab1 + 4 * ks];
+                }
+                // next pair's offsets (the tables carry 64 entries of slack)
+                ab0 = aoff[q0 + 32 + pm] + krow;
+                ab1 = aoff[q0 + 48 + pm] + krow;
+                const int p0 = q0 + krow, p1 = p0 + 16;   // output row krow*4 + r: pixel p + 4 r
+                int o0[4], o1[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    o0[r] = boff[p0 + 4 * r];
+                    o1[r] = boff[p1 + 4 * r];
+                }
+                f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) {
+                    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[ks], bw[ks], c0, 0, 0, 0);
+                    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[ks], bw[ks], c1, 0, 0, 0);
+                }
+                // C/D: row = krow * 4 + r (pixel), col = kcol (channel).  The band is this
+                // wave's alone and an instruction's 64 addresses are distinct: a plain
+                // read-add-write (LDS ops of one wave complete in order; ds_add_f32
+                // measured ~10x slower here)
+                float* d0[4];
+                float* d1[4];
+                float v0[4], v1[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    d0[r] = band + (p0 + 4 * r < qb ? o0[r] + tapoff + kcol : dump + krow * 16 + kcol);
+                    d1[r] = band + (p1 + 4 * r < qb ? o1[r] + tapoff + kcol : dump + krow * 16 + kcol);
+                    v0[r] = *d0[r];
+                    v1[r] = *d1[r];
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    *d0[r] = v0[r] + c0[r];
+                    *d1[r] = v1[r] + c1[r];
+                }
+            }
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) bw[ks] = bn[ks];
+        }
+    }
+};
+
+template <int NT>
+__global__ __launch_bounds__(256) void conv_dgrad_scatter_kernel(StepArgs a, const ConvItem* __restrict__ items) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const ConvItem it = items[xcd_item(a.xcd)];
+    const Member& mb = a.mem[it.member];
+    const int k = mb.k, F = mb.F, H2 = mb.H2, H1 = mb.H1;
+    const int pad = k - 1;
+    const int F4 = (F + 3) & ~3;
+    const int Fp = dgrad_fp(F);
+    const int R = it.R, y0 = it.y0;
+    const int gy_lo = max(0, y0 - pad), gy_hi = min(H2, y0 + R);   // dz2 rows feeding the band
+    const int rows = gy_hi - gy_lo;
+    const int npix = rows * H2;
+    const float* in = a.act + mb.dz2 + (long long)it.b * H2 * H2 * F;
+    const float* W = a.act + mb.w2t;
+    float* out = a.act + mb.dz1 + (long long)it.b * H1 * H1 * F;
+    const float* relu_mask = a.act + mb.a1 + (long long)it.b * H1 * H1 * F;
+
+    const int RS = dgrad_rs(H2, F);
+    const int zoff = align4(rows * RS);
+    float* img = smem;                                               // [rows][RS], then 64 zero floats
+    int* aoff = reinterpret_cast<int*>(smem + zoff + 64);            // [npix + 64]: LDS offset of pixel q
+    int* boff = aoff + align4(npix + 64);                            // [npix + 64]: band offset (tap 0,0)
+    const int BF = dgs_band_floats(R, H1);
+    float* bands = smem + zoff + 64 + 2 * align4(npix + 64);          // [4][BF]
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int krow = lane >> 4, kcol = lane & 15;
+
+    for (int e = tid; e < zoff + 64; e += 256) img[e] = 0.f;
+    for (int e = tid; e < 4 * BF; e += 256) bands[e] = 0.f;
+    for (int q = tid; q < npix + 64; q += 256) {
+        const int yy = q / H2, xx = q - yy * H2;
+        const bool v = q < npix;
+        aoff[q] = v ? yy * RS + xx * Fp : zoff;
+        boff[q] = v ? ((gy_lo + yy - y0) * H1 + xx) * 16 : 0;
+    }
+    __syncthreads();
+    for (int r = 0; r < rows && a.debug != 2; ++r)
+        stage_row(in + (long long)(gy_lo + r) * H2 * F, img + r * RS, H2 * F, F, Fp, tid);
+    __syncthreads();
+
+    // work split: wave w takes channel group w % NT and the (w / NT)-th of the
+    // contiguous tap ranges that group's waves share.  (An even split of the NT * k^2
+    // (group, tap) units -- two band slots for the waves straddling a group at NT = 3
+    // -- measured slower: the extra slots cost band rows per workgroup.)
+    const int nt2 = k * k;
+    const int wc = wave % NT, ph = wave / NT, nph = (4 - wc + NT - 1) / NT;
+    if (a.debug != 1) {
+        // K = F4 channels f in KS = F4 / 4 k-steps: one fully unrolled loop body per KS
+        // (a runtime bound inside the unrolled loop put a branch around every MFMA)
+        const int KS = F4 >> 2;
+        DgsTaps<NT> r{img, aoff, boff, nullptr, W, k, H1, H2, F4, y0, R, gy_lo, gy_hi, 0, krow, kcol, BF - 64};
+        {
+            const int t0 = ph * nt2 / nph, t1 = (ph + 1) * nt2 / nph;
+            r.wc = wc;
+            r.band = bands + wave * BF;
+            switch (KS) {
+                case 3: r.template run<3>(t0, t1); break;
+                case 4: r.template run<4>(t0, t1); break;
+                case 5: r.template run<5>(t0, t1); break;
+                case 6: r.template run<6>(t0, t1); break;
+                case 7: r.template run<7>(t0, t1); break;
+                case 8: r.template run<8>(t0, t1); break;
+                case 9: r.template run<9>(t0, t1); break;
+                case 10: r.template run<10>(t0, t1); break;
+                case 11: r.template run<11>(t0, t1); break;
+                case 12: r.template run<12>(t0, t1); break;
+                default: r.template run<13>(t0, t1); break;
+            }
+        }
+    }
+    __syncthreads();
+    // ---- epilogue: the band pixels, channels c < F: bands of c's group summed in wave order, ReLU gate
+    // one pixel per wave and loop step, channel = lane: no division, and the gate
+    // loads of a wave's 4 pixels issue together (restrict: out never aliases a1)
+    const int band_pix = R * H1;
+    if (lane < F) {
+        const int g = lane >> 4, c16 = lane & 15;
+        const float* __restrict__ gate = relu_mask + (long long)y0 * H1 * F + lane;
+        float* __restrict__ dst = out + (long long)y0 * H1 * F + lane;
+        for (int pix = wave; pix < band_pix; pix += 16) {
+            float mk[4], v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int px = pix + 4 * u;
+                mk[u] = px < band_pix ? gate[(long long)px * F] : 0.f;
+                float acc = 0.f;
+                if (px < band_pix)
+                    for (int w = g; w < 4; w += NT) acc += bands[w * BF + px * 16 + c16];   // wave order
+                v[u] = acc;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int px = pix + 4 * u;
+                if (px < band_pix) dst[(long long)px * F] = mk[u] > 0.f ? v[u] : 0.f;
+            }
+        }
+    }
+}
+
+// ============================================================================
 // Weight gradient: dW[(ky,kx,c)][n] = sum_{b,y,x} in[b][y+ky][x+kx][c] * dout[b][y][x][n]
 // (plus the bias gradient as row Kw = k*k*Cin: an all-ones A row).
 // GEMM view M = Kw + 1 rows of (ky,kx,c), N = F, K = pixels.  One workgroup =
@@ -1362,6 +1580,7 @@ struct Plan {
     bool bound = false;
     size_t lds_conv_max = 0, lds_wg_max = 0;
     bool wg1_wave = true;   // conv1 weight gradient on conv1_wgrad_kernel (env MPO_WG1_WAVE=0: the m-group kernel)
+    int dg_scatter = 0;     // conv2 input gradient by scatter (conv_dgrad_scatter_kernel, env MPO_DG_SCATTER=1)
 };
 
 size_t conv_lds_bytes(int rows, int Wp, int Cin, int Ho, int K, int nt) {
@@ -1369,6 +1588,18 @@ size_t conv_lds_bytes(int rows, int Wp, int Cin, int Ho, int K, int nt) {
     const int Fp = fwd_fp(Cin);
     (void)Fp;
     return (size_t)(align4(rows * fwd_rs(Wp, Cin, Ho)) + ((K + 15) & ~15) + kKoffSlack) * sizeof(float);
+}
+
+// MPO_DG_SCATTER: 0 = the halo-tap gather for every member, 1 = the scatter for every
+// member, 2 = the scatter where it measured faster (F > 32: 3-4 channel groups; for
+// small F its per-tile read-add-write outweighs the gather's halo MFMAs)
+inline bool dg_uses_scatter(int mode, int nt) { return mode == 1 || (mode == 2 && nt >= 3); }
+
+size_t dgrad_scatter_lds_bytes(int R, int k, int F, int H1, int H2) {
+    const int rows = std::min(H2, R + k - 1);
+    const int npix = rows * H2;
+    return (size_t)(align4(rows * dgrad_rs(H2, F)) + 64 + 2 * align4(npix + 64) + 4 * dgs_band_floats(R, H1)) *
+           sizeof(float);
 }
 
 size_t dgrad_lds_bytes(int R, int k, int F, int H2) {
@@ -1496,9 +1727,17 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         const size_t dgb = (size_t)kdg << 10;
         int Rd = 4 * std::max(1, 16 / ((m.H1 + 3) / 4));
         while (Rd > 4 && dgrad_lds_bytes(Rd, k, F, m.H2) > dgb) Rd -= 4;
+        if (i == 0) P.dg_scatter = env_int("MPO_DG_SCATTER", 0);
+        const bool sc = dg_uses_scatter(P.dg_scatter, nt);
+        if (sc) {
+            // scatter: bands of Rd rows within the LDS budget (the dz2 rows + 4 private bands)
+            const size_t sgb = (size_t)env_int("MPO_DGS_KB", 64) << 10;
+            Rd = std::max(1, std::min(m.H1, env_int("MPO_DGS_ROWS", 8)));
+            while (Rd > 1 && dgrad_scatter_lds_bytes(Rd, k, F, m.H1, m.H2) > sgb) --Rd;
+        }
         const size_t l1 = conv_lds_bytes(R1 + k - 1, kImg, 1, m.H1, k * k, nt);
         const size_t l2 = conv_lds_bytes(R2 + k - 1, m.H1, F, m.H2, k * k * F, nt);
-        const size_t ld = dgrad_lds_bytes(Rd, k, F, m.H2);
+        const size_t ld = sc ? dgrad_scatter_lds_bytes(Rd, k, F, m.H1, m.H2) : dgrad_lds_bytes(Rd, k, F, m.H2);
         L1[i] = l1; L2[i] = l2; LD[i] = ld;
         for (int b = 0; b < B; ++b) {
             for (int y = 0; y < m.H1; y += R1) P.conv1.push_back({i, b, y, std::min(R1, m.H1 - y)});
@@ -1611,6 +1850,15 @@ hipError_t launch_dgrad_nt(const StepArgs& a, const ConvItem* items, int count, 
     return hipGetLastError();
 }
 
+template <int NT>
+hipError_t launch_dgrad_scatter_nt(const StepArgs& a, const ConvItem* items, int count, size_t lds, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    auto kern = conv_dgrad_scatter_kernel<NT>;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(count), dim3(256), lds, s, a, items);
+    return hipGetLastError();
+}
+
 template <int OP, int NT>
 hipError_t launch_wg_nt(const StepArgs& a, const WgItem* items, int count, size_t lds, int mt, hipStream_t s) {
     if (count <= 0) return hipSuccess;
@@ -1666,7 +1914,9 @@ hipError_t launch_conv(Plan& P, const StepArgs& a, size_t table_off, const Bucke
 hipError_t launch_dgrad(Plan& P, const StepArgs& a, hipStream_t s) {
     const ConvItem* base = dev_table<ConvItem>(P, P.off_dgrad);
     return launch_segs(P, P.bdg, "conv2_dgrad", s, [&](const Seg& sg) {
-        return MPO_NT_SWITCH(launch_dgrad_nt, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, s);
+        return dg_uses_scatter(P.dg_scatter, sg.nt)
+                   ? MPO_NT_SWITCH(launch_dgrad_scatter_nt, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, s)
+                   : MPO_NT_SWITCH(launch_dgrad_nt, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, s);
     });
 }
 
