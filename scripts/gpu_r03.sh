@@ -32,7 +32,7 @@ step_bench() {
 step_prof() {
   [ "${PROF:-0}" = "0" ] && return 0
   # traces stay on the box (/tmp): only the kernel-stats summary comes back
-  ( cd /tmp && rm -rf /tmp/prof_$TAG && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_$TAG \
+  ( cd /tmp && rm -rf /tmp/prof_$TAG && timeout -k 10 ${PROF_TIMEOUT:-300} rocprofv3 --kernel-trace --stats -d /tmp/prof_$TAG \
       -o run --output-format csv -- python "$GRAFT_REPO_ROOT/bench.py" ${PROF_ARGS:---steps 10 --warmup 2 --no-cpu-baseline --no-pmc} \
       > "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG.log" 2>&1 ) && \
   mkdir -p gpurun_out/prof_$TAG && find /tmp/prof_$TAG -name "*kernel_stats.csv" -exec cp {} gpurun_out/prof_$TAG/ \; && \
