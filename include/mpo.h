@@ -180,6 +180,13 @@ int mpo_gp_ei_score(const MpoGpModel* model, const double* cand, int64_t m,
 int mpo_gp_acq_grad(const MpoGpModel* model, const double* x, int batch, const int32_t* acq,
                     double y_opt, double xi, double kappa, double* f, double* g, void* stream);
 
+/* One polish round from the host: mpo_gp_acq_grad with x, acq, f, g in pinned
+ * (hipHostMalloc / registered) host memory, read and written by the kernel in
+ * place (no staging copies), then a synchronisation of `stream`.  MPO_EINVAL if
+ * a buffer is not pinned host memory. */
+int mpo_gp_acq_grad_host(const MpoGpModel* model, const double* x_host, int batch, const int32_t* acq_host,
+                         double y_opt, double xi, double kappa, double* f_host, double* g_host, void* stream);
+
 /* ------------------------------------------------------------------------
  * Population training of ragged MNIST-CNN trials.
  * Replaces ProcessBlock.train_model -> mpi_learn MPIKFoldManager.train()

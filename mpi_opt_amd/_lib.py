@@ -83,6 +83,7 @@ SIGNATURES = {
                               _P, _SZ, _P]),
     "mpo_gp_ei_score": (_I, [ctypes.POINTER(MpoGpModel), _P, _I64, _D, _D, _P, _P, _P, _P, _P, _SZ, _P]),
     "mpo_gp_acq_grad": (_I, [ctypes.POINTER(MpoGpModel), _P, _I, _P, _D, _D, _D, _P, _P, _P]),
+    "mpo_gp_acq_grad_host": (_I, [ctypes.POINTER(MpoGpModel), _P, _I, _P, _D, _D, _D, _P, _P, _P]),
     "mpo_pop_create": (_I, [ctypes.POINTER(MpoCnnSpec), _I, _I, ctypes.POINTER(ctypes.c_void_p)]),
     "mpo_pop_destroy": (_I, [_P]),
     "mpo_pop_sizes": (_I, [_P, ctypes.POINTER(MpoPopSizes)]),

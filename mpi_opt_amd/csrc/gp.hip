@@ -1666,4 +1666,29 @@ int mpo_gp_acq_grad(const MpoGpModel* model, const double* x, int batch, const i
     MPO_GUARD_END
 }
 
+int mpo_gp_acq_grad_host(const MpoGpModel* model, const double* x_host, int batch, const int32_t* acq_host,
+                         double y_opt, double xi, double kappa, double* f_host, double* g_host, void* stream) {
+    MPO_GUARD_BEGIN
+    MPO_CHECK_ARG(x_host && acq_host && f_host && g_host, "mpo_gp_acq_grad_host: null pointer");
+    auto dev_view = [](const void* h) -> void* {
+        hipPointerAttribute_t at{};
+        if (hipPointerGetAttributes(&at, h) != hipSuccess || at.type != hipMemoryTypeHost || !at.devicePointer) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        return at.devicePointer;
+    };
+    void* xd = dev_view(x_host);
+    void* ad = dev_view(acq_host);
+    void* fd = dev_view(f_host);
+    void* gd = dev_view(g_host);
+    MPO_CHECK_ARG(xd && ad && fd && gd, "mpo_gp_acq_grad_host: buffers must be pinned host memory");
+    const int rc = mpo_gp_acq_grad(model, static_cast<const double*>(xd), batch, static_cast<const int32_t*>(ad), y_opt,
+                                   xi, kappa, static_cast<double*>(fd), static_cast<double*>(gd), stream);
+    if (rc != MPO_OK) return rc;
+    MPO_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    return MPO_OK;
+    MPO_GUARD_END
+}
+
 }  // extern "C"

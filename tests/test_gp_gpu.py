@@ -280,3 +280,24 @@ def test_expanded_distance_far_candidates_fall_back(monkeypatch):
     sd = out["sd"].cpu().numpy()
     assert np.all(np.isfinite(sd))
     assert np.max(np.abs(sd - sd_x) / sd_x) < 1e-9
+
+
+def test_acq_grad_host_requires_pinned_buffers():
+    """mpo_gp_acq_grad_host reads and writes its buffers in place: pageable host
+    memory is refused with MPO_EINVAL before any launch (DeviceGP.acq_grad passes
+    pinned buffers)."""
+    import ctypes
+
+    from mpi_opt_amd import _lib
+
+    f = load(os.path.join(GOLDEN, "gp_ei_n12_d5.npz"))
+    g = device_gp(f)
+    x = np.zeros((2, g.d))
+    a = np.ones(2, dtype=np.int32)
+    fo = np.zeros(2)
+    go = np.zeros((2, g.d))
+    rc = _lib.lib().mpo_gp_acq_grad_host(ctypes.byref(g.model), x.ctypes.data, 2, a.ctypes.data, 0.0, 0.01, 1.96,
+                                         fo.ctypes.data, go.ctypes.data, _lib.stream_handle(g.device))
+    assert rc != 0 and "pinned" in _lib.lib().mpo_last_error().decode()
+    fv, gv = g.acq_grad(f["C"][:3], np.ones(3, dtype=np.int32), float(f["y_opt"]))
+    assert fv.shape == (3,) and gv.shape == (3, g.d) and np.all(np.isfinite(gv))
