@@ -1337,7 +1337,12 @@ __global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlArgs a, int k) 
         const int l = lane & 31, h = lane >> 5;
         double r[16], prod;
         int bad;
-        if constexpr (PAIR) pivot_block_sweep2(Cc, k0, rowb, r, prod, bad);
+        if (a.stop == 23) {   // diagnostics only (MPO_FIT_DEBUG=23): the sweep skipped, timing of the rest
+            prod = 1.0;
+            bad = 0;
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) r[jj] = Cc[(long long)(k0 + l) * kSwNb + 16 * h + jj];
+        } else if constexpr (PAIR) pivot_block_sweep2(Cc, k0, rowb, r, prod, bad);
         else pivot_block_sweep(Cc, k0, rowb, r, prod, bad);
 #pragma unroll
         for (int jj = 0; jj < 16; ++jj) Pl[l * kSwNb + 16 * h + jj] = -r[jj];
