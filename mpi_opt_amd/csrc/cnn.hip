@@ -89,7 +89,8 @@ struct StepArgs {
     float* loss_sum;         // [n_members] running loss sum (eval)
     int* correct;            // [n_members] running correct count (eval)
     long long zero_off;      // 64 zero floats in the activation arena (DMA source past row ends)
-    int debug;               // diagnostics only (env MPO_POP_DEBUG): 1 skip conv MMA loops, 2 skip conv staging
+    int debug;               // diagnostics only (env MPO_POP_DEBUG): 1 skip conv MMA loops, 2 skip conv staging,
+                             // 4 conv fwd / dgrad weight fragments re-read from groups 0-1 (cache-resident; timing only)
     int xcd;                 // 1: XCD-grouped work-item order (xcd_item, env MPO_XCD_SWIZZLE=1); off by default
 };
 
@@ -161,17 +162,45 @@ __host__ __device__ constexpr inline int dgrad_rs(int H2, int F) {
     return H2 * dgrad_fp(F) + ((8 - ((H2 * dgrad_fp(F)) & 31)) & 31);
 }
 
-// Copy n contiguous floats (pixels of cin channels) into an LDS image with
-// pixel stride fp, without a per-element integer division.
-__device__ __forceinline__ void stage_row(const float* __restrict__ src, float* __restrict__ dst, int n, int cin,
-                                          int fp, int tid) {
-    const int q = 256 / cin, r = 256 - q * cin;
-    int gx = tid / cin, c = tid - gx * cin;
-    for (int e = tid; e < n; e += 256) {
-        dst[gx * fp + c] = src[e];
-        c += r;
-        gx += q;
-        if (c >= cin) { c -= cin; ++gx; }
+// Copy rows x w pixels x cin channels of contiguous floats (NHWC rows of one
+// sample) into an LDS image with pixel stride fp and row stride rs.  The element
+// walk (row, pixel, channel) advances by mixed-radix adds (no per-element integer
+// division), and every thread issues kStageBatch loads before their LDS stores:
+// r03 -- a load-then-store loop per row kept ONE global load per thread in flight,
+// and the staging ran ~13 us per conv work item.
+constexpr int kStageBatch = 8;
+__device__ __forceinline__ void stage_rows(const float* __restrict__ src, float* __restrict__ dst, int rows, int w,
+                                           int cin, int fp, int rs, int tid) {
+    const int n = rows * w * cin;
+    int c = tid % cin, t = tid / cin;
+    int x = t % w, r = t / w;
+    const int sc = 256 % cin, st = 256 / cin, sx = st % w, sr = st / w;
+    auto adv = [&]() {
+        c += sc;
+        int cx = 0;
+        if (c >= cin) { c -= cin; cx = 1; }
+        x += sx + cx;
+        int cr = 0;
+        if (x >= w) { x -= w; cr = 1; }
+        r += sr + cr;
+    };
+    int e = tid;
+    for (; e + (kStageBatch - 1) * 256 < n; e += kStageBatch * 256) {
+        float v[kStageBatch];
+        int d[kStageBatch];
+#pragma unroll
+        for (int u = 0; u < kStageBatch; ++u) v[u] = src[e + u * 256];
+#pragma unroll
+        for (int u = 0; u < kStageBatch; ++u) {
+            d[u] = r * rs + x * fp + c;
+            adv();
+        }
+#pragma unroll
+        for (int u = 0; u < kStageBatch; ++u) dst[d[u]] = v[u];
+    }
+    for (; e < n; e += 256) {
+        dst[r * rs + x * fp + c] = src[e];
+        adv();
     }
 }
 
@@ -188,13 +217,13 @@ constexpr int kKoffSlack = 64;
 template <int MT, int NT>
 __device__ __forceinline__ void conv_fwd_loop(const float* __restrict__ img, const int* __restrict__ koff,
                                               const float* __restrict__ W, int ngroups, const int (&pb)[2],
-                                              f32x4 (&acc)[2][NT], int krow, int kcol) {
+                                              f32x4 (&acc)[2][NT], int krow, int kcol, int gmask) {
     constexpr int N16 = NT * 16;
     const float* wsrc = W + krow * N16 + kcol;
     const int* kp = koff + krow * 4;
     float b0[4][NT], b1[4][NT], a0[4][MT], a1[4][MT];
     auto loadB = [&](int g, float (&dst)[4][NT]) {
-        const float* src = wsrc + (long long)g * 16 * N16;
+        const float* src = wsrc + (long long)(g & gmask) * 16 * N16;
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -281,13 +310,15 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
     const int krow = lane >> 4, kcol = lane & 15;
 
     // ---- stage the input rows + the tap-offset table (the only barrier)
-    for (int r = 0; r < rows && a.debug != 2; ++r) {
-        const float* src = in + (long long)(it.y0 + r) * Hin * Cin;
-        float* dst = img + r * RS;
+    if (a.debug != 2) {
+        const float* src = in + (long long)it.y0 * Hin * Cin;
         if (Cin == 1) {
-            for (int e = tid; e < Hin; e += 256) dst[e] = src[e];
+            for (int e = tid; e < rows * Hin; e += 256) {
+                const int r = e / Hin;
+                img[r * RS + e - r * Hin] = src[e];
+            }
         } else {
-            stage_row(src, dst, Hin * Cin, Cin, Fp, tid);
+            stage_rows(src, img, rows, Hin, Cin, Fp, RS, tid);
         }
     }
     for (int kk = tid; kk < K16 + kKoffSlack; kk += 256) {
@@ -322,8 +353,9 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
         for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     __syncthreads();
     const int ngroups = a.debug == 1 ? 0 : K16 >> 4;
-    if (mine == 2) conv_fwd_loop<2, NT>(img, koff, W, ngroups, pb, acc, krow, kcol);
-    else if (mine == 1) conv_fwd_loop<1, NT>(img, koff, W, ngroups, pb, acc, krow, kcol);
+    const int gmask = a.debug == 4 ? 1 : -1;
+    if (mine == 2) conv_fwd_loop<2, NT>(img, koff, W, ngroups, pb, acc, krow, kcol, gmask);
+    else if (mine == 1) conv_fwd_loop<1, NT>(img, koff, W, ngroups, pb, acc, krow, kcol, gmask);
     else return;
 
     // ---- epilogue: C/D map col = lane & 15, row = (lane >> 4) * 4 + r
@@ -389,8 +421,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
 
     for (int e = tid; e < zoff + 64; e += 256) img[e] = 0.f;
     __syncthreads();
-    for (int r = 0; r < rows && a.debug != 2; ++r)
-        stage_row(in + (long long)(gy_lo + r) * H2 * F, img + r * RS, H2 * F, F, Fp, tid);
+    if (a.debug != 2) stage_rows(in + (long long)gy_lo * H2 * F, img, rows, H2, F, Fp, RS, tid);
 
     // ---- this wave's 4x4 tiles, their tap rectangles and the wave's union rectangle
     const int CT = (Ho + 3) >> 2;
@@ -440,7 +471,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
     auto load_group = [&](int ky, int kx, int cb, float (&dst)[4][NT]) {
         // w2t is [k*k][F4][N16], zero padded (+16 rows of slack): no bounds select,
         // so the loads stay in flight until the MFMAs of the group consume them
-        const float* src = W + ((long long)(ky * k + kx) * F4 + cb * 16 + krow) * N16 + kcol;
+        const float* src = W + ((long long)(a.debug == 4 ? (cb & 1) * 16 : (ky * k + kx) * F4 + cb * 16) + krow) * N16 + kcol;
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -689,8 +720,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_scatter_kernel(StepArgs a, con
         boff[q] = v ? ((gy_lo + yy - y0) * H1 + xx) * 16 : 0;
     }
     __syncthreads();
-    for (int r = 0; r < rows && a.debug != 2; ++r)
-        stage_row(in + (long long)(gy_lo + r) * H2 * F, img + r * RS, H2 * F, F, Fp, tid);
+    if (a.debug != 2) stage_rows(in + (long long)gy_lo * H2 * F, img, rows, H2, F, Fp, RS, tid);
     __syncthreads();
 
     // work split: wave w takes channel group w % NT and the (w / NT)-th of the
