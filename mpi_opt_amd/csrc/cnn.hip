@@ -92,6 +92,7 @@ struct StepArgs {
     int debug;               // diagnostics only (env MPO_POP_DEBUG): 1 skip conv MMA loops, 2 skip conv staging,
                              // 4 conv fwd / dgrad weight fragments re-read from groups 0-1 (cache-resident; timing only)
     int xcd;                 // 1: XCD-grouped work-item order (xcd_item, env MPO_XCD_SWIZZLE=1); off by default
+    int conv_mt;             // forward conv m-tiles per wave at most (2: M <= 128 pixels per item; 4: <= 256)
 };
 
 // Work item of this workgroup.  Items are member-major; workgroups are dealt
@@ -210,14 +211,14 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ src, float*
 constexpr int kWSlack = 48;
 constexpr int kKoffSlack = 64;
 
-// Main loop of the forward conv for MT (1 or 2) m-tiles per wave: one 16-k group
+// Main loop of the forward conv for MT (<= MTX) m-tiles per wave: one 16-k group
 // per half-iteration; the weights of group g+1 (L2 -> VGPR) and the A gathers of
 // group g+1 (LDS) are issued before the MFMAs of group g, and the tap offsets
 // one group further ahead, so no MFMA waits on a load issued in its own group.
-template <int MT, int NT>
+template <int MT, int NT, int MTX>
 __device__ __forceinline__ void conv_fwd_loop(const float* __restrict__ img, const int* __restrict__ koff,
-                                              const float* __restrict__ W, int ngroups, const int (&pb)[2],
-                                              f32x4 (&acc)[2][NT], int krow, int kcol, int gmask) {
+                                              const float* __restrict__ W, int ngroups, const int (&pb)[MTX],
+                                              f32x4 (&acc)[MTX][NT], int krow, int kcol, int gmask) {
     constexpr int N16 = NT * 16;
     const float* wsrc = W + krow * N16 + kcol;
     const int* kp = koff + krow * 4;
@@ -270,7 +271,7 @@ __device__ __forceinline__ void conv_fwd_loop(const float* __restrict__ img, con
     }
 }
 
-template <int OP, int NT>
+template <int OP, int NT, int MTX>
 __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvItem* __restrict__ items) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const ConvItem it = items[xcd_item(a.xcd)];
@@ -334,10 +335,11 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
     }
 
     const int mtiles = (M + 15) >> 4;
-    const int mine = __builtin_amdgcn_readfirstlane(mtiles > wave + 4 ? 2 : (mtiles > wave ? 1 : 0));
-    int pb[2];
+    // m-tile t is wave t % 4's slot t / 4
+    const int mine = __builtin_amdgcn_readfirstlane(mtiles > wave ? min(MTX, (mtiles - wave + 3) >> 2) : 0);
+    int pb[MTX];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < MTX; ++i) {
         const int m = (wave + 4 * i) * 16 + (lane & 15);
         int base = 0;
         if (m < M) {
@@ -346,22 +348,30 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
         }
         pb[i] = base;
     }
-    f32x4 acc[2][NT];
+    f32x4 acc[MTX][NT];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MTX; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     __syncthreads();
     const int ngroups = a.debug == 1 ? 0 : K16 >> 4;
     const int gmask = a.debug == 4 ? 1 : -1;
-    if (mine == 2) conv_fwd_loop<2, NT>(img, koff, W, ngroups, pb, acc, krow, kcol, gmask);
-    else if (mine == 1) conv_fwd_loop<1, NT>(img, koff, W, ngroups, pb, acc, krow, kcol, gmask);
-    else return;
+    if constexpr (MTX == 4) {
+        if (mine == 4) conv_fwd_loop<4, NT, MTX>(img, koff, W, ngroups, pb, acc, krow, kcol, gmask);
+        else if (mine == 3) conv_fwd_loop<3, NT, MTX>(img, koff, W, ngroups, pb, acc, krow, kcol, gmask);
+        else if (mine == 2) conv_fwd_loop<2, NT, MTX>(img, koff, W, ngroups, pb, acc, krow, kcol, gmask);
+        else if (mine == 1) conv_fwd_loop<1, NT, MTX>(img, koff, W, ngroups, pb, acc, krow, kcol, gmask);
+        else return;
+    } else {
+        if (mine == 2) conv_fwd_loop<2, NT, MTX>(img, koff, W, ngroups, pb, acc, krow, kcol, gmask);
+        else if (mine == 1) conv_fwd_loop<1, NT, MTX>(img, koff, W, ngroups, pb, acc, krow, kcol, gmask);
+        else return;
+    }
 
     // ---- epilogue: C/D map col = lane & 15, row = (lane >> 4) * 4 + r
     const long long pix0 = (long long)it.y0 * Ho;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < MTX; ++i) {
         if (i >= mine) break;
         const int mt = wave + 4 * i;
 #pragma unroll
@@ -1611,6 +1621,7 @@ struct Plan {
     size_t lds_conv_max = 0, lds_wg_max = 0;
     bool wg1_wave = true;   // conv1 weight gradient on conv1_wgrad_kernel (env MPO_WG1_WAVE=0: the m-group kernel)
     int dg_scatter = 0;     // conv2 input gradient by scatter (conv_dgrad_scatter_kernel, env MPO_DG_SCATTER=1)
+    int conv_mt = 4;        // forward conv m-tiles per wave at most: items of up to 256 pixels (env MPO_CONV_MT=2: 128)
 };
 
 size_t conv_lds_bytes(int rows, int Wp, int Cin, int Ho, int K, int nt) {
@@ -1646,8 +1657,8 @@ size_t wg_lds_bytes(int k, int Hin, int Cin, int Ho, int F) {
 // Row-chunk height: as many output rows as fit M = R*Ho <= 128 pixels, shrunk
 // (down to half of that) to fit 3 or 2 workgroups per CU when possible.
 template <class Fn>
-int choose_rows(int Ho, Fn lds_of, int kb1 = 52, int kb2 = 78) {
-    const int rmax = std::max(1, std::min(Ho, 128 / Ho));
+int choose_rows(int Ho, Fn lds_of, int kb1 = 52, int kb2 = 78, int mcap = 128) {
+    const int rmax = std::max(1, std::min(Ho, mcap / Ho));
     const int rmin = std::max(1, rmax / 2);
     for (size_t budget : {(size_t)kb1 << 10, (size_t)kb2 << 10})
         for (int R = rmax; R >= rmin; --R)
@@ -1744,14 +1755,19 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
     P.act_floats = ao;
 
     // ---- work lists (LDS budgets per workgroup in KiB: A/B knobs, defaults tuned on MI355X)
-    const int kc1 = env_int("MPO_CONV_KB1", 52), kc2 = env_int("MPO_CONV_KB2", 78);
+    // r03: forward items of up to 256 pixels (4 m-tiles per wave) in <= 40 KiB (4 workgroups per CU) where
+    // rows in [rmax/2, rmax] fit, else <= 100 KiB: conv2 fwd 9.66 -> 8.53 ms per 320-member batch
+    // (profiles/r03/train_sweep_mt4_budget_am.log; 128-pixel items at 52/78 KiB were r01-r02's plan)
+    const int kc1 = env_int("MPO_CONV_KB1", 40), kc2 = env_int("MPO_CONV_KB2", 100);
     const int kdg = env_int("MPO_DG_KB", 78);
     std::vector<size_t> L1(n), L2(n), LD(n), LW1(n), LW2(n);   // per-member LDS bytes per op
     for (int i = 0; i < n; ++i) {
         const Member& m = P.mem[i];
         const int k = m.k, F = m.F, nt = m.nt;
-        const int R1 = choose_rows(m.H1, [&](int R) { return conv_lds_bytes(R + k - 1, kImg, 1, m.H1, k * k, nt); }, kc1, kc2);
-        const int R2 = choose_rows(m.H2, [&](int R) { return conv_lds_bytes(R + k - 1, m.H1, F, m.H2, k * k * F, nt); }, kc1, kc2);
+        if (i == 0) P.conv_mt = env_int("MPO_CONV_MT", 4) == 2 ? 2 : 4;
+        const int mcap = P.conv_mt * 64;   // 4 waves x conv_mt m-tiles of 16 pixels
+        const int R1 = choose_rows(m.H1, [&](int R) { return conv_lds_bytes(R + k - 1, kImg, 1, m.H1, k * k, nt); }, kc1, kc2, mcap);
+        const int R2 = choose_rows(m.H2, [&](int R) { return conv_lds_bytes(R + k - 1, m.H1, F, m.H2, k * k * F, nt); }, kc1, kc2, mcap);
         // dgrad: 4x4-pixel tiles in bands of 4 rows, <= 16 tiles (4 per wave) per chunk:
         // R = 4 * floor(16 / CT); 4-row bands fewer if the LDS budget asks for it
         const size_t dgb = (size_t)kdg << 10;
@@ -1865,7 +1881,7 @@ const T* dev_table(const Plan& P, size_t off) {
 template <int OP, int NT>
 hipError_t launch_conv_nt(const StepArgs& a, const ConvItem* items, int count, size_t lds, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    auto kern = conv_img_kernel<OP, NT>;
+    auto kern = a.conv_mt == 4 ? conv_img_kernel<OP, NT, 4> : conv_img_kernel<OP, NT, 2>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(count), dim3(256), lds, s, a, items);
     return hipGetLastError();
@@ -1995,6 +2011,7 @@ StepArgs make_args(const Plan& P, const float* x, const int* labels, const int* 
     a.correct = nullptr;
     a.debug = P.debug;
     a.xcd = P.xcd;
+    a.conv_mt = P.conv_mt;
     a.zero_off = P.zero_off;
     return a;
 }
