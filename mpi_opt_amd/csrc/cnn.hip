@@ -1622,6 +1622,7 @@ struct Plan {
     bool wg1_wave = true;   // conv1 weight gradient on conv1_wgrad_kernel (env MPO_WG1_WAVE=0: the m-group kernel)
     int dg_scatter = 0;     // conv2 input gradient by scatter (conv_dgrad_scatter_kernel, env MPO_DG_SCATTER=1)
     int conv_mt = 4;        // forward conv m-tiles per wave at most: items of up to 256 pixels (env MPO_CONV_MT=2: 128)
+    int dg_tiles = 12;      // 4x4 tiles per conv2 input-gradient work item at most (env MPO_DG_TILES)
 };
 
 size_t conv_lds_bytes(int rows, int Wp, int Cin, int Ho, int K, int nt) {
@@ -1771,7 +1772,10 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         // dgrad: 4x4-pixel tiles in bands of 4 rows, <= 16 tiles (4 per wave) per chunk:
         // R = 4 * floor(16 / CT); 4-row bands fewer if the LDS budget asks for it
         const size_t dgb = (size_t)kdg << 10;
-        int Rd = 4 * std::max(1, 16 / ((m.H1 + 3) / 4));
+        // r03: at most 12 tiles (3 per wave): conv2 dgrad 15.40 -> 15.15 ms per 320-member batch
+        // (profiles/r03/train_sweep_dgtiles_ap.log; 16 was r01-r02's, 8 measured 16.96)
+        if (i == 0) P.dg_tiles = std::max(1, std::min(16, env_int("MPO_DG_TILES", 12)));
+        int Rd = 4 * std::max(1, P.dg_tiles / ((m.H1 + 3) / 4));
         while (Rd > 4 && dgrad_lds_bytes(Rd, k, F, m.H2) > dgb) Rd -= 4;
         if (i == 0) P.dg_scatter = env_int("MPO_DG_SCATTER", 0);
         const bool sc = dg_uses_scatter(P.dg_scatter, nt);
