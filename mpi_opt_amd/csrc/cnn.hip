@@ -144,8 +144,8 @@ __host__ __device__ constexpr inline int fwd_rs(int Wp, int Cin, int Ho) {
 // ============================================================================
 // Image-stationary implicit-GEMM convolution (forward and input-gradient).
 //   out[b][y][x][n] = sum_{ky,kx,c} in_pad[b][y+ky][x+kx][c] * W[(ky*k+kx)*Cin+c][n]
-// One workgroup = (member, sample b, output rows [y0, y0+R)); M = R*Ho <= 128
-// output pixels = 8 m-tiles of 16 spread over 4 waves; N = F in NT tiles of 16.
+// One workgroup = (member, sample b, output rows [y0, y0+R)); M = R*Ho <= 64*MTX
+// output pixels = 4*MTX m-tiles of 16 spread over 4 waves; N = F in NT tiles of 16.
 // ============================================================================
 
 __host__ __device__ constexpr inline int align4(int x) { return (x + 3) & ~3; }
@@ -1655,8 +1655,8 @@ size_t wg_lds_bytes(int k, int Hin, int Cin, int Ho, int F) {
     return (size_t)(ring + 3 * dS + kWgWaves * 64 + 4) * sizeof(float);
 }
 
-// Row-chunk height: as many output rows as fit M = R*Ho <= 128 pixels, shrunk
-// (down to half of that) to fit 3 or 2 workgroups per CU when possible.
+// Row-chunk height: as many output rows as fit M = R*Ho <= mcap pixels, shrunk
+// (down to half of that) to fit the kb1 budget, else kb2, when possible (r03 plan: 256 pixels, 40 / 100 KiB).
 template <class Fn>
 int choose_rows(int Ho, Fn lds_of, int kb1 = 52, int kb2 = 78, int mcap = 128) {
     const int rmax = std::max(1, std::min(Ho, mcap / Ho));
