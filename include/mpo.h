@@ -201,11 +201,20 @@ typedef struct MpoCnnSpec {
     int32_t kernel_size;  /* k      Integer(2, 10)   */
     int32_t pool_size;    /* p      Integer(2, 10)   */
     int32_t dense;        /* dense  Integer(50, 200) */
-    float lr;             /* Adam learning rate (reference: 1e-3)            */
+    float lr;             /* learning rate (reference: Adam, 1e-3)           */
     float dropout;        /* dropout rate (reference: 0.25, mpiLAPI.py:151)   */
     uint32_t seed;        /* dropout stream seed                             */
-    int32_t reserved;
+    int32_t options;      /* MPO_LOSS_* | MPO_OPT_* (0: the reference's binary_crossentropy + Adam) */
 } MpoCnnSpec;
+
+/* MpoCnnSpec.options: option3's --loss (hyperparameter_search_option3.py:61) and
+ * master --optimizer (:60), both handed to mpi_learn's Algo (:270-275). */
+#define MPO_LOSS_BCE 0x0      /* Keras binary_crossentropy on the softmax (mean over the 10 outputs) */
+#define MPO_LOSS_CCE 0x1      /* Keras categorical_crossentropy (renormalised, clipped 1e-7)        */
+#define MPO_LOSS_MASK 0xff
+#define MPO_OPT_ADAM 0x000    /* Keras Adam (beta 0.9 / 0.999, eps 1e-8)                            */
+#define MPO_OPT_SGD 0x100     /* Keras SGD, no momentum: p -= lr g                                  */
+#define MPO_OPT_MASK 0xff00
 
 typedef struct MpoPopSizes {
     int64_t n_params;     /* floats in the parameter arena (also grads, adam m, adam v) */

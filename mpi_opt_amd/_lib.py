@@ -18,6 +18,9 @@ MPO_ACQ_PI = 2
 MPO_ACQ_LCB = 4
 MPO_TOPK_MAX = 8
 ACQ_FLAGS = {"EI": MPO_ACQ_EI, "PI": MPO_ACQ_PI, "LCB": MPO_ACQ_LCB}
+# MpoCnnSpec.options: option3's --loss / --optimizer (include/mpo.h MPO_LOSS_* | MPO_OPT_*)
+LOSS_CODES = {"binary_crossentropy": 0x0, "categorical_crossentropy": 0x1}
+OPT_CODES = {"adam": 0x000, "sgd": 0x100}
 ACQ_ROW = {"EI": 0, "PI": 1, "LCB": 2}
 
 
@@ -38,7 +41,7 @@ class MpoGpModel(ctypes.Structure):
 class MpoCnnSpec(ctypes.Structure):
     _fields_ = [("nb_filters", ctypes.c_int32), ("kernel_size", ctypes.c_int32), ("pool_size", ctypes.c_int32),
                 ("dense", ctypes.c_int32), ("lr", ctypes.c_float), ("dropout", ctypes.c_float),
-                ("seed", ctypes.c_uint32), ("reserved", ctypes.c_int32)]
+                ("seed", ctypes.c_uint32), ("options", ctypes.c_int32)]
 
 
 class MpoPopSizes(ctypes.Structure):

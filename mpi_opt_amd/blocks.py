@@ -37,6 +37,7 @@ import os
 
 import numpy as np
 
+from .chains import LazyPoint, resolve, resolve_all
 from .tag_lookup import tag_lookup
 
 FOM_CEILING = -math.log(1e-7)   # clipped binary cross-entropy cannot exceed this
@@ -58,16 +59,23 @@ class TrialEvaluator:
     """Trains trials (parameter lists of ``model_provider``'s space) on one GPU."""
 
     def __init__(self, model_provider, x, y, n_fold=1, epochs=10, batch=100, lr=1e-3, device=None,
-                 history_dir=None, init_seed=0, holdout=None):
+                 history_dir=None, init_seed=0, holdout=None, progress=None, loss="binary_crossentropy",
+                 optimizer="adam", stopping=None):
         self.model_provider = model_provider
         self.x, self.y = x, y
         self.n_fold, self.epochs, self.batch, self.lr = n_fold, epochs, batch, lr
+        # option3 --loss / --optimizer (hyperparameter_search_option3.py:60-61, Algo :270-275) for the
+        # test_mnist populations; DenseNet trials train as their builder compiles them
+        # (categorical_crossentropy + Adam, base_model.py:71-72)
+        self.loss, self.optimizer = loss, optimizer
+        self.stopping = stopping    # stopping.StopRule: --early-stopping / --target-metric (process_block.py:83-90)
         self.device = device
         self.history_dir = history_dir
         self.init_seed = init_seed
         self.holdout = holdout      # training samples of the train_list files (None: 70 % of x)
         self.n_evaluated = 0
         self.train_s = 0.0          # wall seconds spent training populations (synchronised)
+        self.progress = progress    # callable(str): a line per trained epoch (long runs)
 
     def units(self, params_list):
         """(trial index, fold) pairs with their training FLOPs (LPT cost)."""
@@ -120,13 +128,23 @@ class TrialEvaluator:
         for (t, f, spec, _) in units:
             uid = self._uid(seed_base, t, f)
             s = TrialSpec(spec.nb_filters, spec.kernel_size, spec.pool_size, spec.dense, spec.lr, spec.dropout,
-                          seed=uid)
+                          seed=uid, loss=self.loss, optimizer=self.optimizer)
             specs.append(s)
             folds.append(f)
             init.append(glorot_uniform_init(s, uid))
         eng = PopulationEngine(specs, batch=self.batch, device=self.device, init=init)
         return self._histories(units, eng.fit_folds(self.x, self.y, folds, self.n_fold, self.epochs,
-                                                      holdout=self.holdout))
+                                                      holdout=self.holdout, progress=self._epoch_cb(len(units)),
+                                                      stopping=self.stopping))
+
+    def _epoch_cb(self, members):
+        if self.progress is None:
+            return None
+        import time
+
+        t0 = time.perf_counter()
+        return lambda ep, eps: self.progress(f"population of {members} members: epoch {ep}/{eps} "
+                                             f"({time.perf_counter() - t0:.1f} s)")
 
     def _train_densenet(self, units, seed_base):
         from .densenet import DenseNetPopulation, he_uniform_init
@@ -138,14 +156,16 @@ class TrialEvaluator:
         init = [he_uniform_init(layers, self._uid(seed_base, t, f)) for (t, f, _, _) in units]
         pop = DenseNetPopulation(arch, lrs, batch=self.batch, device=self.device, init=init)
         return self._histories(units, pop.fit_folds(self.x, self.y, folds, self.n_fold, self.epochs,
-                                                      holdout=self.holdout))
+                                                      holdout=self.holdout, progress=self._epoch_cb(len(units)),
+                                                      stopping=self.stopping))
 
     @staticmethod
     def _histories(units, hist):
         out = {}
         for i, (t, f, _, _) in enumerate(units):
-            out[(t, f)] = {"val_loss": [float(v) for v in hist["val_loss"][i]],
-                           "val_acc": [float(v) for v in hist["val_acc"][i]]}
+            e = int(hist["epochs_run"][i])         # a stopped member's history ends at its stopping epoch
+            out[(t, f)] = {"val_loss": [float(v) for v in hist["val_loss"][i][:e]],
+                           "val_acc": [float(v) for v in hist["val_acc"][i][:e]]}
             for key in ("dropped_train_samples", "dropped_val_samples"):
                 if key in hist:
                     out[(t, f)][key] = int(hist[key][i])
@@ -170,15 +190,24 @@ class TrialEvaluator:
         return self.foms(params_list, results)
 
     def _record(self, params, fold_hists):
-        """Per-trial history JSON in the schema option0/1 parse (process_block.py:93-94)."""
+        """History JSON per (trial, fold) in the schema option0/1 parse
+        (``history["0"]["val_loss"]``, option0:71-82): each fold's manager records
+        its own details with ``meta = {"parameters": ..., "fold": manager.fold_num}``
+        (process_block.py:93-94), so one file per fold, ``fold`` = its index."""
         if not self.history_dir:
             return
         os.makedirs(self.history_dir, exist_ok=True)
         h = hashlib.md5(json.dumps([float(p) if not isinstance(p, str) else p for p in params]).encode()).hexdigest()
-        doc = {"history": {str(i): fh for i, fh in enumerate(fold_hists)},
-               "meta": {"parameters": [float(p) for p in params], "fold": len(fold_hists)}}
-        with open(os.path.join(self.history_dir, f"{h}.json"), "w") as f:
-            json.dump(doc, f)
+        for fold, fh in enumerate(fold_hists):
+            doc = {"history": {"0": fh}, "meta": {"parameters": [float(p) for p in params], "fold": fold}}
+            with open(os.path.join(self.history_dir, f"{h}_fold{fold}.json"), "w") as f:
+                json.dump(doc, f)
+
+
+def _same_params(a, b):
+    if isinstance(a, LazyPoint) or isinstance(b, LazyPoint):
+        return a is b
+    return a == b
 
 
 class _Request:
@@ -227,12 +256,15 @@ class PopulationComm:
         if obj is None:
             self.exited.add(dest)
             return
-        self.received[dest] = list(obj)
+        # a point of a lazy ask batch (mpi_opt_amd.chains) stays unresolved until
+        # its population trains: the same object must reach every rank of the block
+        val = obj if isinstance(obj, LazyPoint) else list(obj)
+        self.received[dest] = val
         b = self._block_of(dest)
         first = (b - 1) * self.block_size + 1
         ranks = range(first, first + self.block_size)
-        if all(self.received.get(r) == list(obj) for r in ranks):
-            self.pending[b] = list(obj)
+        if all(_same_params(self.received.get(r), val) for r in ranks):
+            self.pending[b] = val
             self.busy.add(b)
 
     def irecv(self, source, tag):
@@ -242,7 +274,7 @@ class PopulationComm:
 
     def evaluate_pending(self):
         blocks = sorted(self.pending)
-        params = [self.pending.pop(b) for b in blocks]
+        params = resolve_all([self.pending.pop(b) for b in blocks])
         foms = self.evaluator.evaluate(params)
         self.batches.append(len(params))
         self.trained_params.extend(params)
@@ -251,7 +283,7 @@ class PopulationComm:
 
     def Barrier(self):
         if self.train_tail and self.exited and self.pending:
-            launched = {b: list(p) for b, p in self.pending.items()}
+            launched = {b: resolve(p) for b, p in self.pending.items()}
             self.evaluate_pending()
             self.tail = [(launched[b], self.results[b]) for b in sorted(launched)]
 
@@ -309,7 +341,7 @@ class DistributedEvaluator:
       (SURVEY §8e "EI"), used by :class:`ShardedScorer`.
     """
 
-    def __init__(self, local, group=None):
+    def __init__(self, local, group=None, chain_runner=None):
         import torch.distributed as dist
 
         self.local = local
@@ -318,6 +350,7 @@ class DistributedEvaluator:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.n_evaluated = 0
+        self.chain_runner = chain_runner    # this rank's chains.ThreadChainExecutor (set by DistributedChainExecutor)
 
     def _announce(self, msg):
         box = [msg]
@@ -347,6 +380,26 @@ class DistributedEvaluator:
         parts = self._gather(part)
         return {a: merge_topk([p[a] for p in parts if a in p], int(req["k"])) for a in req["acqs"]}
 
+    def _chains(self, jobs):
+        """Every rank runs its LPT share of the ask batches; all ranks get all batches."""
+        from . import optimizer as O
+
+        owner = lpt_assign([j.cost for j in jobs], self.world)
+        mine = [i for i, o in enumerate(owner) if o == self.rank]
+        if self.chain_runner is None:
+            raise RuntimeError("DistributedEvaluator: no chain runner on this rank")
+        if self.rank != 0:
+            O.reset_stats()
+        res = self.chain_runner.run_now([jobs[i] for i in mine]) if mine else []
+        stats = dict(O.STATS) if self.rank != 0 else None
+        merged = [None] * len(jobs)
+        for part, st in self._gather(({i: r for i, r in zip(mine, res)}, stats)):
+            for i, r in part.items():
+                merged[i] = r
+            if st is not None and self.rank == 0:
+                O.merge_stats(st)
+        return merged
+
     def _serve_one(self):
         msg = self._announce(None)
         if msg is None:
@@ -354,6 +407,8 @@ class DistributedEvaluator:
         kind, body = msg
         if kind == "train":
             self._train(body)
+        elif kind == "chains":
+            self._chains(body)
         elif kind == "score":
             self._score(body)
         else:
@@ -365,6 +420,11 @@ class DistributedEvaluator:
         params_list = [list(p) for p in params_list]
         self._announce(("train", params_list))
         return self.local.foms(params_list, self._train(params_list))
+
+    def chains(self, jobs):
+        """Rank 0: run ask batches (optimizer.ChainJob) over all ranks -> [(X, trace)]."""
+        self._announce(("chains", list(jobs)))
+        return self._chains(list(jobs))
 
     def score(self, req):
         """Rank 0: a sharded acquisition request -> {acq: (values, indices)} top-k."""

@@ -52,6 +52,7 @@ struct Member {
     int F, k, p, dense;
     int H1, H2, s, K1;
     float lr, rate, inv_keep;
+    int loss, opt;      // MPO_LOSS_*, MPO_OPT_* (MpoCnnSpec.options)
     unsigned seed;
     unsigned drop_thr;  // keep iff (hash >> 8) >= drop_thr
     int nt;             // ceil(F / 16)
@@ -1434,6 +1435,25 @@ __global__ __launch_bounds__(256) void softmax_bce_kernel(StepArgs a, const MIte
         float e[kClasses], s = 0.f;
 #pragma unroll
         for (int c = 0; c < kClasses; ++c) { e[c] = expf(z[c] - zm); s += e[c]; }
+        corr += (am == y);
+        if (mb.loss == MPO_LOSS_CCE) {
+            // Keras categorical_crossentropy: q = p / sum p, clipped target probability;
+            // d loss / d logits = live (q - onehot) / B (the DenseNet head's form)
+            float q[kClasses], S2 = 0.f;
+#pragma unroll
+            for (int c = 0; c < kClasses; ++c) { q[c] = e[c] / s; S2 += q[c]; }
+#pragma unroll
+            for (int c = 0; c < kClasses; ++c) q[c] /= S2;
+            const float qt = q[y];
+            lsum += -logf(fminf(fmaxf(qt, kBceEps), 1.f - kBceEps));
+            if (a.train) {
+                const float live = (qt >= kBceEps && qt <= 1.f - kBceEps) ? 1.f / (float)B : 0.f;
+                float* dz = a.act + mb.dz3 + (long long)b * kClasses;
+#pragma unroll
+                for (int c = 0; c < kClasses; ++c) dz[c] = live * (q[c] - (c == y ? 1.f : 0.f));
+            }
+            continue;
+        }
         float l = 0.f, gdot = 0.f, gp[kClasses], pr[kClasses];
 #pragma unroll
         for (int c = 0; c < kClasses; ++c) {
@@ -1447,7 +1467,6 @@ __global__ __launch_bounds__(256) void softmax_bce_kernel(StepArgs a, const MIte
             gdot += gp[c] * p;
         }
         lsum += l / (float)kClasses;
-        corr += (am == y);
         if (a.train) {
             float* dz = a.act + mb.dz3 + (long long)b * kClasses;
 #pragma unroll
@@ -1510,10 +1529,14 @@ __global__ __launch_bounds__(256) void adam_kernel(StepArgs a, const MItem* __re
                                                    float b2, float eps, int chunk) {
     const MItem it = items[blockIdx.x];
     const Member& mb = a.mem[it.member];
-    const double corr = sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t));
-    const float lr_t = (float)(mb.lr * corr);
     const long long begin = mb.w1 + (long long)it.aux * chunk;
     const long long end = min(mb.pend, begin + chunk);
+    if (mb.opt == MPO_OPT_SGD) {            // Keras SGD, no momentum
+        for (long long i = begin + threadIdx.x; i < end; i += blockDim.x) params[i] -= mb.lr * a.grads[i];
+        return;
+    }
+    const double corr = sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t));
+    const float lr_t = (float)(mb.lr * corr);
     for (long long i = begin + threadIdx.x; i < end; i += blockDim.x) {
         const float g = a.grads[i];
         const float m = b1 * mo[i] + (1.f - b1) * g;
@@ -1719,6 +1742,13 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         m.s = m.H2 / m.p;
         if (m.s < 1) { mpo::set_error("mpo_pop_create: member %d pool larger than feature map", i); return MPO_ENOTSUP; }
         m.K1 = m.s * m.s * m.F;
+        const int loss = s.options & MPO_LOSS_MASK, opt = s.options & MPO_OPT_MASK;
+        if ((s.options & ~(MPO_LOSS_MASK | MPO_OPT_MASK)) || (loss != MPO_LOSS_BCE && loss != MPO_LOSS_CCE) ||
+            (opt != MPO_OPT_ADAM && opt != MPO_OPT_SGD)) {
+            mpo::set_error("mpo_pop_create: member %d has unsupported options 0x%x", i, (unsigned)s.options);
+            return MPO_ENOTSUP;
+        }
+        m.loss = loss; m.opt = opt;
         m.lr = s.lr; m.rate = s.dropout; m.inv_keep = 1.f / (1.f - s.dropout); m.seed = s.seed;
         m.drop_thr = (unsigned)std::ceil((double)s.dropout * 16777216.0);
         m.nt = (m.F + 15) / 16;

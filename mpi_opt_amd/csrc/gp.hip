@@ -815,6 +815,9 @@ inline int pad_dims(int d) {
 
 constexpr size_t kMaxLds = 160 * 1024;
 constexpr int kMergeGroups = 256;  // stage-1 top-k merge groups
+// Scoring grid bound: the resident capacity is <= 8 workgroups of 4 waves per CU
+// (32 waves), 256 CUs on MI355X; workspace for top-k lists is sized from this.
+constexpr int kScoreGridCap = 8 * 256;
 
 size_t score_lds_bytes(int dp, int np16) {
     const int T = np16 / 16;
@@ -842,9 +845,7 @@ hipError_t launch_score(const ScoreArgs& a, int ntiles, size_t lds, hipStream_t 
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), 256, lds);
-    int grid = std::max(1, std::min(ntiles, std::max(1, per_cu) * std::max(1, cus)));
-    const char* g = getenv("MPO_GP_GRID");   // experiments: "tiles" = one tile per workgroup
-    if (g && g[0] == 't') grid = ntiles;
+    int grid = std::max(1, std::min(std::min(ntiles, kScoreGridCap), std::max(1, per_cu) * std::max(1, cus)));
     if (grid_out) *grid_out = grid;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, a);
     return hipGetLastError();
@@ -1356,8 +1357,9 @@ struct ScoreWs {
     double* mq;
 };
 
-// top-k lists: 4 per workgroup (one per wave), and a workgroup has at least one tile
-inline int64_t score_nparts(int64_t m) { return 4 * ((m + kBM - 1) / kBM); }
+// top-k lists: 4 per workgroup (one per wave); a workgroup has at least one tile
+// and the grid never exceeds kScoreGridCap (tiles are looped over)
+inline int64_t score_nparts(int64_t m) { return 4 * std::min<int64_t>((m + kBM - 1) / kBM, kScoreGridCap); }
 
 inline ScoreWs carve_score_ws(void* ws, int64_t m, int k, size_t* used) {
     const int64_t nparts = score_nparts(m);
@@ -1651,13 +1653,16 @@ int mpo_gp_acq_grad(const MpoGpModel* model, const double* x, int batch, const i
     MPO_CHECK_ARG(model && x && acq && f && g, "mpo_gp_acq_grad: null pointer");
     MPO_CHECK_ARG(batch > 0 && batch <= 65535, "mpo_gp_acq_grad: batch=%d outside [1, 65535]", batch);
     MPO_CHECK_ARG(model->n > 0 && model->d > 0 && model->d <= 32 && model->W, "mpo_gp_acq_grad: model not prepared");
-    // static LDS of the 16-wave form: red[1024] + ga / gu [32][32] doubles = 24 KiB
+    // dynamic LDS per point: 19 n doubles (16 waves) or 7 n (4 waves); the static
+    // part (reduction rows, gradient tiles) is read from each kernel's code object
+    static const size_t st16 = mpo::static_lds_bytes(reinterpret_cast<const void*>(acq_grad_kernel<16>));
+    static const size_t st4 = mpo::static_lds_bytes(reinterpret_cast<const void*>(acq_grad_kernel<4>));
     const size_t lds16 = (size_t)19 * model->n * sizeof(double), lds4 = (size_t)7 * model->n * sizeof(double);
-    const bool wide = lds16 + (24 << 10) <= kMaxLds;
+    const bool wide = lds16 + st16 <= kMaxLds;
     const size_t lds = wide ? lds16 : lds4;
-    if (lds4 > kMaxLds - 8192) { mpo::set_error("mpo_gp_acq_grad: n=%d too large", model->n); return MPO_ENOTSUP; }
+    if (!wide && lds4 + st4 > kMaxLds) { mpo::set_error("mpo_gp_acq_grad: n=%d too large", model->n); return MPO_ENOTSUP; }
     auto kern = wide ? acq_grad_kernel<16> : acq_grad_kernel<4>;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    MPO_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(kern, dim3(batch), dim3(wide ? 1024 : 256), lds, static_cast<hipStream_t>(stream),
                        model->n, model->d, model->dp, model->amp, model->y_mean, model->y_std, model->xs, model->ls,
                        model->alpha, model->W, x, acq, y_opt, xi, kappa, f, g);
@@ -1670,6 +1675,7 @@ int mpo_gp_acq_grad_host(const MpoGpModel* model, const double* x_host, int batc
                          double y_opt, double xi, double kappa, double* f_host, double* g_host, void* stream) {
     MPO_GUARD_BEGIN
     MPO_CHECK_ARG(x_host && acq_host && f_host && g_host, "mpo_gp_acq_grad_host: null pointer");
+    mpo::StreamDeviceScope on_device(static_cast<hipStream_t>(stream));
     auto dev_view = [](const void* h) -> void* {
         hipPointerAttribute_t at{};
         if (hipPointerGetAttributes(&at, h) != hipSuccess || at.type != hipMemoryTypeHost || !at.devicePointer) {

@@ -1838,6 +1838,7 @@ int mpo_gp_lml_grad_host(const double* X, const double* y_norm, int n, int d, co
                          double* out_host, void* dev_io, size_t io_bytes, void* ws, size_t ws_bytes, void* stream) {
     MPO_GUARD_BEGIN
     MPO_CHECK_ARG(theta_host && out_host && dev_io, "mpo_gp_lml_grad_host: null pointer");
+    mpo::StreamDeviceScope on_device(static_cast<hipStream_t>(stream));
     MPO_CHECK_ARG(d > 0 && batch > 0, "mpo_gp_lml_grad_host: bad shape d=%d batch=%d", d, batch);
     MPO_CHECK_ARG(io_bytes >= mpo_gp_lml_io_bytes(d, batch), "mpo_gp_lml_grad_host: io buffer too small (%zu < %zu)",
                   io_bytes, mpo_gp_lml_io_bytes(d, batch));

@@ -32,6 +32,40 @@ struct WsCarver {
     }
 };
 
+// Makes the device a stream belongs to current for the scope of an entry point
+// and restores the caller's afterwards: entry points that query or configure the
+// device (hipFuncSetAttribute, attributes, pinned-pointer lookups) then target the
+// stream's GPU whatever device the calling thread has current.
+struct StreamDeviceScope {
+    int prev = -1, dev = -1;
+    explicit StreamDeviceScope(hipStream_t s) {
+        if (s == nullptr || hipGetDevice(&prev) != hipSuccess || hipStreamGetDevice(s, &dev) != hipSuccess) {
+            (void)hipGetLastError();
+            prev = dev = -1;
+            return;
+        }
+        if (dev != prev && hipSetDevice(dev) != hipSuccess) {
+            (void)hipGetLastError();
+            prev = dev = -1;
+        }
+    }
+    ~StreamDeviceScope() {
+        if (prev >= 0 && dev != prev) (void)hipSetDevice(prev);
+    }
+    StreamDeviceScope(const StreamDeviceScope&) = delete;
+    StreamDeviceScope& operator=(const StreamDeviceScope&) = delete;
+};
+
+// Static (compile-time) LDS bytes of a kernel, from its code object.
+inline size_t static_lds_bytes(const void* kern) {
+    hipFuncAttributes at{};
+    if (hipFuncGetAttributes(&at, kern) != hipSuccess) {
+        (void)hipGetLastError();
+        return SIZE_MAX / 2;
+    }
+    return at.sharedSizeBytes;
+}
+
 }  // namespace mpo
 
 #define MPO_CHECK_ARG(cond, ...)              \

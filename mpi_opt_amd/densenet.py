@@ -25,7 +25,7 @@ import torch
 
 from . import _lib
 from ._lib import check, lib, ptr
-from .population import kfold_split
+from .population import kfold_split, train_folds  # noqa: F401 (kfold_split re-exported)
 
 KIND_NAMES = {0: "conv0", 1: "dense", 2: "trans", 3: "head"}
 
@@ -295,46 +295,13 @@ class DenseNetPopulation:
         return self._pen
 
     # -- full k-fold training -----------------------------------------------------
-    def fit_folds(self, x, labels, folds, n_fold, epochs, record_train_loss=False, holdout=None):
+    def fit_folds(self, x, labels, folds, n_fold, epochs, record_train_loss=False, holdout=None, progress=None,
+                  stopping=None):
         """Train every member for ``epochs`` on its fold (in order, no shuffle),
-        validating once per epoch; val_loss = mean CE + l2 penalty (Keras)."""
-        n_samples = x.shape[0]
-        B = self.batch
-        tr, va = [], []
-        for i in range(self.n):
-            t, v = kfold_split(n_samples, n_fold, int(folds[i]), holdout)
-            tr.append(t)
-            va.append(v)
-        n_tr = min(len(t) for t in tr)
-        n_va = min(len(v) for v in va)
-        steps_per_epoch = n_tr // B
-        val_batches = n_va // B
-        if steps_per_epoch == 0 or val_batches == 0:
-            raise ValueError(f"fold too small for batch {B}: {n_tr} train / {n_va} validation samples")
-        dropped_tr = [len(t) - steps_per_epoch * B for t in tr]     # reported, never hidden
-        dropped_va = [len(v) - val_batches * B for v in va]
-        order_tr = torch.from_numpy(np.stack([t[:n_tr] for t in tr])).to(self.device)
-        order_va = torch.from_numpy(np.stack([v[:n_va] for v in va])).to(self.device)
-        val_loss = torch.zeros(self.n, epochs, dtype=torch.float32, device=self.device)
-        val_acc = torch.zeros(self.n, epochs, dtype=torch.float32, device=self.device)
-        tl = []
-        for ep in range(epochs):
-            for st in range(steps_per_epoch):
-                loss = self.train_step(x, labels, order_tr, st * B)
-                if record_train_loss:
-                    tl.append(loss.clone())
-            self.eval_reset()
-            for vb in range(val_batches):
-                self.eval_step(x, labels, order_va, vb * B)
-            denom = float(val_batches * B)
-            val_loss[:, ep] = self.val_loss_sum / denom + self.penalty()
-            val_acc[:, ep] = self.val_correct.to(torch.float32) / denom
-        out = {"val_loss": val_loss.cpu().numpy(), "val_acc": val_acc.cpu().numpy(),
-               "steps_per_epoch": steps_per_epoch, "val_batches": val_batches,
-               "dropped_train_samples": dropped_tr, "dropped_val_samples": dropped_va}
-        if record_train_loss:
-            out["train_loss"] = torch.stack(tl, 1).cpu().numpy() if tl else np.zeros((self.n, 0))
-        return out
+        validating once per epoch; val_loss = mean CE + l2 penalty (Keras).  The
+        loop is population.train_folds."""
+        return train_folds(self, x, labels, folds, n_fold, epochs, record_train_loss, holdout, progress, stopping,
+                           val_offset=self.penalty)
 
 
 def synthetic_cifar(n=50000, img_dim=(32, 32, 3), classes=10, seed=0, device=None):

@@ -119,14 +119,109 @@ def polish_lockstep(model, starts, acqs, y_opt, xi, kappa, bounds, maxiter=20):
 
 
 #: process-wide accounts of the GP work (bench / search reports): refits, their
-#: observation counts and the seconds spent refitting vs proposing
+#: observation counts and the seconds spent refitting vs proposing.  Chains run
+#: on worker threads (:mod:`~mpi_opt_amd.chains`), so updates take ``STATS_LOCK``;
+#: the seconds are then summed over concurrent workers (device-thread seconds).
 STATS = {"refits": 0, "n_sum": 0, "n_max": 0, "refit_s": 0.0, "propose_s": 0.0, "prepare_s": 0.0, "score_s": 0.0,
          "polish_s": 0.0, "samples": []}
+STATS_LOCK = threading.Lock()
 
 
 def reset_stats():
-    STATS.update(refits=0, n_sum=0, n_max=0, refit_s=0.0, propose_s=0.0, prepare_s=0.0, score_s=0.0, polish_s=0.0,
-                 samples=[])
+    with STATS_LOCK:
+        STATS.update(refits=0, n_sum=0, n_max=0, refit_s=0.0, propose_s=0.0, prepare_s=0.0, score_s=0.0,
+                     polish_s=0.0, samples=[])
+
+
+def merge_stats(delta):
+    """Add another process's STATS (a chain worker rank's) into this one's."""
+    with STATS_LOCK:
+        for k, v in delta.items():
+            if k == "n_max":
+                STATS[k] = max(STATS[k], v)
+            elif k == "samples":
+                STATS[k].extend(v)
+            else:
+                STATS[k] += v
+
+
+def _record_refit(n, t_refit, t_prepare, t_score, t_polish, t_propose, t_total):
+    with STATS_LOCK:
+        STATS["refits"] += 1
+        STATS["n_sum"] += n
+        STATS["n_max"] = max(STATS["n_max"], n)
+        STATS["refit_s"] += t_refit
+        STATS["prepare_s"] += t_prepare
+        STATS["score_s"] += t_score
+        STATS["polish_s"] += t_polish
+        STATS["propose_s"] += t_propose
+        STATS["samples"].append((n, t_total))      # (n, seconds of refit + proposal)
+
+
+class ChainJob:
+    """Everything one ``ask(n_points, strategy)`` batch depends on: the optimizer's
+    state when ``ask`` was called (its told points, gp_hedge gains, initial-point
+    budget and configuration) and the seed the copy draws from the optimizer's
+    RandomState.  The batch is a pure function of this record -- the copy never
+    touches the asking optimizer again (skopt's ``ask``: ``opt = self.copy(
+    random_state=self.rng.randint(...))``, then lies told to ``opt`` only) -- so a
+    job can run later, on another thread, stream, process or GPU, and give the
+    same points.  Picklable (no device state)."""
+
+    __slots__ = ("config", "Xi", "yi", "gains", "initial_samples", "n_initial_points", "seed", "n_points",
+                 "strategy", "trace", "cost")
+
+    def __init__(self, opt, seed, n_points, strategy):
+        self.config = opt._config()
+        self.Xi = [list(x) for x in opt.Xi]
+        self.yi = list(opt.yi)
+        self.gains = np.copy(opt.gains_) if hasattr(opt, "gains_") else None
+        self.initial_samples = opt._initial_samples
+        self.n_initial_points = opt.n_initial_points_
+        # an int from ask(); copy(random_state=...) may pass anything check_random_state takes
+        self.seed = int(seed) if isinstance(seed, (int, np.integer)) else seed
+        self.n_points, self.strategy = int(n_points), strategy
+        self.trace = opt.trace is not None
+        # LPT weight: a refit costs ~n^2 at these sizes (the LML's n^3 work is spread
+        # over n/16 workgroups); one refit per lie once the initial points are spent
+        n0 = len(self.yi)
+        self.cost = float(sum((n0 + i + 1) ** 2 for i in range(self.n_points)))
+
+    def copy_optimizer(self, device=None, scorer=None):
+        """``Optimizer.copy(random_state=seed)`` of the asking optimizer, on ``device``."""
+        opt = Optimizer(random_state=self.seed, device=device, scorer=scorer, **self.config)
+        opt._initial_samples = self.initial_samples
+        if self.gains is not None:
+            opt.gains_ = np.copy(self.gains)
+        opt.trace = [] if self.trace else None
+        if self.Xi:
+            opt._tell([list(x) for x in self.Xi], list(self.yi))
+        return opt
+
+    def run(self, device=None, scorer=None):
+        """The batch: (list of points, the copy's refit trace or None)."""
+        opt = self.copy_optimizer(device, scorer)
+        return _lie_loop(opt, self.n_points, self.strategy), opt.trace
+
+
+def _lie_loop(opt, n_points, strategy):
+    """skopt's constant-liar loop on the copy ``opt``: ask, then tell the lie."""
+    X = []
+    for _ in range(n_points):
+        x = opt._ask()
+        X.append(x)
+        if strategy == "cl_min":
+            lie = np.min(opt.yi) if opt.yi else 0.0
+        elif strategy == "cl_mean":
+            lie = np.mean(opt.yi) if opt.yi else 0.0
+        else:
+            lie = np.max(opt.yi) if opt.yi else 0.0
+        opt._tell(x, lie)
+        # only the newest surrogate is used again (gains, the next proposal):
+        # release the older ones' device factorisations as the chain grows
+        for m in opt.models[:-1]:
+            m._dev = None
+    return X
 
 
 class OptimizeResult(dict):
@@ -146,7 +241,7 @@ class Optimizer:
     def __init__(self, dimensions, base_estimator="gp", n_random_starts=None, n_initial_points=10,
                  initial_point_generator="random", acq_func="gp_hedge", acq_optimizer="auto",
                  random_state=None, model_queue_size=None, acq_func_kwargs=None, acq_optimizer_kwargs=None,
-                 device=None, _gp_seed=None, scorer=None):
+                 device=None, _gp_seed=None, scorer=None, chain_executor=None):
         self.rng = check_random_state(random_state)
         self.space = Space(dimensions)
         if n_random_starts is not None:
@@ -186,22 +281,26 @@ class Optimizer:
         self.Xi, self.yi, self.models = [], [], []
         self.cache_ = {}
         self.trace = None       # a list here records each refit (theta, top-k, polish, pick) for parity tests
+        # optional: runs ask(n) batches asynchronously (mpi_opt_amd.chains); ask then
+        # returns a LazyBatch whose points resolve when first used
+        self.chain_executor = chain_executor
+
+    def __setstate__(self, d):
+        # checkpoints written before these attributes existed resume with their defaults
+        d.setdefault("trace", None)
+        d.setdefault("chain_executor", None)
+        self.__dict__.update(d)
+
+    def _config(self):
+        """The constructor arguments a copy() shares with this optimizer."""
+        return dict(dimensions=self.space.dimensions, base_estimator=self.base_estimator_,
+                    n_initial_points=self.n_initial_points_, initial_point_generator=self._initial_point_generator,
+                    acq_func=self.acq_func, acq_optimizer=self.acq_optimizer, acq_func_kwargs=self.acq_func_kwargs,
+                    acq_optimizer_kwargs=self.acq_optimizer_kwargs, _gp_seed=self._gp_seed)
 
     # ---- ask -------------------------------------------------------------------
     def copy(self, random_state=None):
-        opt = Optimizer(self.space.dimensions, base_estimator=self.base_estimator_,
-                        n_initial_points=self.n_initial_points_,
-                        initial_point_generator=self._initial_point_generator, acq_func=self.acq_func,
-                        acq_optimizer=self.acq_optimizer, acq_func_kwargs=self.acq_func_kwargs,
-                        acq_optimizer_kwargs=self.acq_optimizer_kwargs, random_state=random_state,
-                        device=self.device, _gp_seed=self._gp_seed, scorer=self.scorer)
-        opt._initial_samples = self._initial_samples
-        if hasattr(self, "gains_"):
-            opt.gains_ = np.copy(self.gains_)
-        opt.trace = [] if self.trace is not None else None
-        if self.Xi:
-            opt._tell(self.Xi, self.yi)
-        return opt
+        return ChainJob(self, random_state, 0, "cl_min").copy_optimizer(self.device, self.scorer)
 
     def ask(self, n_points=None, strategy="cl_min"):
         if n_points is None:
@@ -210,20 +309,13 @@ class Optimizer:
             raise ValueError(f"strategy {strategy!r}")
         if (n_points, strategy) in self.cache_:
             return self.cache_[(n_points, strategy)]
-        opt = self.copy(random_state=self.rng.randint(0, np.iinfo(np.int32).max))
-        X = []
-        for _ in range(n_points):
-            x = opt.ask()
-            X.append(x)
-            if strategy == "cl_min":
-                lie = np.min(opt.yi) if opt.yi else 0.0
-            elif strategy == "cl_mean":
-                lie = np.mean(opt.yi) if opt.yi else 0.0
-            else:
-                lie = np.max(opt.yi) if opt.yi else 0.0
-            opt._tell(x, lie)
-        if self.trace is not None:
-            self.batch_trace = opt.trace
+        job = ChainJob(self, self.rng.randint(0, np.iinfo(np.int32).max), n_points, strategy)
+        if self.chain_executor is not None:
+            X = self.chain_executor.submit(job)
+        else:
+            X, trace = job.run(self.device, self.scorer)
+            if trace is not None:
+                self.batch_trace = trace
         self.cache_ = {(n_points, strategy): X}
         return X
 
@@ -238,6 +330,12 @@ class Optimizer:
 
     # ---- tell ------------------------------------------------------------------
     def tell(self, x, y, fit=True):
+        from .chains import LazyPoint, resolve
+
+        if isinstance(x, LazyPoint):         # points popped from a lazy ask batch
+            x = resolve(x)
+        elif len(x) and isinstance(x[0], LazyPoint):
+            x = [resolve(v) for v in x]
         if len(x) and isinstance(x[0], (list, tuple, np.ndarray)):
             if not np.ndim(y) == 1 or len(y) != len(x):
                 raise ValueError("tell: X and y must have matching lengths")
@@ -263,14 +361,9 @@ class Optimizer:
         t0 = time.perf_counter()
         amp, ls, noise = fit_gp_hyperparameters(Xt, y, random_state=self._gp_seed, device=self.device)
         t1 = time.perf_counter()
-        STATS["refits"] += 1
-        STATS["n_sum"] += len(y)
-        STATS["n_max"] = max(STATS["n_max"], len(y))
-        STATS["refit_s"] += t1 - t0
         est = GPModel(Xt, y, amp, ls, noise, device=self.device)
         est.dev                                   # the device posterior (mpo_gp_prepare)
         t2 = time.perf_counter()
-        STATS["prepare_s"] += t2 - t1
         if hasattr(self, "next_xs_") and self.acq_func == "gp_hedge":
             self.gains_ -= est.predict_mean(np.vstack(self.next_xs_))
         if self.model_queue_size is None or self.model_queue_size > 0:
@@ -286,7 +379,7 @@ class Optimizer:
         t3 = time.perf_counter()
         top = self._score_topk(est, X, y_opt, xi, kappa, k)
         t4 = time.perf_counter()
-        STATS["score_s"] += t4 - t3
+        t_polish = 0.0
         rec = {"theta": (est.amp, est.length_scale.copy(), est.noise), "top": dict(top), "polished": {}} \
             if self.trace is not None else None
         self.next_xs_ = []
@@ -294,7 +387,7 @@ class Optimizer:
             runs = [(a, i) for a in self.cand_acq_funcs_ for i in top[a]]
             polished = polish_lockstep(est, [X[i] for _, i in runs], [a for a, _ in runs], y_opt, xi, kappa,
                                        self.space.transformed_bounds)
-            STATS["polish_s"] += time.perf_counter() - t4
+            t_polish = time.perf_counter() - t4
         for acq in self.cand_acq_funcs_:
             idx = top[acq]
             if self.acq_optimizer == "sampling":
@@ -321,8 +414,7 @@ class Optimizer:
             self.trace.append(rec)
         self._next_x = self.space.inverse_transform(next_x.reshape(1, -1))[0]
         t5 = time.perf_counter()
-        STATS["propose_s"] += t5 - t1
-        STATS["samples"].append((len(y), t5 - t0))      # (n, seconds of refit + proposal)
+        _record_refit(len(y), t1 - t0, t2 - t1, t4 - t3, t_polish, t5 - t1, t5 - t0)
 
     def _score_topk(self, est, X, y_opt, xi, kappa, k):
         """skopt's ``np.argsort(values)[:k]`` per acquisition (lowest index first on
@@ -351,16 +443,18 @@ class Optimizer:
             self.tell(x, func(x))
         return self._result()
 
-    def set_runtime(self, device=None, scorer=None):
+    def set_runtime(self, device=None, scorer=None, chain_executor=None):
         """Re-attach the per-run state a checkpoint does not carry (the device of
-        this run and, when distributed, the candidate scorer); the models'
-        device posteriors are rebuilt lazily on ``device``."""
+        this run, when distributed the candidate scorer, the ask-batch executor);
+        the models' device posteriors are rebuilt lazily on ``device``."""
         self.device = device
         self.scorer = scorer
+        self.chain_executor = chain_executor
         for m in self.models:
             m.device, m._dev = device, None
 
     def __getstate__(self):
         d = _copy.copy(self.__dict__)
         d["scorer"] = None          # a process-group handle is not checkpoint state
+        d["chain_executor"] = None  # nor are worker threads
         return d

@@ -43,6 +43,17 @@ class TrialSpec:
     lr: float = 1e-3
     dropout: float = 0.25
     seed: int = 0
+    loss: str = "binary_crossentropy"     # option3 --loss (:61)
+    optimizer: str = "adam"               # option3 --optimizer (:60), the master's update rule
+
+    def options(self):
+        """MpoCnnSpec.options bits; raises for a loss / optimizer the kernels do not implement."""
+        try:
+            return _lib.LOSS_CODES[self.loss] | _lib.OPT_CODES[self.optimizer]
+        except KeyError:
+            raise ValueError(f"unsupported loss / optimizer {self.loss!r} / {self.optimizer!r}: the population "
+                             f"kernels implement losses {sorted(_lib.LOSS_CODES)} and optimizers "
+                             f"{sorted(_lib.OPT_CODES)}") from None
 
     def geometry(self):
         H1 = IMG - self.kernel_size + 1
@@ -140,7 +151,7 @@ class PopulationEngine:
         arr = (MpoCnnSpec * self.n)()
         for i, s in enumerate(self.specs):
             arr[i] = MpoCnnSpec(int(s.nb_filters), int(s.kernel_size), int(s.pool_size), int(s.dense),
-                                float(s.lr), float(s.dropout), int(s.seed) & 0xFFFFFFFF, 0)
+                                float(s.lr), float(s.dropout), int(s.seed) & 0xFFFFFFFF, s.options())
         h = ctypes.c_void_p()
         check(L.mpo_pop_create(arr, self.n, self.batch, ctypes.byref(h)), "mpo_pop_create")
         self._h = h
@@ -261,52 +272,71 @@ class PopulationEngine:
                                           _lib.stream_handle(self.device)), "mpo_pop_eval_step")
 
     # -- full k-fold training -----------------------------------------------------
-    def fit_folds(self, x, labels, folds, n_fold, epochs, record_train_loss=False, holdout=None):
+    def fit_folds(self, x, labels, folds, n_fold, epochs, record_train_loss=False, holdout=None, progress=None,
+                  stopping=None):
         """Train every member for ``epochs`` on its fold's training indices (in
         order, no shuffle), validating once per epoch (validate_every =
-        count/batch, option3:260).  ``folds[i]`` is member i's fold index.
-        Returns {"val_loss": [n, epochs], "val_acc": [n, epochs], "train_loss": ...}."""
-        n_samples = x.shape[0]
-        B = self.batch
-        tr, va = [], []
-        for i in range(self.n):
-            t, v = kfold_split(n_samples, n_fold, int(folds[i]), holdout)
-            tr.append(t)
-            va.append(v)
-        # members step in lock-step on full batches: every member trains on the
-        # first steps_per_epoch*B indices of its fold and validates on the first
-        # val_batches*B; what that leaves out (uneven folds, a partial last batch
-        # that Keras would still run) is reported in the history, never hidden
-        n_tr = min(len(t) for t in tr)
-        n_va = min(len(v) for v in va)
-        steps_per_epoch = n_tr // B
-        val_batches = n_va // B
-        if steps_per_epoch == 0 or val_batches == 0:
-            raise ValueError(f"fold too small for batch {B}: {n_tr} train / {n_va} validation samples")
-        dropped_tr = [len(t) - steps_per_epoch * B for t in tr]
-        dropped_va = [len(v) - val_batches * B for v in va]
-        order_tr = torch.from_numpy(np.stack([t[:n_tr] for t in tr])).to(self.device)
-        order_va = torch.from_numpy(np.stack([v[:n_va] for v in va])).to(self.device)
-        val_loss = torch.zeros(self.n, epochs, dtype=torch.float32, device=self.device)
-        val_acc = torch.zeros(self.n, epochs, dtype=torch.float32, device=self.device)
-        tl = []
-        for ep in range(epochs):
-            for st in range(steps_per_epoch):
-                loss = self.train_step(x, labels, order_tr, st * B)
-                if record_train_loss:
-                    tl.append(loss.clone())
-            self.eval_reset()
-            for vb in range(val_batches):
-                self.eval_step(x, labels, order_va, vb * B)
-            denom = float(val_batches * B)
-            val_loss[:, ep] = self.val_loss_sum / denom
-            val_acc[:, ep] = self.val_correct.to(torch.float32) / denom
-        out = {"val_loss": val_loss.cpu().numpy(), "val_acc": val_acc.cpu().numpy(),
-               "steps_per_epoch": steps_per_epoch, "val_batches": val_batches,
-               "dropped_train_samples": dropped_tr, "dropped_val_samples": dropped_va}
-        if record_train_loss:
-            out["train_loss"] = torch.stack(tl, 1).cpu().numpy() if tl else np.zeros((self.n, 0))
-        return out
+        count/batch, option3:260).  ``folds[i]`` is member i's fold index;
+        ``progress(epoch, epochs)`` is called after each epoch's validation;
+        ``stopping`` (a :class:`~mpi_opt_amd.stopping.StopRule`) ends members early.
+        Returns {"val_loss": [n, epochs], "val_acc": [n, epochs], "epochs_run": [n], ...}."""
+        return train_folds(self, x, labels, folds, n_fold, epochs, record_train_loss, holdout, progress, stopping)
+
+
+def train_folds(eng, x, labels, folds, n_fold, epochs, record_train_loss=False, holdout=None, progress=None,
+                stopping=None, val_offset=None):
+    """The k-fold training loop shared by the MNIST and DenseNet populations
+    (``eng.train_step`` / ``eval_reset`` / ``eval_step`` / ``val_loss_sum`` /
+    ``val_correct``): members step in lock-step on full batches, every member on
+    the first steps_per_epoch*B indices of its fold, validating on the first
+    val_batches*B; what that leaves out (uneven folds, a partial last batch that
+    Keras would still run) is reported in the history, never hidden.
+    ``val_offset()`` is added to the validation loss (DenseNet's l2 penalty)."""
+    n_samples = x.shape[0]
+    B = eng.batch
+    tr, va = [], []
+    for i in range(eng.n):
+        t, v = kfold_split(n_samples, n_fold, int(folds[i]), holdout)
+        tr.append(t)
+        va.append(v)
+    n_tr = min(len(t) for t in tr)
+    n_va = min(len(v) for v in va)
+    steps_per_epoch = n_tr // B
+    val_batches = n_va // B
+    if steps_per_epoch == 0 or val_batches == 0:
+        raise ValueError(f"fold too small for batch {B}: {n_tr} train / {n_va} validation samples")
+    dropped_tr = [len(t) - steps_per_epoch * B for t in tr]
+    dropped_va = [len(v) - val_batches * B for v in va]
+    order_tr = torch.from_numpy(np.stack([t[:n_tr] for t in tr])).to(eng.device)
+    order_va = torch.from_numpy(np.stack([v[:n_va] for v in va])).to(eng.device)
+    val_loss = torch.zeros(eng.n, epochs, dtype=torch.float32, device=eng.device)
+    val_acc = torch.zeros(eng.n, epochs, dtype=torch.float32, device=eng.device)
+    state = stopping.start(eng.n) if stopping is not None else None
+    tl = []
+    for ep in range(epochs):
+        for st in range(steps_per_epoch):
+            loss = eng.train_step(x, labels, order_tr, st * B)
+            if record_train_loss:
+                tl.append(loss.clone())
+        eng.eval_reset()
+        for vb in range(val_batches):
+            eng.eval_step(x, labels, order_va, vb * B)
+        denom = float(val_batches * B)
+        val_loss[:, ep] = eng.val_loss_sum / denom + (val_offset() if val_offset is not None else 0.0)
+        val_acc[:, ep] = eng.val_correct.to(torch.float32) / denom
+        if progress is not None:
+            progress(ep + 1, epochs)
+        if state is not None:
+            state.update(ep, val_loss[:, ep].cpu().numpy(), val_acc[:, ep].cpu().numpy())
+            if state.all_stopped():
+                break
+    out = {"val_loss": val_loss.cpu().numpy(), "val_acc": val_acc.cpu().numpy(),
+           "steps_per_epoch": steps_per_epoch, "val_batches": val_batches,
+           "dropped_train_samples": dropped_tr, "dropped_val_samples": dropped_va,
+           "epochs_run": state.epochs(epochs) if state is not None else np.full(eng.n, epochs)}
+    if record_train_loss:
+        out["train_loss"] = torch.stack(tl, 1).cpu().numpy() if tl else np.zeros((eng.n, 0))
+    return out
 
 
 def kfold_gather(X, idx, out=None):

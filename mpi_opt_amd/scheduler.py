@@ -31,6 +31,7 @@ import random
 import time
 from dataclasses import dataclass, field
 
+from .chains import LazyBatch, resolve
 from .tag_lookup import tag_lookup
 
 PARAMS_TAG = tag_lookup("params")
@@ -115,7 +116,10 @@ class AskTellScheduler:
         st = self.state
         if not st.suggestions:
             t0 = time.perf_counter()
-            st.suggestions = list(self.optimizer.ask(batch))
+            X = self.optimizer.ask(batch)
+            # a lazy batch (optimizer with a chain executor) is popped as unresolved
+            # points; a list is copied (the optimizer's ask cache holds it)
+            st.suggestions = X.points() if isinstance(X, LazyBatch) else list(X)
             self.timings["ask_s"] += time.perf_counter() - t0
             self.timings["asks"] += 1
         return st.suggestions.pop()
@@ -156,10 +160,11 @@ class AskTellScheduler:
             return False
         del self.inflight[block]
         st = self.state
-        st.param_list.append(launch.params)
+        params = resolve(launch.params)       # trained, so its batch has resolved
+        st.param_list.append(params)
         st.fom_list.append(fom)
-        st.unsent.append((launch.params, fom))
-        self._log(f"block {block} reported {fom} for {launch.params}")
+        st.unsent.append((params, fom))
+        self._log(f"block {block} reported {fom} for {params}")
         return True
 
     def _free_block(self):

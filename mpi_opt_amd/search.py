@@ -10,10 +10,17 @@ Same flags and defaults as /root/reference/hyperparameter_search_option3.py:54-9
 leftover).  ``--world-size`` plays the role of ``mpirun -n`` (the number of
 ranks the reference would have): it fixes how many trials run concurrently
 (``num_blocks``).  Every trial trains as population members on the GPU(s)
-instead of on MPI blocks; flags that configure mpi_learn's Downpour/EASGD
-exchange (--sync-every, --easgd, --elastic-*, --n-master, --n-process,
---worker-optimizer) are accepted and recorded but have no effect: a trial is
-trained synchronously on one GPU (single-trial semantics).
+instead of on MPI blocks.
+
+Training flags: ``--loss`` (binary_crossentropy | categorical_crossentropy) and
+``--optimizer`` (adam | sgd) select the member's loss and update rule in the
+kernels; ``--early-stopping`` / ``--target-metric`` stop members per fold
+(mpi_opt_amd.stopping); another value is refused with exit status 2.  Flags
+that configure mpi_learn's Downpour/EASGD exchange (--sync-every, --easgd,
+--elastic-*, --n-master, --n-process, --worker-optimizer) are accepted and
+recorded but have no effect: a trial is trained synchronously on one GPU
+(single-trial semantics).  ``--preload-data`` / ``--cache-data``
+concern mpi_learn's file loader; the data here is resident in HBM.
 """
 from __future__ import annotations
 
@@ -27,14 +34,17 @@ def make_parser():
     p.add_argument("--verbose", action="store_true")
     p.add_argument("--batch", help="batch size", default=100, type=int)
     p.add_argument("--epochs", help="number of training epochs", default=10, type=int)
-    p.add_argument("--optimizer", help="optimizer for master to use", default="adam")
-    p.add_argument("--loss", help="loss function", default="binary_crossentropy")
+    p.add_argument("--optimizer", help="optimizer for master to use (adam | sgd)", default="adam")
+    p.add_argument("--loss", help="loss function (binary_crossentropy | categorical_crossentropy)",
+                   default="binary_crossentropy")
     p.add_argument("--sync-every", default=1, type=int, dest="sync_every",
                    help="how often to sync weights with master (no effect: synchronous single-GPU trials)")
     p.add_argument("--preload-data", default=0, type=int, dest="data_preload")
     p.add_argument("--cache-data", default="", dest="caching_dir")
-    p.add_argument("--early-stopping", default=None, dest="early_stopping")
-    p.add_argument("--target-metric", default=None, dest="target_metric")
+    p.add_argument("--early-stopping", default=None, dest="early_stopping",
+                   help="patience for early stopping: N (val_loss) or METRIC,~<,N / METRIC,~>,N")
+    p.add_argument("--target-metric", default=None, dest="target_metric",
+                   help="stop a fold once METRIC,OP,VALUE holds (e.g. val_acc,>,0.97)")
     p.add_argument("--easgd", action="store_true")
     p.add_argument("--worker-optimizer", dest="worker_optimizer", default="sgd")
     p.add_argument("--elastic-force", type=float, default=0.9)
@@ -60,6 +70,9 @@ def make_parser():
     p.add_argument("--checkpoint", default="coordinator.pkl")
     p.add_argument("--ei-candidates", type=int, default=10000,
                    help="acquisition candidates per ask (skopt n_points); split over the GPUs when distributed")
+    p.add_argument("--chain-workers", type=int, default=4,
+                   help="concurrent cl_min ask batches per GPU (worker threads, one HIP stream each); "
+                        "0 runs every ask inline, as the reference's Coordinator does")
     return p
 
 
@@ -67,12 +80,27 @@ def check_sanity(args):
     assert args.block_size > 1, "Block size must be at least 2 (master + worker)"
 
 
+def check_training_flags(args):
+    """--loss / --optimizer / --early-stopping / --target-metric configure the
+    trials' training (option3:60-61, 66-69 -> Algo and MPIKFoldManager); a value
+    the population kernels do not implement is refused, never ignored.
+    Returns the parsed stopping rule (or None)."""
+    from . import _lib
+    from .stopping import StopRule
+
+    if args.loss not in _lib.LOSS_CODES:
+        raise ValueError(f"--loss {args.loss!r}: the population kernels implement {sorted(_lib.LOSS_CODES)}")
+    if args.optimizer not in _lib.OPT_CODES:
+        raise ValueError(f"--optimizer {args.optimizer!r}: the population kernels implement {sorted(_lib.OPT_CODES)}")
+    return StopRule.from_args(args.early_stopping, args.target_metric)
+
+
 def block_layout(world_size, block_size):
     """option3:174-181: (num_blocks, left_over)."""
     return divmod(world_size - 1, block_size)
 
 
-def run_search(args, x=None, y=None, log=print):
+def run_search(args, x=None, y=None, log=print, progress=None):
     """Run the option3 search for parsed ``args``; returns a report dict (rank 0)
     or None (ranks > 0, which serve their shards until rank 0 is done).
 
@@ -84,11 +112,13 @@ def run_search(args, x=None, y=None, log=print):
     import torch
 
     from .blocks import DistributedEvaluator, PopulationComm, ShardedScorer, TrialEvaluator
+    from .chains import DistributedChainExecutor, ThreadChainExecutor
     from .models import BuilderFromFunction, mnist_space, test_mnist
     from .population import synthetic_mnist
     from .scheduler import AskTellScheduler
 
     num_blocks, left_over = block_layout(args.world_size, args.block_size)
+    stopping = check_training_flags(args)
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -118,15 +148,26 @@ def run_search(args, x=None, y=None, log=print):
     if x is None:
         x, y = synthetic_mnist(args.n_samples, seed=0, device=dev)
     evaluator = TrialEvaluator(provider, x, y, n_fold=args.n_fold, epochs=args.epochs, batch=args.batch,
-                               lr=args.lr, device=dev, history_dir=args.history_dir, holdout=holdout)
+                               lr=args.lr, device=dev, history_dir=args.history_dir, holdout=holdout,
+                               progress=progress if (dist is None or dist.get_rank() == 0) else None,
+                               loss=args.loss, optimizer=args.optimizer, stopping=stopping)
     local_eval = evaluator
+    chains = ThreadChainExecutor(dev, workers=args.chain_workers) if args.chain_workers > 0 else None
     if dist is not None:
         evaluator = DistributedEvaluator(evaluator)
+        if chains is not None:
+            chains = DistributedChainExecutor(evaluator, chains)
         if evaluator.rank != 0:
-            evaluator.serve()
+            try:
+                evaluator.serve()
+            finally:
+                if chains is not None:
+                    chains.close()
             return None
     comm = PopulationComm(num_blocks, args.block_size, evaluator)
     opt_kw = {"device": dev, "acq_optimizer_kwargs": {"n_points": args.ei_candidates}}
+    if chains is not None:
+        opt_kw["chain_executor"] = chains                 # ask batches run concurrently (mpi_opt_amd.chains)
     if dist is not None:
         opt_kw["scorer"] = ShardedScorer(evaluator)       # candidates split M/W over the GPUs
     sched = AskTellScheduler(comm, num_blocks, provider.parameters, checkpoint=args.checkpoint,
@@ -137,22 +178,32 @@ def run_search(args, x=None, y=None, log=print):
     if args.previous_state:
         sched.load(args.previous_state)
         # the pickle carries no device state: re-attach this run's device and scorer
-        sched.optimizer.set_runtime(device=dev, scorer=opt_kw.get("scorer"))
+        sched.optimizer.set_runtime(device=dev, scorer=opt_kw.get("scorer"), chain_executor=chains)
     t0 = time.perf_counter()
-    state = sched.run(num_iterations=args.num_iterations)
-    wall = time.perf_counter() - t0
-    if dist is not None:
-        evaluator.shutdown()
+    try:
+        state = sched.run(num_iterations=args.num_iterations)
+        wall = time.perf_counter() - t0
+    finally:
+        if dist is not None:
+            evaluator.shutdown()
+        if chains is not None:
+            chains.close()
     tm = sched.timings
+    chain_wait = chains.wait_s if chains is not None else 0.0
     report = {
         "wall_s": wall,
         "trials_trained": comm.trials_trained,
         "trials_told": len(state.fom_list),
         "populations": list(comm.batches),
         "trained_params": [list(p) for p in comm.trained_params],
+        "told_params": [list(p) for p in state.param_list], "told_foms": list(state.fom_list),
         "num_blocks": num_blocks,
-        "optimizer_s": tm["ask_s"] + tm["tell_s"],
+        # seconds the search loop spent on the optimizer: asks (inline batches, or just
+        # recording a lazy one), tells, and waiting for lazy batches before a population trains
+        "optimizer_s": tm["ask_s"] + tm["tell_s"] + chain_wait,
         "ask_s": tm["ask_s"], "tell_s": tm["tell_s"], "asks": tm["asks"], "tells": tm["tells"],
+        "chain_wait_s": chain_wait, "chain_workers": args.chain_workers,
+        "chain_busy_s": chains.busy_s if chains is not None else 0.0,
         "train_s": local_eval.train_s,
         # headline on TOLD trials (the ones the optimizer saw); the in-flight tail the
         # exit barrier trains (coordinator.py:98-101 never tells it) is reported apart
@@ -171,6 +222,11 @@ def run_search(args, x=None, y=None, log=print):
 def main(argv=None):
     args = make_parser().parse_args(argv)
     check_sanity(args)
+    try:
+        check_training_flags(args)
+    except ValueError as e:
+        print(f"error: {e}", file=sys.stderr)
+        return 2
     if args.example != "mnist":
         print(f"example {args.example!r}: its data ({'LCD jets' if args.example == 'topclass' else '3D GAN'}) "
               "and model are outside the MNIST population engine", file=sys.stderr)

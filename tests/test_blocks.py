@@ -102,10 +102,13 @@ def test_foms_and_history_schema(tmp_path):
            (1, 0): {"val_loss": [float("nan")], "val_acc": [0]}, (1, 1): {"val_loss": [0.2], "val_acc": [0]}}
     foms = ev.foms([[10, 2, 2, 50, 0.1], [20, 3, 3, 60, 0.2]], res)
     assert foms[0] == 0.2 and foms[1] == FOM_CEILING
-    files = list(tmp_path.iterdir())
-    assert len(files) == 2
-    doc = json.loads(files[0].read_text())
-    assert "val_loss" in doc["history"]["0"] and "parameters" in doc["meta"]
+    files = sorted(tmp_path.iterdir())
+    assert len(files) == 4                  # one per (trial, fold), process_block.py:93-94
+    docs = [json.loads(f.read_text()) for f in files]
+    assert sorted(d["meta"]["fold"] for d in docs) == [0, 0, 1, 1]
+    by = {(tuple(d["meta"]["parameters"]), d["meta"]["fold"]): d["history"]["0"] for d in docs}
+    assert by[((10.0, 2.0, 2.0, 50.0, 0.1), 1)]["val_loss"] == [0.4, 0.1]
+    assert all(list(d["history"]) == ["0"] for d in docs)
     assert math.isfinite(FOM_CEILING) and FOM_CEILING > 16
 
 

@@ -1,0 +1,198 @@
+"""Concurrent cl_min chains (mpi_opt_amd.chains): the search with lazy ask
+batches -- run on worker threads, or dealt over gloo ranks -- tells, asks and
+trains exactly what the sequential protocol does.
+
+The GP refit needs the GPU, so here ``Optimizer._fit_and_propose`` is replaced
+by a CPU surrogate that keeps what matters for the equivalence: it depends on
+every told point, updates the gp_hedge gains and consumes a data-dependent
+number of RandomState draws (skopt's ``rng.multinomial``).  The device chains
+are checked against the sequential ones in tests/test_search_gpu.py."""
+import os
+import pickle
+import socket
+import types
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from mpi_opt_amd import optimizer as O
+from mpi_opt_amd.blocks import DistributedEvaluator, PopulationComm
+from mpi_opt_amd.chains import DistributedChainExecutor, LazyBatch, LazyPoint, ThreadChainExecutor
+from mpi_opt_amd.models import mnist_space
+from mpi_opt_amd.scheduler import AskTellScheduler
+
+
+def fake_fit_and_propose(self):
+    Xt = self.space.transform(self.Xi)
+    y = np.asarray(self.yi, dtype=float)
+    w = np.linalg.lstsq(np.c_[Xt, np.ones(len(y))], y, rcond=None)[0]
+
+    def mean(Z):
+        return np.c_[Z, np.ones(len(Z))] @ w
+
+    if hasattr(self, "next_xs_"):
+        self.gains_ -= mean(np.vstack(self.next_xs_))
+    X = self.space.rvs_transformed(n_samples=64, random_state=self.rng)
+    best = Xt[int(np.argmin(y))]
+    self.next_xs_ = [X[int(np.argmin(mean(X) + k * ((X - best) ** 2).sum(1)))] for k in range(3)]
+    logits = self.gains_ - np.max(self.gains_)
+    probs = np.exp(logits)
+    probs /= probs.sum()
+    pick = int(np.argmax(self.rng.multinomial(1, probs)))
+    self._next_x = self.space.inverse_transform(self.next_xs_[pick].reshape(1, -1))[0]
+    self.models.append(types.SimpleNamespace(_dev=None, w=w))
+    O._record_refit(len(y), 0.0, 0.0, 0.0, 0.0, 0.0, 0.0)
+
+
+class InstantEval:
+    """FOM = a deterministic function of the trial's parameters."""
+
+    def evaluate(self, params):
+        return [float((p[0] * 0.013 + p[1] * 0.07 + p[3] * 0.001 + p[4]) % 1.0) for p in params]
+
+
+def _search(tmp, executor=None, world=9, block=2, iters=24):
+    nb = (world - 1) // block
+    comm = PopulationComm(nb, block, InstantEval())
+    kw = {"chain_executor": executor} if executor is not None else {}
+    O.reset_stats()
+    sched = AskTellScheduler(comm, nb, mnist_space(), checkpoint=os.path.join(tmp, "c.pkl"), optimizer_kwargs=kw)
+    st = sched.run(num_iterations=iters)
+    return {"told": [list(map(float, p)) for p in st.param_list], "foms": list(st.fom_list),
+            "trained": [list(map(float, p)) for p in comm.trained_params], "batches": list(comm.batches),
+            "tail": [(list(map(float, p)), f) for p, f in comm.tail], "refits": O.STATS["refits"],
+            "best": (list(map(float, st.best_params)), st.best_fom)}
+
+
+@pytest.fixture
+def fake_gp(monkeypatch):
+    monkeypatch.setattr(O.Optimizer, "_fit_and_propose", fake_fit_and_propose)
+
+
+def test_lazy_threaded_search_equals_sequential(fake_gp, tmp_path):
+    import random
+
+    random.seed(5)
+    want = _search(str(tmp_path))
+    ex = ThreadChainExecutor(device=None, workers=3)
+    try:
+        random.seed(5)
+        got = _search(str(tmp_path), ex)
+    finally:
+        ex.close()
+    assert want["batches"] == [4, 4, 4, 4, 4, 4]
+    assert want["refits"] > 100
+    assert got == want
+
+
+def test_lazy_batch_pops_without_touching_the_ask_cache(fake_gp):
+    opt = O.Optimizer(mnist_space(), random_state=3)
+    for x, y in zip(opt.ask(12), np.linspace(0, 1, 12)):
+        opt.tell(x, float(y))
+    seq = opt.ask(6)
+    opt2 = O.Optimizer(mnist_space(), random_state=3)
+    ex = ThreadChainExecutor(device=None, workers=2)
+    try:
+        opt2.chain_executor = ex
+        for x, y in zip(opt2.ask(12), np.linspace(0, 1, 12)):   # a lazy batch iterates resolved
+            opt2.tell(x, float(y))
+        lazy = opt2.ask(6)
+        assert isinstance(lazy, LazyBatch)
+        pts = lazy.points()
+        last = pts.pop()
+        assert isinstance(last, LazyPoint) and list(last) == list(seq[-1])
+        assert opt2.ask(6) is lazy                               # cached until the next tell
+        assert [list(p) for p in lazy] == [list(p) for p in seq]
+        opt2.tell(last, 0.5)                                      # tell resolves a lazy point
+        assert opt2.Xi[-1] == list(seq[-1])
+    finally:
+        ex.close()
+
+
+def test_checkpoint_without_new_attributes_resumes(fake_gp):
+    """an Optimizer pickled before ``trace`` existed must resume."""
+    opt = O.Optimizer(mnist_space(), random_state=1)
+    for x, y in zip(opt.ask(11), np.linspace(0, 1, 11)):
+        opt.tell(x, float(y))
+    d = dict(opt.__dict__)
+    d.pop("trace")
+    d.pop("chain_executor")
+    old = O.Optimizer.__new__(O.Optimizer)
+    old.__dict__.update(d)
+    blob = pickle.dumps(old)
+    back = pickle.loads(blob)
+    assert back.trace is None and back.chain_executor is None
+    back.ask(3)
+    back.copy(random_state=4)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class _Local:
+    """DistributedEvaluator's local trainer: no training, FOMs from InstantEval."""
+
+    device = None
+
+    def units(self, params_list):
+        return [(t, 0, None, 1.0) for t in range(len(params_list))]
+
+    def train_units(self, units, seed_base=0):
+        return {(t, 0): None for (t, _, _, _) in units}
+
+    def foms(self, params_list, results):
+        return InstantEval().evaluate(params_list)
+
+
+def _dist_worker(rank, world, port, tmp, q):
+    import random
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    O.Optimizer._fit_and_propose = fake_fit_and_propose
+    ev = DistributedEvaluator(_Local())
+    ex = DistributedChainExecutor(ev, ThreadChainExecutor(device=None, workers=2))
+    if rank == 0:
+        random.seed(5)
+        nb = 4
+        comm = PopulationComm(nb, 2, ev)
+        O.reset_stats()
+        sched = AskTellScheduler(comm, nb, mnist_space(), checkpoint=os.path.join(tmp, "d.pkl"),
+                                 optimizer_kwargs={"chain_executor": ex})
+        st = sched.run(num_iterations=24)
+        ev.shutdown()
+        q.put({"told": [list(map(float, p)) for p in st.param_list], "foms": list(st.fom_list),
+               "trained": [list(map(float, p)) for p in comm.trained_params], "batches": list(comm.batches),
+               "refits": O.STATS["refits"], "rounds": ex.rounds})
+    else:
+        ev.serve()
+    ex.close()
+    dist.destroy_process_group()
+
+
+def test_chains_dealt_over_gloo_ranks_equal_sequential(fake_gp, tmp_path):
+    import random
+
+    random.seed(5)
+    want = _search(str(tmp_path))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dist_worker, args=(r, 3, port, str(tmp_path), q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rounds = got.pop("rounds")
+    assert rounds == len(want["batches"])       # one dispatch of buffered batches per population
+    for k in ("told", "foms", "trained", "batches", "refits"):
+        assert got[k] == want[k], k

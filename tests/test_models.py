@@ -50,3 +50,44 @@ def test_base_models_interface():
 
 def test_reference_spaces():
     assert [d.name for d in M.mnist_space()] == ["nb_filters", "pool_size", "kernel_size", "dense", "dropout"]
+
+
+def test_test_mnist_matches_the_reference_builder():
+    """T2 pinned to the reference: tests/golden/reference_cli_mnist.json holds
+    what /root/reference/mpiLAPI.py:138-176 ``test_mnist`` builds through
+    option3's ``BuilderFromFunction`` (option3:22-31) for the space's corners and
+    seeded draws -- the Keras layer calls and the JSON a Keras 2.1 ``to_json``
+    writes (recorded in the build container under stand-ins,
+    tests/golden/make_reference_cli_mnist_fixture.py).  This build's builder
+    makes the same layer sequence with the same arguments, and both JSONs ingest
+    to the same device spec (including the reference's 'drop_out' quirk: the
+    space's 'dropout' never reaches the model)."""
+    import json
+    import os
+
+    from mpi_opt_amd.models import BuilderFromFunction, mnist_space, spec_from_json
+    from mpi_opt_amd.models import test_mnist as ours
+    from tests.conftest import GOLDEN
+
+    fx = json.load(open(os.path.join(GOLDEN, "reference_cli_mnist.json")))
+    assert [d.name for d in mnist_space()] == fx["test_mnist"][0]["names"]
+    key = {"Conv2D": ("filters", "kernel_size", "padding"), "MaxPooling2D": ("pool_size",), "Dropout": ("rate",),
+           "Dense": ("units",), "Activation": ("activation",), "Flatten": ()}
+    for m in fx["test_mnist"]:
+        if "extra" in m:
+            kw = dict(zip(m["names"], m["params"]), **m["extra"])
+            js = ours(**kw)
+        else:
+            js = BuilderFromFunction(ours, mnist_space()).builder(*m["params"]).json_str
+        mine = json.loads(js)["config"]
+        layers = mine["layers"] if isinstance(mine, dict) else mine
+        refl = json.loads(m["json"])["config"]
+        assert [l["class_name"] for l in layers] == [c["class"] for c in m["calls"]] == \
+            [l["class_name"] for l in refl]
+        for a, b in zip(layers, refl):
+            for k in key[a["class_name"]]:
+                assert a["config"][k] == b["config"][k], (a["class_name"], k)
+        assert layers[0]["config"]["batch_input_shape"] == refl[0]["config"]["batch_input_shape"]
+        sa, sb = spec_from_json(js), spec_from_json(m["json"])
+        assert (sa.nb_filters, sa.kernel_size, sa.pool_size, sa.dense, sa.dropout) == \
+            (sb.nb_filters, sb.kernel_size, sb.pool_size, sb.dense, sb.dropout)

@@ -1,17 +1,50 @@
-"""The CLI keeps option3's flags and defaults (hyperparameter_search_option3.py:54-96)."""
-from mpi_opt_amd.search import block_layout, check_sanity, main, make_parser
+"""The CLI keeps option3's flags and defaults (hyperparameter_search_option3.py:54-96),
+pinned by tests/golden/reference_cli_mnist.json: the reference's own
+``make_parser()`` run in the build container under recording stand-ins for its
+imports (tests/golden/make_reference_cli_mnist_fixture.py)."""
+import argparse
+import json
+import os
 
-REFERENCE_DEFAULTS = dict(verbose=False, batch=100, epochs=10, optimizer="adam", loss="binary_crossentropy",
-                          sync_every=1, data_preload=0, caching_dir="", early_stopping=None, target_metric=None,
-                          easgd=False, worker_optimizer="sgd", elastic_force=0.9, elastic_lr=1.0,
-                          elastic_momentum=0, block_size=2, n_fold=1, n_master=1, n_process=1, num_iterations=10,
-                          previous_state=None, target_objective=None, example="mnist")
+import pytest
+
+from mpi_opt_amd.search import block_layout, check_sanity, check_training_flags, main, make_parser
+from tests.conftest import GOLDEN
+
+FIXTURE = json.load(open(os.path.join(GOLDEN, "reference_cli_mnist.json")))
 
 
 def test_defaults_match_reference():
-    a = make_parser().parse_args([])
-    for k, v in REFERENCE_DEFAULTS.items():
-        assert getattr(a, k) == v, k
+    a = vars(make_parser().parse_args([]))
+    for k, v in FIXTURE["defaults"].items():
+        assert a[k] == v, k
+
+
+def test_every_reference_flag_is_kept():
+    """Option strings, dest, default, type and action of every flag the
+    reference's parser defines; this build's flags are additions."""
+    ours = {tuple(a.option_strings): a for a in make_parser()._actions if not isinstance(a, argparse._HelpAction)}
+    for ref in FIXTURE["parser"]:
+        a = ours.get(tuple(ref["option_strings"]))
+        assert a is not None, ref["option_strings"]
+        assert a.dest == ref["dest"] and a.default == ref["default"], ref["option_strings"]
+        assert getattr(a.type, "__name__", None) == ref["type"] and type(a).__name__ == ref["action"]
+        assert (list(a.choices) if a.choices else None) == ref["choices"], ref["option_strings"]
+
+
+def test_training_flags_are_honoured_or_refused():
+    """--loss / --optimizer / --early-stopping / --target-metric reach the trainer
+    (option3:60-61, 66-69) or stop the CLI with status 2 -- never silently ignored."""
+    p = make_parser()
+    assert check_training_flags(p.parse_args([])) is None
+    rule = check_training_flags(p.parse_args(["--loss", "categorical_crossentropy", "--optimizer", "sgd",
+                                              "--early-stopping", "3", "--target-metric", "val_acc,>,0.97"]))
+    assert rule.patience == 3 and rule.target == ("val_acc", ">", 0.97)
+    for bad in (["--loss", "mse"], ["--optimizer", "rmsprop"], ["--early-stopping", "soon"],
+                ["--target-metric", "val_acc>0.9"]):
+        with pytest.raises(ValueError):
+            check_training_flags(p.parse_args(bad))
+        assert main(bad) == 2
 
 
 def test_readme_invocation_parses():

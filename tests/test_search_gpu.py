@@ -18,9 +18,10 @@ def test_search_cli_end_to_end(tmp_path, monkeypatch):
     assert rc == 0
     assert (tmp_path / "coordinator.pkl").exists()
     files = list((tmp_path / "hist").iterdir())
-    assert len(files) >= 9
+    assert len(files) >= 2 * 9                      # one per (trial, fold)
     doc = json.loads(files[0].read_text())
-    assert len(doc["history"]) == 2 and len(doc["history"]["0"]["val_loss"]) == 1
+    assert list(doc["history"]) == ["0"] and len(doc["history"]["0"]["val_loss"]) == 1
+    assert doc["meta"]["fold"] in (0, 1)
 
 
 def test_evaluator_is_deterministic():
@@ -62,10 +63,12 @@ def test_configs0_search_shape(tmp_path, monkeypatch):
     assert rep["populations"] == [4, 4, 2]
     assert rep["trials_trained"] == 10 and rep["trials_told"] == 6
     assert rep["train_s"] > 0 and rep["optimizer_s"] >= 0
-    files = list((tmp_path / "hist").iterdir())
-    assert len(files) == 10
-    doc = json.loads(files[0].read_text())
-    assert len(doc["history"]) == 5 and len(doc["history"]["0"]["val_loss"]) == 2
+    files = sorted((tmp_path / "hist").iterdir())
+    assert len(files) == 10 * 5                     # one per (trial, fold): meta.fold = manager.fold_num
+    docs = [json.loads(f.read_text()) for f in files]
+    assert sorted(d["meta"]["fold"] for d in docs) == sorted(list(range(5)) * 10)
+    doc = docs[0]
+    assert list(doc["history"]) == ["0"] and len(doc["history"]["0"]["val_loss"]) == 2
     assert doc["history"]["0"]["dropped_train_samples"] == 0
 
 
@@ -90,5 +93,44 @@ def test_search_reads_hdf5_data_dir(tmp_path, monkeypatch):
     assert rep["trials_trained"] == 3
     doc = json.loads(next((tmp_path / "hist").iterdir()).read_text())
     h = doc["history"]["0"]
+    assert doc["meta"]["fold"] == 0
     # 77 train samples (a + b) -> 7 steps of 10, 50 validation samples (c) -> 5 batches
     assert h["dropped_train_samples"] == 7 and h["dropped_val_samples"] == 0
+
+
+def _search3(tmp_path, workers):
+    from mpi_opt_amd import optimizer as O
+    from mpi_opt_amd import search
+
+    random.seed(3)
+    args = search.make_parser().parse_args(
+        ["--world-size", "17", "--block-size", "2", "--n-fold", "5", "--num-iterations", "32", "--epochs", "1",
+         "--n-samples", "2500", "--chain-workers", str(workers),
+         "--checkpoint", str(tmp_path / f"c{workers}.pkl")])
+    rep = search.run_search(args)
+    rep["refit_ns"] = sorted(n for n, _ in O.STATS["samples"])
+    return rep
+
+
+def test_configs3_layout_concurrent_chains_equal_sequential(tmp_path):
+    """BASELINE configs[3]'s layout (-n 2k+1 --block-size 2 --n-fold 5, a fresh
+    cl_min ask(num_iterations) after every tell, coordinator.py:46-50, 73) at
+    reduced size: 8 blocks, 32 iterations, 1 epoch on 2 500 samples.  The ask
+    batches run on 4 concurrent chains (mpi_opt_amd.chains) and inline: the told
+    points, their FOMs, every trained trial and the populations are identical,
+    and the GP refits are exactly the protocol's (bench.protocol_refits replays
+    it with a refit-counting optimizer: count and observation numbers)."""
+    import bench
+
+    seq = _search3(tmp_path, 0)
+    par = _search3(tmp_path, 4)
+    want_refits, want_pops = bench.protocol_refits(17, 2, 32)
+    for rep in (seq, par):
+        assert rep["populations"] == want_pops == [8, 8, 8, 8]
+        assert rep["trials_told"] == 24 and rep["trials_trained"] == 32 and rep["tail_trials"] == 8
+        assert rep["gp"]["refits"] == len(want_refits)
+        assert rep["refit_ns"] == sorted(want_refits)
+    assert par["told_params"] == seq["told_params"] and par["told_foms"] == seq["told_foms"]
+    assert par["trained_params"] == seq["trained_params"]
+    assert par["best_fom"] == seq["best_fom"] and par["best_params"] == seq["best_params"]
+    assert par["chain_wait_s"] > 0 and seq["chain_wait_s"] == 0

@@ -213,3 +213,76 @@ def test_scatter_dgrad_matches_oracle_and_is_isolated(monkeypatch):
     test_one_step_gradients_match_oracle()
     test_population_isolation()
     test_multistep_losses_within_1e3(2)
+
+
+# (loss, optimizer) per member: option3's --loss / --optimizer (hyperparameter_search_option3.py:60-61)
+OPTION_MEMBERS = [
+    ((10, 2, 2, 50, 1e-3, 0.25, 0), "categorical_crossentropy", "adam"),
+    ((33, 5, 3, 77, 2e-3, 0.25, 2), "binary_crossentropy", "sgd"),
+    ((17, 3, 7, 120, 5e-2, 0.1, 3), "categorical_crossentropy", "sgd"),
+    ((50, 2, 2, 200, 1e-3, 0.25, 4), "binary_crossentropy", "adam"),
+]
+
+
+def test_loss_and_optimizer_options_match_oracle():
+    """Members with categorical_crossentropy and/or SGD (MpoCnnSpec.options)
+    train in one population beside the reference's BCE + Adam: first-step
+    gradients per tensor and 2 epochs of per-step train / per-epoch validation
+    losses against the oracle's TrialOracle(loss=..., optimizer=...), 1e-3."""
+    from mpi_opt_amd.population import PopulationEngine, TrialSpec, glorot_uniform_init
+
+    members = [m for m, _, _ in OPTION_MEMBERS]
+    specs = [TrialSpec(F, k, p, d, lr, dr, seed=2000 + i, loss=lo, optimizer=op)
+             for i, ((F, k, p, d, lr, dr, _), lo, op) in enumerate(OPTION_MEMBERS)]
+    init = [glorot_uniform_init(s, 40 + i) for i, s in enumerate(specs)]
+
+    def oracle(i):
+        s = specs[i]
+        return C.TrialOracle(s.nb_filters, s.kernel_size, s.pool_size, s.dense,
+                             {n: v.astype(np.float64) for n, v in init[i].items()}, lr=s.lr, dropout=s.dropout,
+                             seed=s.seed, loss=s.loss, optimizer=s.optimizer)
+
+    x, y = dataset(4)
+    tr, va = orders(members, x)
+    xd, yd = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    eng = PopulationEngine(specs, batch=BATCH, init=init)
+    loss = eng.train_step(xd, yd, torch.from_numpy(tr).cuda(), 0).cpu().numpy()
+    grads = eng.grads.cpu().numpy()
+    for i, s in enumerate(specs):
+        o = oracle(i)
+        ref_loss, _, _, cache = o.forward(x[tr[i][:BATCH]], y[tr[i][:BATCH]], step=0, train=True)
+        g, absg = o.backward(cache, abs_terms=True, decisions=device_decisions(eng, i, s))
+        assert abs(loss[i] - ref_loss) <= 1e-5 * abs(ref_loss), (i, loss[i], ref_loss)
+        for name, (off, shape) in eng._slices(i).items():
+            gd = grads[off:off + int(np.prod(shape))].reshape(shape)
+            bound = 1e-4 * np.abs(g[name]).max() + 2e-5 * absg[name]
+            assert np.all(np.abs(gd - g[name]) <= bound), (i, s.loss, name)
+    eng = PopulationEngine(specs, batch=BATCH, init=init)
+    hist = eng.fit_folds(xd, yd, [m[-1] for m in members], N_FOLD, 2, record_train_loss=True)
+    steps = hist["steps_per_epoch"]
+    for i in range(len(specs)):
+        o = oracle(i)
+        ref_tl, ref_vl, step = [], [], 0
+        for ep in range(2):
+            for st in range(steps):
+                rows = tr[i][st * BATCH:(st + 1) * BATCH]
+                ref_tl.append(o.train_step(x[rows], y[rows], step))
+                step += 1
+            ref_vl.append(o.eval_loss(x[va[i]], y[va[i]]))
+        assert (np.abs(hist["train_loss"][i] - ref_tl) / np.abs(ref_tl)).max() < 1e-3, (i, specs[i].loss)
+        assert (np.abs(hist["val_loss"][i] - ref_vl) / np.abs(ref_vl)).max() < 1e-3, (i, specs[i].loss)
+
+
+def test_unsupported_options_are_refused():
+    from mpi_opt_amd import _lib
+    from mpi_opt_amd.population import PopulationEngine, TrialSpec
+
+    with pytest.raises(ValueError):
+        PopulationEngine([TrialSpec(10, 2, 2, 50, loss="mse")], batch=BATCH)
+    import ctypes
+
+    arr = (_lib.MpoCnnSpec * 1)()
+    arr[0] = _lib.MpoCnnSpec(10, 2, 2, 50, 1e-3, 0.25, 1, 0x7)          # no such loss code
+    h = ctypes.c_void_p()
+    assert _lib.lib().mpo_pop_create(arr, 1, BATCH, ctypes.byref(h)) != 0
+    assert "options" in _lib.lib().mpo_last_error().decode()
