@@ -120,3 +120,61 @@ def test_two_rank_gloo_matches_single_process():
     ref = CpuEval(BuilderFromFunction(mnist_model_fn, mnist_space()), None, None, n_fold=3)
     want = [ref.evaluate(b) for b in BATCHES]
     assert got == want
+
+
+def _units_worker(rank, world, port, params, q):
+    """Each rank: the LPT shard of the 256 x 5 (trial, fold) units it owns and its FLOPs."""
+    from mpi_opt_amd.blocks import lpt_assign
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    local = CpuEval(BuilderFromFunction(mnist_model_fn, mnist_space()), None, None, n_fold=5)
+    seen = []
+    orig = local.train_units
+
+    def record(units, seed_base=0):
+        seen.extend((t, f, c) for (t, f, _, c) in units)
+        return orig(units, seed_base)
+
+    local.train_units = record
+    ev = DistributedEvaluator(local)
+    if rank == 0:
+        foms = ev.evaluate(params)
+        ev.shutdown()
+    else:
+        ev.serve()
+        foms = None
+    q.put((rank, foms, seen))
+    dist.destroy_process_group()
+
+
+def test_configs3_256_trials_x_5_folds_over_8_ranks():
+    """BASELINE configs[3] sharding, rehearsed on 8 gloo ranks (CPU): 256 trials
+    from option3's mnist space x 5 folds = 1 280 (trial, fold) units, LPT over
+    the ranks by training FLOPs.  Every unit trains exactly once, the per-rank
+    FLOPs are balanced within 10 % of the mean, and the FOMs equal one process
+    evaluating the whole batch (unit seeds depend only on the unit)."""
+    import numpy as np
+
+    from mpi_opt_amd.space import Space
+
+    space = Space(mnist_space())
+    params = [list(p) for p in space.rvs(n_samples=256, random_state=np.random.RandomState(13579))]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_units_worker, args=(r, 8, port, params, q)) for r in range(8)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(8)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    by_rank = {r: seen for r, _, seen in out}
+    foms = next(f for r, f, _ in out if r == 0)
+    units = sorted((t, f) for seen in by_rank.values() for (t, f, _) in seen)
+    assert units == [(t, f) for t in range(256) for f in range(5)]
+    loads = np.array([sum(c for (_, _, c) in by_rank[r]) for r in range(8)])
+    assert loads.max() / loads.mean() <= 1.10, loads / loads.mean()
+    ref = CpuEval(BuilderFromFunction(mnist_model_fn, mnist_space()), None, None, n_fold=5)
+    assert foms == ref.evaluate(params)
