@@ -33,6 +33,7 @@
 #include "mpo_internal.h"
 
 #include <algorithm>
+#include <cstring>
 #include <cmath>
 #include <cstdlib>
 #include <memory>
@@ -92,23 +93,8 @@ struct StepArgs {
     long long zero_off;      // 64 zero floats in the activation arena (DMA source past row ends)
     int debug;               // diagnostics only (env MPO_POP_DEBUG): 1 skip conv MMA loops, 2 skip conv staging,
                              // 4 conv fwd / dgrad weight fragments re-read from groups 0-1 (cache-resident; timing only)
-    int xcd;                 // 1: XCD-grouped work-item order (xcd_item, env MPO_XCD_SWIZZLE=1); off by default
     int conv_mt;             // forward conv m-tiles per wave at most (2: M <= 128 pixels per item; 4: <= 256)
 };
-
-// Work item of this workgroup.  Items are member-major; workgroups are dealt
-// round-robin over the 8 XCDs (blocks b and b + 8 share one: MI355X_MICROARCH.md,
-// "Workgroup dispatch"), so the identity order spreads every member's items --
-// and the L2 fetches of its weights and activations -- over all 8 XCD L2s.  The
-// bijective remap gives XCD group x a contiguous run of items instead (guide T1),
-// so a member's items share one L2.  Placement is a speed choice only: any
-// permutation computes the same results.
-__device__ __forceinline__ int xcd_item(int on) {
-    const int b = blockIdx.x;
-    if (!on) return b;
-    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, x = b & 7, slot = b >> 3;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + slot;
-}
 
 // ---- dropout counter hash (identical in oracle/cnn.py) ---------------------
 __device__ __forceinline__ unsigned lowbias32(unsigned x) {
@@ -275,7 +261,7 @@ __device__ __forceinline__ void conv_fwd_loop(const float* __restrict__ img, con
 template <int OP, int NT, int MTX>
 __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvItem* __restrict__ items) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const ConvItem it = items[xcd_item(a.xcd)];
+    const ConvItem it = items[blockIdx.x];
     const Member& mb = a.mem[it.member];
     const int k = mb.k, F = mb.F;
     int Hin, Cin, Ho;
@@ -408,7 +394,7 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
 template <int NT>
 __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvItem* __restrict__ items) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const ConvItem it = items[xcd_item(a.xcd)];
+    const ConvItem it = items[blockIdx.x];
     const Member& mb = a.mem[it.member];
     const int k = mb.k, F = mb.F, H2 = mb.H2, Ho = mb.H1;
     const int pad = k - 1;
@@ -576,222 +562,6 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
     }
 }
 
-// ============================================================================
-// Input gradient of conv2 by scatter (r03, MPO_DG_SCATTER):
-//   dz1[b][y+ky][x+kx][c] += sum_f dz2[b][y][x][f] * w2[ky][kx][c][f]
-// input-stationary: every (tap, dz2 pixel) pair contributing to the band is one
-// MFMA row exactly once, so the MFMAs are the algorithmic count (the halo-tap
-// gather above runs 1.16-1.64x of it by k).  One workgroup = (member, sample,
-// output rows [y0, y0+R)); the dz2 rows feeding the band are staged once in the
-// LDS (the gather's layout).  For a tap the feeding dz2 pixels are one contiguous
-// run of flattened (y, x) indices, cut into 16-pixel MFMA tiles (M = pixels, N =
-// 16 channels c, K = F4 channels f); the tile's 16 output pixels are distinct, so
-// its 4 values per lane go to the band with ds_add_f32 on distinct addresses.
-// Determinism: each wave accumulates into its OWN band [R][H1][16] (one channel
-// group, a fixed subset of the taps, taps and tiles in a fixed order), and the
-// bands of a channel group are summed in wave order in the epilogue (ReLU gate of
-// a1 applied there).  Wave w: channel group w % NT, a contiguous tap range.
-// Measured (profiles/r03/scatter_ab.txt, 320 members, one GPU): the band's
-// read-add-write (8 LDS reads + 8 writes per two tiles; ds_add_f32 was ~10x slower
-// still) and the per-workgroup setup outweigh the 1.16-1.64x MFMAs it saves:
-// 48.3 vs 42.0 ms per train batch for all members, 45.2 with only F > 32 on it.
-// Off by default (MPO_DG_SCATTER=1 / 2 select it); kept, tested, for the record.
-// ============================================================================
-// per-wave band stride: [R][H1][16] and 64 floats a lane may write past a tap's run
-__host__ __device__ inline int dgs_band_floats(int R, int H1) { return R * H1 * 16 + 64; }
-
-// The per-wave tap loop of conv_dgrad_scatter_kernel for KS k-steps: B (the tap's
-// weights) in registers, the tap's tiles two at a time (two independent MFMA chains,
-// the next pair's LDS offsets read one pair ahead), results added to the wave's
-// band.  Tile rows past the tap's run (qb) are computed from in-bounds LDS data and
-// discarded.
-template <int NT>
-struct DgsTaps {
-    const float* img;
-    const int* aoff;
-    const int* boff;
-    float* band;
-    const float* W;
-    int k, H1, H2, F4, y0, R, gy_lo, gy_hi, wc, krow, kcol, dump;
-
-    template <int KS>
-    __device__ __forceinline__ void load_b(int t, float (&bw)[KS]) const {
-        constexpr int N16 = NT * 16;
-        const int ky = t / k, kx = t - ky * k;
-        const int rt = (k - 1 - ky) * k + (k - 1 - kx);
-        // w2[ky][kx][c][f] = w2t[rot(t)][f][c] (zero-padded to F4 x N16)
-        const float* wsrc = W + ((long long)rt * F4 + krow) * N16 + wc * 16 + kcol;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) bw[ks] = wsrc[(long long)ks * 4 * N16];
-    }
-
-    // taps [t0, t1) of channel group wc into `band`
-    template <int KS>
-    __device__ __forceinline__ void run(int t0, int t1) {
-        if (t0 >= t1) return;
-        float bw[KS], bn[KS];
-        load_b<KS>(t0, bw);
-        for (int t = t0; t < t1; ++t) {
-            // the next tap's weights load (L2) while this tap's tiles run
-            if (t + 1 < t1) load_b<KS>(t + 1, bn);
-            const int ky = t / k, kx = t - ky * k;
-            const int ylo = max(gy_lo, y0 - ky), yhi = min(gy_hi, y0 + R - ky);
-            const int qa = (ylo - gy_lo) * H2, qb = (yhi - gy_lo) * H2;
-            const int tapoff = (ky * H1 + kx) * 16;
-            // tile row m is pixel q0 + perm(m), perm(m) = 4 (m & 3) + (m >> 2): output row
-            // krow * 4 + r is then pixel q0 + 4 r + krow, so the 4 lane groups of one
-            // read-add-write instruction hit consecutive pixels (alternate 16-bank
-            // halves of the [pix][16] band: 2-way instead of 4-way bank conflicts)
-            const int pm = 4 * (kcol & 3) + (kcol >> 2);
-            int ab0 = aoff[qa + pm] + krow, ab1 = aoff[qa + 16 + pm] + krow;
-            for (int q0 = qa; q0 < qb; q0 += 32) {
-                float a0[KS], a1[KS];
-#pragma unroll
-                for (int ks = 0; ks < KS; ++ks) {
-                    a0[ks] = img[ab0 + 4 * ks];
-                    a1[ks] = img[ab1 + 4 * ks];
-                }
-                // next pair's offsets (the tables carry 64 entries of slack)
-                ab0 = aoff[q0 + 32 + pm] + krow;
-                ab1 = aoff[q0 + 48 + pm] + krow;
-                const int p0 = q0 + krow, p1 = p0 + 16;   // output row krow*4 + r: pixel p + 4 r
-                int o0[4], o1[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    o0[r] = boff[p0 + 4 * r];
-                    o1[r] = boff[p1 + 4 * r];
-                }
-                f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int ks = 0; ks < KS; ++ks) {
-                    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[ks], bw[ks], c0, 0, 0, 0);
-                    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[ks], bw[ks], c1, 0, 0, 0);
-                }
-                // C/D: row = krow * 4 + r (pixel), col = kcol (channel).  The band is this
-                // wave's alone and an instruction's 64 addresses are distinct: a plain
-                // read-add-write (LDS ops of one wave complete in order; ds_add_f32
-                // measured ~10x slower here)
-                float* d0[4];
-                float* d1[4];
-                float v0[4], v1[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    d0[r] = band + (p0 + 4 * r < qb ? o0[r] + tapoff + kcol : dump + krow * 16 + kcol);
-                    d1[r] = band + (p1 + 4 * r < qb ? o1[r] + tapoff + kcol : dump + krow * 16 + kcol);
-                    v0[r] = *d0[r];
-                    v1[r] = *d1[r];
-                }
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    *d0[r] = v0[r] + c0[r];
-                    *d1[r] = v1[r] + c1[r];
-                }
-            }
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) bw[ks] = bn[ks];
-        }
-    }
-};
-
-template <int NT>
-__global__ __launch_bounds__(256) void conv_dgrad_scatter_kernel(StepArgs a, const ConvItem* __restrict__ items) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const ConvItem it = items[xcd_item(a.xcd)];
-    const Member& mb = a.mem[it.member];
-    const int k = mb.k, F = mb.F, H2 = mb.H2, H1 = mb.H1;
-    const int pad = k - 1;
-    const int F4 = (F + 3) & ~3;
-    const int Fp = dgrad_fp(F);
-    const int R = it.R, y0 = it.y0;
-    const int gy_lo = max(0, y0 - pad), gy_hi = min(H2, y0 + R);   // dz2 rows feeding the band
-    const int rows = gy_hi - gy_lo;
-    const int npix = rows * H2;
-    const float* in = a.act + mb.dz2 + (long long)it.b * H2 * H2 * F;
-    const float* W = a.act + mb.w2t;
-    float* out = a.act + mb.dz1 + (long long)it.b * H1 * H1 * F;
-    const float* relu_mask = a.act + mb.a1 + (long long)it.b * H1 * H1 * F;
-
-    const int RS = dgrad_rs(H2, F);
-    const int zoff = align4(rows * RS);
-    float* img = smem;                                               // [rows][RS], then 64 zero floats
-    int* aoff = reinterpret_cast<int*>(smem + zoff + 64);            // [npix + 64]: LDS offset of pixel q
-    int* boff = aoff + align4(npix + 64);                            // [npix + 64]: band offset (tap 0,0)
-    const int BF = dgs_band_floats(R, H1);
-    float* bands = smem + zoff + 64 + 2 * align4(npix + 64);          // [4][BF]
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int krow = lane >> 4, kcol = lane & 15;
-
-    for (int e = tid; e < zoff + 64; e += 256) img[e] = 0.f;
-    for (int e = tid; e < 4 * BF; e += 256) bands[e] = 0.f;
-    for (int q = tid; q < npix + 64; q += 256) {
-        const int yy = q / H2, xx = q - yy * H2;
-        const bool v = q < npix;
-        aoff[q] = v ? yy * RS + xx * Fp : zoff;
-        boff[q] = v ? ((gy_lo + yy - y0) * H1 + xx) * 16 : 0;
-    }
-    __syncthreads();
-    if (a.debug != 2) stage_rows(in + (long long)gy_lo * H2 * F, img, rows, H2, F, Fp, RS, tid);
-    __syncthreads();
-
-    // work split: wave w takes channel group w % NT and the (w / NT)-th of the
-    // contiguous tap ranges that group's waves share.  (An even split of the NT * k^2
-    // (group, tap) units -- two band slots for the waves straddling a group at NT = 3
-    // -- measured slower: the extra slots cost band rows per workgroup.)
-    const int nt2 = k * k;
-    const int wc = wave % NT, ph = wave / NT, nph = (4 - wc + NT - 1) / NT;
-    if (a.debug != 1) {
-        // K = F4 channels f in KS = F4 / 4 k-steps: one fully unrolled loop body per KS
-        // (a runtime bound inside the unrolled loop put a branch around every MFMA)
-        const int KS = F4 >> 2;
-        DgsTaps<NT> r{img, aoff, boff, nullptr, W, k, H1, H2, F4, y0, R, gy_lo, gy_hi, 0, krow, kcol, BF - 64};
-        {
-            const int t0 = ph * nt2 / nph, t1 = (ph + 1) * nt2 / nph;
-            r.wc = wc;
-            r.band = bands + wave * BF;
-            switch (KS) {
-                case 3: r.template run<3>(t0, t1); break;
-                case 4: r.template run<4>(t0, t1); break;
-                case 5: r.template run<5>(t0, t1); break;
-                case 6: r.template run<6>(t0, t1); break;
-                case 7: r.template run<7>(t0, t1); break;
-                case 8: r.template run<8>(t0, t1); break;
-                case 9: r.template run<9>(t0, t1); break;
-                case 10: r.template run<10>(t0, t1); break;
-                case 11: r.template run<11>(t0, t1); break;
-                case 12: r.template run<12>(t0, t1); break;
-                default: r.template run<13>(t0, t1); break;
-            }
-        }
-    }
-    __syncthreads();
-    // ---- epilogue: the band pixels, channels c < F: bands of c's group summed in wave order, ReLU gate
-    // one pixel per wave and loop step, channel = lane: no division, and the gate
-    // loads of a wave's 4 pixels issue together (restrict: out never aliases a1)
-    const int band_pix = R * H1;
-    if (lane < F) {
-        const int g = lane >> 4, c16 = lane & 15;
-        const float* __restrict__ gate = relu_mask + (long long)y0 * H1 * F + lane;
-        float* __restrict__ dst = out + (long long)y0 * H1 * F + lane;
-        for (int pix = wave; pix < band_pix; pix += 16) {
-            float mk[4], v[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int px = pix + 4 * u;
-                mk[u] = px < band_pix ? gate[(long long)px * F] : 0.f;
-                float acc = 0.f;
-                if (px < band_pix)
-                    for (int w = g; w < 4; w += NT) acc += bands[w * BF + px * 16 + c16];   // wave order
-                v[u] = acc;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int px = pix + 4 * u;
-                if (px < band_pix) dst[(long long)px * F] = mk[u] > 0.f ? v[u] : 0.f;
-            }
-        }
-    }
-}
 
 // ============================================================================
 // Weight gradient: dW[(ky,kx,c)][n] = sum_{b,y,x} in[b][y+ky][x+kx][c] * dout[b][y][x][n]
@@ -862,7 +632,7 @@ __device__ __forceinline__ void wgrad_row(const float* __restrict__ img, const f
 template <int OP, int NT, int MT>
 __global__ __launch_bounds__(kWgThreads) void conv_wgrad_kernel(StepArgs a, const WgItem* __restrict__ items) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const WgItem it = items[xcd_item(a.xcd)];
+    const WgItem it = items[blockIdx.x];
     const Member& mb = a.mem[it.member];
     const int k = mb.k, F = mb.F;
     int Hin, Cin, Ho;
@@ -1012,7 +782,7 @@ __host__ __device__ constexpr inline int w1_lds_floats(int nb, int mt, int nt) {
 template <int NT, int MT>
 __global__ __launch_bounds__(kW1Waves * 64) void conv1_wgrad_kernel(StepArgs a, const WgItem* __restrict__ items) {
     extern __shared__ __attribute__((aligned(16))) float sh[];   // images | slack | {0, 1}; then the reduction
-    const WgItem it = items[xcd_item(a.xcd)];
+    const WgItem it = items[blockIdx.x];
     const Member& mb = a.mem[it.member];
     const int k = mb.k, F = mb.F, Ho = mb.H1, Kw = k * k;
     const int tid = threadIdx.x, lane = tid & 63, krow = lane >> 4, kcol = lane & 15;
@@ -1616,13 +1386,28 @@ int env_int(const char* name, int dflt) {
     return (v && *v) ? atoi(v) : dflt;
 }
 
+// Planner overrides for tuning sweeps, one variable: MPO_POP_PLAN="key=value,..."
+// (keys: dg_tiles, dg_kb, conv_mt, conv_kb1, conv_kb2, wg_spg1, wg_spg2).  Every
+// value only changes how work is cut into items, never the arithmetic.
+int plan_knob(const char* key, int dflt) {
+    const char* v = getenv("MPO_POP_PLAN");
+    if (!v) return dflt;
+    const size_t n = strlen(key);
+    for (const char* p = v; *p;) {
+        if (!strncmp(p, key, n) && p[n] == '=') return atoi(p + n + 1);
+        const char* c = strchr(p, ',');
+        if (!c) break;
+        p = c + 1;
+    }
+    return dflt;
+}
+
 struct Plan {
     int n = 0, B = 0;
     PhaseTimer timer;
     bool timer_detail = false;
     long long zero_off = 0;
     int debug = 0;
-    int xcd = 0;
     std::vector<Member> mem;
     long long n_params = 0, act_floats = 0;
     std::vector<ConvItem> conv1, conv2, dgrad;
@@ -1642,10 +1427,8 @@ struct Plan {
     float *params = nullptr, *grads = nullptr, *m = nullptr, *v = nullptr, *act = nullptr;
     bool bound = false;
     size_t lds_conv_max = 0, lds_wg_max = 0;
-    bool wg1_wave = true;   // conv1 weight gradient on conv1_wgrad_kernel (env MPO_WG1_WAVE=0: the m-group kernel)
-    int dg_scatter = 0;     // conv2 input gradient by scatter (conv_dgrad_scatter_kernel, env MPO_DG_SCATTER=1)
-    int conv_mt = 4;        // forward conv m-tiles per wave at most: items of up to 256 pixels (env MPO_CONV_MT=2: 128)
-    int dg_tiles = 12;      // 4x4 tiles per conv2 input-gradient work item at most (env MPO_DG_TILES)
+    int conv_mt = 4;        // forward conv m-tiles per wave at most: items of up to 256 pixels (MPO_POP_PLAN conv_mt=2: 128)
+    int dg_tiles = 12;      // 4x4 tiles per conv2 input-gradient work item at most (MPO_POP_PLAN dg_tiles)
 };
 
 size_t conv_lds_bytes(int rows, int Wp, int Cin, int Ho, int K, int nt) {
@@ -1653,18 +1436,6 @@ size_t conv_lds_bytes(int rows, int Wp, int Cin, int Ho, int K, int nt) {
     const int Fp = fwd_fp(Cin);
     (void)Fp;
     return (size_t)(align4(rows * fwd_rs(Wp, Cin, Ho)) + ((K + 15) & ~15) + kKoffSlack) * sizeof(float);
-}
-
-// MPO_DG_SCATTER: 0 = the halo-tap gather for every member, 1 = the scatter for every
-// member, 2 = the scatter where it measured faster (F > 32: 3-4 channel groups; for
-// small F its per-tile read-add-write outweighs the gather's halo MFMAs)
-inline bool dg_uses_scatter(int mode, int nt) { return mode == 1 || (mode == 2 && nt >= 3); }
-
-size_t dgrad_scatter_lds_bytes(int R, int k, int F, int H1, int H2) {
-    const int rows = std::min(H2, R + k - 1);
-    const int npix = rows * H2;
-    return (size_t)(align4(rows * dgrad_rs(H2, F)) + 64 + 2 * align4(npix + 64) + 4 * dgs_band_floats(R, H1)) *
-           sizeof(float);
 }
 
 size_t dgrad_lds_bytes(int R, int k, int F, int H2) {
@@ -1760,7 +1531,7 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         m.pend = po;
         // wgrad sample groups (partial slabs reduced in a fixed order): ~10
         // samples per conv2 block, ~4 per conv1 block (its GEMM is tiny)
-        const int spg2 = std::max(1, env_int("MPO_WG_SPG2", 4)), spg1 = std::max(1, env_int("MPO_WG_SPG1", 4));
+        const int spg2 = std::max(1, plan_knob("wg_spg2", 4)), spg1 = std::max(1, plan_knob("wg_spg1", 4));
         m.g2 = std::max(1, std::min(B, (B + spg2 - 1) / spg2));
         m.g1 = std::max(1, std::min(B, (B + spg1 - 1) / spg1));
         m.a1 = aalloc((long long)B * m.H1 * m.H1 * F);
@@ -1789,13 +1560,13 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
     // r03: forward items of up to 256 pixels (4 m-tiles per wave) in <= 40 KiB (4 workgroups per CU) where
     // rows in [rmax/2, rmax] fit, else <= 100 KiB: conv2 fwd 9.66 -> 8.53 ms per 320-member batch
     // (profiles/r03/train_sweep_mt4_budget_am.log; 128-pixel items at 52/78 KiB were r01-r02's plan)
-    const int kc1 = env_int("MPO_CONV_KB1", 40), kc2 = env_int("MPO_CONV_KB2", 100);
-    const int kdg = env_int("MPO_DG_KB", 78);
+    const int kc1 = plan_knob("conv_kb1", 40), kc2 = plan_knob("conv_kb2", 100);
+    const int kdg = plan_knob("dg_kb", 78);
     std::vector<size_t> L1(n), L2(n), LD(n), LW1(n), LW2(n);   // per-member LDS bytes per op
     for (int i = 0; i < n; ++i) {
         const Member& m = P.mem[i];
         const int k = m.k, F = m.F, nt = m.nt;
-        if (i == 0) P.conv_mt = env_int("MPO_CONV_MT", 4) == 2 ? 2 : 4;
+        if (i == 0) P.conv_mt = plan_knob("conv_mt", 4) == 2 ? 2 : 4;
         const int mcap = P.conv_mt * 64;   // 4 waves x conv_mt m-tiles of 16 pixels
         const int R1 = choose_rows(m.H1, [&](int R) { return conv_lds_bytes(R + k - 1, kImg, 1, m.H1, k * k, nt); }, kc1, kc2, mcap);
         const int R2 = choose_rows(m.H2, [&](int R) { return conv_lds_bytes(R + k - 1, m.H1, F, m.H2, k * k * F, nt); }, kc1, kc2, mcap);
@@ -1804,20 +1575,12 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         const size_t dgb = (size_t)kdg << 10;
         // r03: at most 12 tiles (3 per wave): conv2 dgrad 15.40 -> 15.15 ms per 320-member batch
         // (profiles/r03/train_sweep_dgtiles_ap.log; 16 was r01-r02's, 8 measured 16.96)
-        if (i == 0) P.dg_tiles = std::max(1, std::min(16, env_int("MPO_DG_TILES", 12)));
+        if (i == 0) P.dg_tiles = std::max(1, std::min(16, plan_knob("dg_tiles", 12)));
         int Rd = 4 * std::max(1, P.dg_tiles / ((m.H1 + 3) / 4));
         while (Rd > 4 && dgrad_lds_bytes(Rd, k, F, m.H2) > dgb) Rd -= 4;
-        if (i == 0) P.dg_scatter = env_int("MPO_DG_SCATTER", 0);
-        const bool sc = dg_uses_scatter(P.dg_scatter, nt);
-        if (sc) {
-            // scatter: bands of Rd rows within the LDS budget (the dz2 rows + 4 private bands)
-            const size_t sgb = (size_t)env_int("MPO_DGS_KB", 64) << 10;
-            Rd = std::max(1, std::min(m.H1, env_int("MPO_DGS_ROWS", 8)));
-            while (Rd > 1 && dgrad_scatter_lds_bytes(Rd, k, F, m.H1, m.H2) > sgb) --Rd;
-        }
         const size_t l1 = conv_lds_bytes(R1 + k - 1, kImg, 1, m.H1, k * k, nt);
         const size_t l2 = conv_lds_bytes(R2 + k - 1, m.H1, F, m.H2, k * k * F, nt);
-        const size_t ld = sc ? dgrad_scatter_lds_bytes(Rd, k, F, m.H1, m.H2) : dgrad_lds_bytes(Rd, k, F, m.H2);
+        const size_t ld = dgrad_lds_bytes(Rd, k, F, m.H2);
         L1[i] = l1; L2[i] = l2; LD[i] = ld;
         for (int b = 0; b < B; ++b) {
             for (int y = 0; y < m.H1; y += R1) P.conv1.push_back({i, b, y, std::min(R1, m.H1 - y)});
@@ -1830,7 +1593,6 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         const size_t lw2 = wg_lds_bytes(k, m.H1, F, m.H2, F);
         const size_t lw1 = wg_lds_bytes(k, kImg, 1, m.H1, F);
         LW2[i] = lw2; LW1[i] = lw1;
-        if (i == 0) P.wg1_wave = env_int("MPO_WG1_WAVE", 1) != 0;
         const int K2 = k * k * F, K1w = k * k;
         for (int g = 0; g < m.g2; ++g) {
             const int b0 = (int)((long long)B * g / m.g2), b1 = (int)((long long)B * (g + 1) / m.g2);
@@ -1838,11 +1600,10 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         }
         // conv1_wgrad_kernel: every m-tile in one wave, MT bucketed to 1, 2, 4 or 7
         const int t1 = (K1w + 1 + 15) / 16, mt1 = t1 <= 1 ? 1 : t1 <= 2 ? 2 : t1 <= 4 ? 4 : 7;
-        if (P.wg1_wave) LW1[i] = (size_t)w1_lds_floats((B + m.g1 - 1) / m.g1, mt1, nt) * sizeof(float);
+        LW1[i] = (size_t)w1_lds_floats((B + m.g1 - 1) / m.g1, mt1, nt) * sizeof(float);
         for (int g = 0; g < m.g1; ++g) {
             const int b0 = (int)((long long)B * g / m.g1), b1 = (int)((long long)B * (g + 1) / m.g1);
-            if (P.wg1_wave) { P.wg1.push_back({i, 0, b0, b1, g, mt1}); continue; }
-            for (int mg = 0; mg * kWgRows <= K1w; ++mg) P.wg1.push_back({i, mg, b0, b1, g, wg_mt(K1w, mg)});
+            P.wg1.push_back({i, 0, b0, b1, g, mt1});
         }
         P.lds_wg_max = std::max({P.lds_wg_max, lw2, lw1});
         auto tiles = [&](std::vector<GemmItem>& v, int M, int N) {
@@ -1930,15 +1691,6 @@ hipError_t launch_dgrad_nt(const StepArgs& a, const ConvItem* items, int count, 
     return hipGetLastError();
 }
 
-template <int NT>
-hipError_t launch_dgrad_scatter_nt(const StepArgs& a, const ConvItem* items, int count, size_t lds, hipStream_t s) {
-    if (count <= 0) return hipSuccess;
-    auto kern = conv_dgrad_scatter_kernel<NT>;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3(count), dim3(256), lds, s, a, items);
-    return hipGetLastError();
-}
-
 template <int OP, int NT>
 hipError_t launch_wg_nt(const StepArgs& a, const WgItem* items, int count, size_t lds, int mt, hipStream_t s) {
     if (count <= 0) return hipSuccess;
@@ -1994,9 +1746,7 @@ hipError_t launch_conv(Plan& P, const StepArgs& a, size_t table_off, const Bucke
 hipError_t launch_dgrad(Plan& P, const StepArgs& a, hipStream_t s) {
     const ConvItem* base = dev_table<ConvItem>(P, P.off_dgrad);
     return launch_segs(P, P.bdg, "conv2_dgrad", s, [&](const Seg& sg) {
-        return dg_uses_scatter(P.dg_scatter, sg.nt)
-                   ? MPO_NT_SWITCH(launch_dgrad_scatter_nt, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, s)
-                   : MPO_NT_SWITCH(launch_dgrad_nt, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, s);
+        return MPO_NT_SWITCH(launch_dgrad_nt, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, s);
     });
 }
 
@@ -2012,9 +1762,10 @@ template <int OP>
 hipError_t launch_wg(Plan& P, const StepArgs& a, size_t table_off, const Bucketed& bk, hipStream_t s) {
     const WgItem* base = dev_table<WgItem>(P, table_off);
     return launch_segs(P, bk, OP == WG_CONV1 ? "conv1_wgrad" : "conv2_wgrad", s, [&](const Seg& sg) {
-        if (OP == WG_CONV1 && P.wg1_wave)
+        if constexpr (OP == WG_CONV1)
             return MPO_NT_SWITCH(launch_wg1_wave_nt, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, sg.sub, s);
-        return MPO_NT_SWITCH(WgLaunch<OP>::template go, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, sg.sub, s);
+        else
+            return MPO_NT_SWITCH(WgLaunch<OP>::template go, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, sg.sub, s);
     });
 }
 
@@ -2044,7 +1795,6 @@ StepArgs make_args(const Plan& P, const float* x, const int* labels, const int* 
     a.loss_sum = nullptr;
     a.correct = nullptr;
     a.debug = P.debug;
-    a.xcd = P.xcd;
     a.conv_mt = P.conv_mt;
     a.zero_off = P.zero_off;
     return a;
@@ -2084,7 +1834,6 @@ int mpo_pop_create(const MpoCnnSpec* specs, int n_members, int batch, void** han
     auto P = std::make_unique<Plan>();
     P->timer.on = env_int("MPO_POP_PROFILE", 0) != 0;
     P->debug = env_int("MPO_POP_DEBUG", 0);
-    P->xcd = env_int("MPO_XCD_SWIZZLE", 0) != 0;   // measured 21% slower on (profiles/r03/train_xcd*_e.json)
     P->timer_detail = env_int("MPO_POP_PROFILE", 0) > 1;
     int rc = build_plan(*P, specs, n_members, batch);
     if (rc) return rc;

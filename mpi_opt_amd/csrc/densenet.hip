@@ -73,13 +73,6 @@ struct ConvArgs {
     const float* w; long long w_ms;                       // padded weights [K16 + slack][N16]
     float* out; long long out_ms; int out_ps;
     int H, W, Cin, N, R;
-    // input-gradient conv of a BN site (r03): dn_bn_bwd_reduce fused into the epilogue.
-    // bpart != null: the site's input cat (bx) and coef [4][H] (bco: mean, inv, scale,
-    // shift); per (member, sample, row h) (sum dy, sum dy xhat), dy = out ELU'(x scale +
-    // shift), xhat = (x - mean) inv, into bpart [n][B][H][2] (the fold's slices = samples)
-    const float* bx; long long bx_ms; int bx_ps;
-    const float* bco; long long bco_ms;
-    double* bpart; int B;
 };
 
 struct WgArgs {
@@ -225,74 +218,6 @@ __device__ __forceinline__ void dn_conv_loop(const float* __restrict__ img, cons
     }
 }
 
-// dn_bn_bwd_reduce in the input-gradient conv's epilogue (ConvArgs::bpart): the
-// workgroup holds dz (this conv's output) for all N channels of its rows of sample
-// b, so the per-(member, sample, row) sums (dy, dy xhat) close inside it.  An m-tile
-// covers at most a few image rows (one when W is a multiple of 16); per (m-tile,
-// row) each lane sums its values in fp64, a fixed butterfly closes the wave, and the
-// rows' (m-tile) slots are added in m-tile order -- the same bits for a member alone
-// or in a population.  The per-sample slots are then folded over the batch by
-// dn_bn_bwd_fold (S = B).
-constexpr int kBnrRows = 32;   // rows per conv chunk: kMaxPix / W for W >= 4
-
-template <int NT>
-__device__ __forceinline__ void bn_reduce_epilogue(const ConvArgs& a, const f32x4 (&acc)[2][NT], int mine, int m, int b,
-                                                   int y0, int rows_out, int Mc, int wave, int lane, int krow, int kcol,
-                                                   float* smem) {
-    // the slots [rows][8 m-tiles][2] reuse the conv's LDS image (launch_conv sizes the
-    // dynamic LDS to hold them); the first barrier also retires every wave's image reads
-    double (*bred)[8][2] = reinterpret_cast<double (*)[8][2]>(smem);
-    const int H = a.H, W = a.W;
-    __syncthreads();
-    for (int e = threadIdx.x; e < kBnrRows * 16; e += 256) (&bred[0][0][0])[e] = 0.0;
-    __syncthreads();
-    const float* co = a.bco + m * a.bco_ms;
-    const float* xb = a.bx + m * a.bx_ms + ((long long)b * H + y0) * W * a.bx_ps;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        if (i >= mine) break;
-        const int mt = wave + 4 * i;
-        const int rf = (mt * 16) / W, rl = min((mt * 16 + 15) / W, rows_out - 1);
-        for (int rho = rf; rho <= rl; ++rho) {
-            const int h = y0 + rho;
-            const float mean = co[h], inv = co[H + h], sc = co[2 * H + h], sh = co[3 * H + h];
-            double s1 = 0.0, s2 = 0.0;
-#pragma unroll
-            for (int j = 0; j < NT; ++j) {
-                const int n = j * 16 + kcol;
-                if (n >= a.N) continue;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int mm = mt * 16 + krow * 4 + r;
-                    if (mm >= Mc || mm / W != rho) continue;
-                    const float x = xb[(long long)mm * a.bx_ps + n];
-                    const float y = x * sc + sh;
-                    const float dy = acc[i][j][r] * (y > 0.f ? 1.f : __expf(y));
-                    const float xh = (x - mean) * inv;
-                    s1 += dy;
-                    s2 += (double)dy * xh;
-                }
-            }
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) {
-                s1 += __shfl_xor(s1, o);
-                s2 += __shfl_xor(s2, o);
-            }
-            if (lane == 0) {
-                bred[rho][mt][0] = s1;
-                bred[rho][mt][1] = s2;
-            }
-        }
-    }
-    __syncthreads();
-    if ((int)threadIdx.x < 2 * rows_out) {
-        const int rho = threadIdx.x >> 1, q = threadIdx.x & 1;
-        double v = 0.0;
-        for (int t = 0; t < 8; ++t) v += bred[rho][t][q];
-        a.bpart[(((long long)m * a.B + b) * H + y0 + rho) * 2 + q] = v;
-    }
-}
-
 template <int KS, int NT>
 __global__ __launch_bounds__(256) void dn_conv_kernel(ConvArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -358,7 +283,7 @@ __global__ __launch_bounds__(256) void dn_conv_kernel(ConvArgs a) {
     const int N16 = NT * 16;
     if (mine == 2) dn_conv_loop<2, NT>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
     else if (mine == 1) dn_conv_loop<1, NT>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
-    else if (!a.bpart) return;
+    else return;
 
     float* dst = a.out + m * a.out_ms + ((long long)b * H + y0) * W * a.out_ps;
 #pragma unroll
@@ -376,7 +301,6 @@ __global__ __launch_bounds__(256) void dn_conv_kernel(ConvArgs a) {
             }
         }
     }
-    if (a.bpart) bn_reduce_epilogue<NT>(a, acc, mine, m, b, y0, rows_out, Mc, wave, lane, krow, kcol, smem);
 }
 
 // ============================================================================
@@ -1158,7 +1082,6 @@ struct DnPlan {
     long long bnp_off = 0;
     long long bnt_off = 0;      // fp64 BN totals of the latest site [n][H][2]      // fp64 BN slice partials [n][S][H][2] (shared by all sites)
     std::vector<int> bn_S, bn_bs;   // per layer: batch slices and samples per slice
-    bool bn_fuse = false;           // BN-backward sums in the input-gradient conv's epilogue (MPO_DN_BNFUSE=1)
     float *params = nullptr, *grads = nullptr, *m = nullptr, *v = nullptr, *state = nullptr, *act = nullptr;
     bool bound = false;
 };
@@ -1301,16 +1224,6 @@ int build_plan(DnPlan& p) {
         p.bn_bs[i] = bs;
         p.bn_S[i] = (B + bs - 1) / bs;
         bnp_max = std::max(bnp_max, (long long)p.bn_S[i] * ly.H * 2);
-        // the fused BN-backward sums of the input-gradient conv: one slice per sample
-        if (ly.kind != K_HEAD) bnp_max = std::max(bnp_max, (long long)B * ly.H * 2);
-    }
-    {
-        // 1: the BN-backward sums in the input-gradient conv's epilogue.  Measured slower
-        // (profiles/r03/dn_bnfuse_ab.txt: 83.8 vs 79.5 ms per step -- the epilogue's
-        // per-value row tests, wave reductions and the 100-slice fold cost more than
-        // the streaming dn_bn_bwd_reduce kernel), so off by default
-        const char* e = getenv("MPO_DN_BNFUSE");
-        p.bn_fuse = e && e[0] == '1';
     }
     long long bnp_ms;
     p.bnp_off = ar.take(bnp_max * 2, &bnp_ms);   // doubles = 2 floats (arena offsets are 64-float aligned)
@@ -1349,7 +1262,6 @@ int launch_conv(const ConvArgs& a, int n_members, int B, hipStream_t s) {
     const int nt = (a.N + 15) / 16;
     const dim3 grid((a.H + a.R - 1) / a.R, B, n_members);
     size_t lds = conv_lds(a.R, a.W, KS, a.Cin);
-    if (a.bpart) lds = std::max(lds, (size_t)kBnrRows * 16 * sizeof(double));   // the epilogue's BN slots
     if (lds > ((size_t)160 << 10)) { mpo::set_error("dn_conv: LDS %zu B exceeds 160 KiB", lds); return MPO_ENOTSUP; }
     switch (nt) {
         case 1: launch_conv_t<KS, 1>(a, grid, lds, s); break;
@@ -1543,14 +1455,12 @@ int enqueue_forward(DnPlan& p, const float* x, const int* labels, const int* ord
     return MPO_OK;
 }
 
-// fused: the input-gradient conv already wrote the per-sample sums (S = B slices)
-void enqueue_bn_bwd(DnPlan& p, const BnArgs& bn, int li, hipStream_t s, bool fused = false) {
+void enqueue_bn_bwd(DnPlan& p, const BnArgs& bn, int li, hipStream_t s) {
     double* bnp = reinterpret_cast<double*>(p.act + p.bnp_off);
-    const int S = fused ? p.B : p.bn_S[li];
+    const int S = p.bn_S[li];
     const bool v4 = bn_vec4(bn);
-    if (!fused)
-        hipLaunchKernelGGL(v4 ? dn_bn_bwd_reduce_kernel<4> : dn_bn_bwd_reduce_kernel<1>, dim3(bn.H, S, p.n), dim3(256),
-                           0, s, bn, bnp, S, p.bn_bs[li]);
+    hipLaunchKernelGGL(v4 ? dn_bn_bwd_reduce_kernel<4> : dn_bn_bwd_reduce_kernel<1>, dim3(bn.H, S, p.n), dim3(256),
+                       0, s, bn, bnp, S, p.bn_bs[li]);
     hipLaunchKernelGGL(dn_bn_bwd_fold_kernel, dim3(p.n), dim3(64), 0, s, bn, bnp, S);
     hipLaunchKernelGGL(v4 ? dn_bn_bwd_apply_kernel<4> : dn_bn_bwd_apply_kernel<1>, dim3((p.B * bn.H + 1) / 2, p.n),
                        dim3(256), 0, s, bn, (const double*)bnp, S);
@@ -1607,19 +1517,12 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
         c.w = p.act + ly.wd_off_act; c.w_ms = ((long long)ly.wd_rows * ly.wd_n16 + 63) & ~63LL;
         c.out = p.act + p.dz_off; c.out_ms = p.dz_ms; c.out_ps = ly.cin;
         c.H = ly.H; c.W = ly.W; c.Cin = ly.cout; c.N = ly.cin; c.R = ly.R;
-        const bool fused = p.bn_fuse && ly.R <= kBnrRows;
-        if (fused) {   // the site's BN-backward sums in this conv's epilogue
-            c.bx = bn.x; c.bx_ms = bn.x_ms; c.bx_ps = bn.x_ps;
-            c.bco = bn.coef; c.bco_ms = bn.coef_ms;
-            c.bpart = reinterpret_cast<double*>(p.act + p.bnp_off);
-            c.B = B;
-        }
         if (ly.ks == 3) DN_TRY(launch_conv<3>(c, n, B, s));
         else DN_TRY(launch_conv<1>(c, n, B, s));
         bn.dz = p.act + p.dz_off; bn.dz_ms = p.dz_ms;
         bn.dx = p.act + p.dcat_off[st]; bn.dx_ms = p.cat_ms[st]; bn.dx_ps = p.sC[st];
         bn.accumulate = ly.kind == K_DENSE ? 1 : 0;
-        enqueue_bn_bwd(p, bn, i, s, fused);
+        enqueue_bn_bwd(p, bn, i, s);
     }
     MPO_LAUNCH_CHECK();
     return MPO_OK;

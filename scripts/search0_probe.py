@@ -2,7 +2,7 @@
 10 random trials trained as populations [4, 4, 2] x 5 folds) timed per train step
 under plan-knob variants, all in one process (same box, same data).
 
-    python scripts/search0_probe.py base MPO_DG_TILES=16 MPO_CONV_MT=2
+    python scripts/search0_probe.py base dg_tiles=16 conv_mt=2
 """
 import os
 import sys
@@ -35,11 +35,8 @@ def members_of(params):
 
 
 def run(variant, pops, x, y, steps=60, evals=10):
-    env = {}
-    if variant != "base":
-        for kv in variant.split(","):
-            k, v = kv.split("=")
-            env[k] = v
+    # a variant is "base" or MPO_POP_PLAN's "key=value,..." (planner overrides, csrc/cnn.hip plan_knob)
+    env = {} if variant == "base" else {"MPO_POP_PLAN": variant}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     res = []

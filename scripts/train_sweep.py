@@ -23,11 +23,8 @@ def members_of(trials, folds=5):
 
 
 def run(variant, x, y, order, members, steps=3):
-    env = {}
-    if variant != "base":
-        for kv in variant.split(","):
-            k, v = kv.split("=")
-            env[k] = v
+    # a variant is "base" or MPO_POP_PLAN's "key=value,..." (planner overrides, csrc/cnn.hip plan_knob)
+    env = {} if variant == "base" else {"MPO_POP_PLAN": variant}
     env.setdefault("MPO_POP_PROFILE", "1")
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)

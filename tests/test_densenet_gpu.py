@@ -156,25 +156,3 @@ def test_trial_evaluator_routes_densenet_specs():
     # every trial trains with the evaluator's lr; the trials differ by their init seeds
     assert all(ev.model_provider.builder(*p).spec(lr=ev.lr).lr == ev.lr for p in ([-3.0], [-2.0]))
     assert len(set(round(f, 6) for f in foms)) == 3
-
-
-@pytest.mark.parametrize("case", CASES, ids=["cifar-d10", "odd-d7"])
-def test_fused_bn_backward_sums_agree_with_reduce_kernel(case, monkeypatch):
-    """r03: the BN-backward sums (dbeta, dgamma per image row) closed in the
-    input-gradient conv's epilogue (MPO_DN_BNFUSE=1, opt-in) and by dn_bn_bwd_reduce (default)
-    are the same fp64 sums in another order: every gradient tensor within 1e-5 of its
-    max |g| (f32), losses equal."""
-    lrs = [1e-3, 3e-3]
-    out = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("MPO_DN_BNFUSE", mode)
-        pop, layers, init, x, y, order, xd, yd, od_ = _setup(case["img"], case["classes"], case["depth"],
-                                                             case["blocks"], case["growth"], case["nbf"], lrs,
-                                                             case["B"], 40)
-        loss = pop.train_step(xd, yd, od_, 0).cpu().numpy()
-        out[mode] = (loss, [pop.get_grads(i) for i in range(len(lrs))])
-    np.testing.assert_array_equal(out["1"][0], out["0"][0])
-    for i in range(len(lrs)):
-        for n, g0 in out["0"][1][i].items():
-            g1 = out["1"][1][i][n]
-            assert np.max(np.abs(g1 - g0)) <= 1e-5 * (np.max(np.abs(g0)) + 1e-30), (i, n)

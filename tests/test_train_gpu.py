@@ -156,74 +156,6 @@ def test_population_isolation():
         assert la[2] == lo[0]
 
 
-def test_conv1_wgrad_kernels_agree(monkeypatch):
-    """conv1_wgrad_kernel (default) and the m-group conv_wgrad<WG_CONV1> kernel
-    (MPO_WG1_WAVE=0) give the same conv1 weight and bias gradients (different f32
-    summation orders: within 1e-5 of the tensor scale); the rest bit-identical."""
-    x, y = dataset(2)
-    tr, _ = orders(MEMBERS, x)
-    xd, yd = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
-    otr = torch.from_numpy(tr).cuda()
-    out = {}
-    for wave in ("1", "0"):
-        monkeypatch.setenv("MPO_WG1_WAVE", wave)
-        eng, specs, _ = make_engine()
-        eng.train_step(xd, yd, otr, 0)
-        out[wave] = (eng, eng.grads.cpu().numpy())
-    for i in range(len(MEMBERS)):
-        for name, (off, shape) in out["1"][0]._slices(i).items():
-            a = out["1"][1][off:off + int(np.prod(shape))]
-            b = out["0"][1][off:off + int(np.prod(shape))]
-            if name in ("w1", "b1"):
-                assert np.max(np.abs(a - b)) <= 1e-5 * (np.max(np.abs(b)) + 1e-30), (i, name)
-            else:
-                assert np.array_equal(a, b), (i, name)
-
-
-def test_scatter_dgrad_agrees_with_gather(monkeypatch):
-    """r03: conv_dgrad_scatter_kernel (MPO_DG_SCATTER=1: input-stationary, the
-    algorithmic MFMA count) and the halo-tap gather give the same conv2 input
-    gradient up to f32 summation order: only w1/b1 (conv1's weight gradient reads
-    dz1) differ, within 1e-5 of the tensor scale; every other tensor bit-identical."""
-    x, y = dataset(2)
-    tr, _ = orders(MEMBERS, x)
-    xd, yd = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
-    otr = torch.from_numpy(tr).cuda()
-    out = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("MPO_DG_SCATTER", mode)
-        eng, specs, _ = make_engine()
-        eng.train_step(xd, yd, otr, 0)
-        out[mode] = (eng, eng.grads.cpu().numpy())
-    for i in range(len(MEMBERS)):
-        for name, (off, shape) in out["1"][0]._slices(i).items():
-            a = out["1"][1][off:off + int(np.prod(shape))]
-            b = out["0"][1][off:off + int(np.prod(shape))]
-            if name in ("w1", "b1"):
-                assert np.max(np.abs(a - b)) <= 1e-5 * (np.max(np.abs(b)) + 1e-30), (i, name)
-            else:
-                assert np.array_equal(a, b), (i, name)
-
-
-def test_scatter_dgrad_matches_oracle_and_is_isolated(monkeypatch):
-    """The scatter path against the fp64 oracle (one-step gradients, 2-epoch loss
-    trajectories within 1e-3) and member isolation (bit-identical alone or in the
-    population: each wave's private band and the fixed wave-order sum)."""
-    monkeypatch.setenv("MPO_DG_SCATTER", "1")
-    test_one_step_gradients_match_oracle()
-    test_population_isolation()
-    test_multistep_losses_within_1e3(2)
-
-
-# (loss, optimizer) per member: option3's --loss / --optimizer (hyperparameter_search_option3.py:60-61)
-OPTION_MEMBERS = [
-    ((10, 2, 2, 50, 1e-3, 0.25, 0), "categorical_crossentropy", "adam"),
-    ((33, 5, 3, 77, 2e-3, 0.25, 2), "binary_crossentropy", "sgd"),
-    ((17, 3, 7, 120, 5e-2, 0.1, 3), "categorical_crossentropy", "sgd"),
-    ((50, 2, 2, 200, 1e-3, 0.25, 4), "binary_crossentropy", "adam"),
-]
-
-
 def test_loss_and_optimizer_options_match_oracle():
     """Members with categorical_crossentropy and/or SGD (MpoCnnSpec.options)
     train in one population beside the reference's BCE + Adam: first-step
