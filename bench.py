@@ -699,9 +699,13 @@ def bench_search_gp(args, torch, dist, ws, rank, dev):
                      "distinct_points": len({tuple(b) for b in batch})}
     out["_told_state"] = (pts, ys)
     out["_samples"] = samples
-    out["_samples_all"] = samples + list(st["samples"])
-    # GPU-seconds per 10-epoch 5-fold trial on one GPU, from this run's populations
-    out["_trial_s_gpu"] = rep["train_s"] / max(1, rep["trials_trained"]) * 10.0
+    # the projection's inputs: this run's refits (n) and optimizer window, the sequential
+    # ask(256)'s (n, seconds) latencies, the training GPU-seconds per 10-epoch 5-fold trial
+    out["_proj"] = {"run_refit_ns": [n for n, _ in samples], "optimizer_s": opt_s,
+                    "latency_samples": list(st["samples"]) + [sm for sm in samples if sm[0] < 64],
+                    "trial_s_gpu": rep["train_s"] / max(1, rep["trials_trained"]) * 10.0,
+                    "chain_workers": rep["chain_workers"]}
+    out["timeline"] = rep["timeline"]
     return out
 
 
@@ -716,6 +720,7 @@ class _CountingOptimizer:
         self.n0 = n_initial_points
         self.told = 0
         self.refits = []
+        self.tell_refits = []        # the subset refitted by tells (rank 0, sequential)
 
     def _point(self):
         return [int(self.rng.randint(d.low, d.high + 1)) if type(d).__name__ == "Integer"
@@ -727,6 +732,7 @@ class _CountingOptimizer:
         self.told += len(ys)
         if self.told >= self.n0:
             self.refits.append(self.told)
+            self.tell_refits.append(self.told)
         return OptimizeResult(x=list(xs[0]), fun=float(min(ys)))
 
     def ask(self, n):
@@ -736,7 +742,7 @@ class _CountingOptimizer:
         return [self._point() for _ in range(n)]
 
 
-def protocol_refits(world_size, block_size, num_iterations):
+def protocol_refits(world_size, block_size, num_iterations, with_tells=False):
     """The refits (their observation counts) and populations the reference's
     protocol runs for an option3 layout: the build's scheduler and PopulationComm
     driven with instant random FOMs and a refit-counting optimizer (CPU only)."""
@@ -762,6 +768,8 @@ def protocol_refits(world_size, block_size, num_iterations):
     with tempfile.TemporaryDirectory() as tmp:
         sched = _Sched(comm, nb, mnist_space(), checkpoint=os.path.join(tmp, "c.pkl"))
         sched.run(num_iterations=num_iterations)
+    if with_tells:
+        return sched.optimizer.refits, list(comm.batches), sched.optimizer.tell_refits
     return sched.optimizer.refits, list(comm.batches)
 
 
@@ -784,26 +792,38 @@ def _price(curve, ns):
     return float(sum(np.sum(c * ns ** p) for p, c in curve))
 
 
-def project_configs3(samples, trial_s_gpu, gpus=8, cpu=None):
+def project_configs3(proj, gpus=8, cpu=None):
     """BASELINE configs[3] in full (``-n 129 --block-size 2 --n-fold 5
-    --num-iterations 256 --epochs 10``, 256 trials over 8 GPUs): the protocol's
-    exact refit schedule (protocol_refits) priced by the refit + proposal cost
-    curve measured in this run, plus training at the measured GPU-seconds per
-    10-epoch 5-fold trial (``trial_s_gpu``, one GPU) spread over ``gpus`` GPUs --
-    the optimizer and the populations do not overlap in the population protocol
-    (a population trains once every block is busy).  With ``cpu`` ({"samples":
-    [(n, s)], "trial_s": s}) the same for the reference's host path.  A
-    projection from measured parts, not a measurement."""
-    refits, pops = protocol_refits(129, 2, 256)
-    coef = fit_refit_cost(samples)
+    --num-iterations 256 --epochs 10``, 256 trials over ``gpus`` GPUs), from this
+    run's measured parts -- a projection, labelled as such:
+
+    * the protocol's exact refit schedule (protocol_refits), split into the tells'
+      refits (rank 0, one after another) and the cl_min chains' (dealt over the
+      GPUs, ``chain_workers`` concurrent chains each, mpi_opt_amd.chains);
+    * a tell refit costs its sequential latency t(n) (fitted on the standalone
+      ask(256)'s refits + this run's small-n ones); a chain refit costs its
+      share of this run's optimizer window: c(n) = t(n) * optimizer_s / sum_run t(n)
+      (the measured concurrency on one GPU), divided by ``gpus``;
+    * training: trials x GPU-seconds per 10-epoch 5-fold trial / ``gpus``.
+    The optimizer and the populations do not overlap (a population's batches
+    resolve before it trains)."""
+    refits, pops, tells = protocol_refits(129, 2, 256, with_tells=True)
+    coef = fit_refit_cost(proj["latency_samples"])
     ns = np.array(refits, dtype=float)
-    t_gp = _price(coef, ns)
+    ts = np.array(tells, dtype=float)
+    run_ns = np.array(proj["run_refit_ns"], dtype=float)
+    scale = proj["optimizer_s"] / max(1e-12, _price(coef, run_ns))
+    t_tell = _price(coef, ts)
+    t_chain = (_price(coef, ns) - t_tell) * scale / gpus
     trials = sum(pops)
-    t_train = trials * trial_s_gpu / gpus
+    t_train = trials * proj["trial_s_gpu"] / gpus
+    t_gp = t_tell + t_chain
     out = {"workload": "configs[3] in full: -n 129 --block-size 2 --n-fold 5 --num-iterations 256 --epochs 10, "
-                       f"{gpus} GPUs", "refits": len(refits), "refit_n_mean": float(ns.mean()),
+                       f"{gpus} GPUs (projection from this run's measured parts)",
+           "refits": len(refits), "tell_refits": len(tells), "refit_n_mean": float(ns.mean()),
            "refit_n_max": int(ns.max()), "populations": pops, "trials_trained": trials,
-           "refit_cost_fit_s": coef, "optimizer_s": t_gp, "training_s": t_train,
+           "refit_latency_fit_s": coef, "chain_concurrency_scale": scale,
+           "optimizer_s": t_gp, "optimizer_tells_s": t_tell, "optimizer_chains_s": t_chain, "training_s": t_train,
            "trials_per_hour": trials * 3600.0 / (t_gp + t_train), "optimizer_share": t_gp / (t_gp + t_train)}
     if cpu:
         ccoef = fit_refit_cost(cpu["samples"], powers=(2, 3))
@@ -974,7 +994,7 @@ def main():
                 srch3.pop("_told_state")
                 srch3.pop("_samples")
                 srch3["cpu_baseline"] = None
-            srch3["projection_configs3_8gpu"] = project_configs3(srch3.pop("_samples_all"), srch3.pop("_trial_s_gpu"),
+            srch3["projection_configs3_8gpu"] = project_configs3(srch3.pop("_proj"),
                                                                  cpu=cpu_parts)
         if dn is not None:
             dn["cpu_baseline"] = cpu_baseline_densenet() if cpu else None

@@ -240,6 +240,12 @@ class PopulationComm:
         self.batches = []        # sizes of the populations trained
         self.trained_params = [] # parameters of every trial trained, in training order
         self.tail = []           # (params, fom) of trials trained after the exit broadcast (never told)
+        # per population: (seconds since the previous population finished, seconds waiting for
+        # its lazy ask batches, seconds training it, trials) -- the search's timeline
+        self.timeline = []
+        import time
+
+        self._t_last = time.perf_counter()
 
     def Get_size(self):
         return 1 + self.num_blocks * self.block_size
@@ -273,9 +279,16 @@ class PopulationComm:
         return _Request(self, self._block_of(source))
 
     def evaluate_pending(self):
+        import time
+
+        t0 = time.perf_counter()
         blocks = sorted(self.pending)
         params = resolve_all([self.pending.pop(b) for b in blocks])
+        t1 = time.perf_counter()
         foms = self.evaluator.evaluate(params)
+        t2 = time.perf_counter()
+        self.timeline.append((t0 - self._t_last, t1 - t0, t2 - t1, len(params)))
+        self._t_last = t2
         self.batches.append(len(params))
         self.trained_params.extend(params)
         for b, f in zip(blocks, foms):

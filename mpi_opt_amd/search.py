@@ -210,6 +210,8 @@ def run_search(args, x=None, y=None, log=print, progress=None):
         "trials_per_hour": 3600.0 * len(state.fom_list) / wall if wall > 0 else None,
         "trained_per_hour": 3600.0 * comm.trials_trained / wall if wall > 0 else None,
         "tail_trials": len(comm.tail),
+        # per population: [between populations (tells, asks, launches), waiting for ask batches, training, trials]
+        "timeline": [list(t) for t in comm.timeline],
         "best_fom": state.best_fom, "best_params": state.best_params,
         "gp": dict(_opt_mod.STATS),     # refits (tell + every cl_min lie), their n, refit / proposal seconds
     }

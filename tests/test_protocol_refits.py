@@ -39,3 +39,20 @@ def test_refit_cost_fit_recovers_a_polynomial():
     samples = [(n, 0.002 + 1e-5 * n + 3e-8 * n * n) for n in range(10, 500, 7)]
     coef = dict(bench.fit_refit_cost(samples))
     assert np.allclose([coef[0], coef[1], coef[2]], [0.002, 1e-5, 3e-8], rtol=1e-6)
+
+
+def test_configs3_projection_splits_tells_and_chains():
+    """project_configs3: tell refits cost their sequential latency on rank 0; chain
+    refits cost their measured concurrent share, divided over the GPUs."""
+    import bench
+
+    refits, pops, tells = bench.protocol_refits(129, 2, 256, with_tells=True)
+    assert len(refits) == 49471 and pops == [64, 64, 64, 64] and len(tells) == 182
+    proj = {"run_refit_ns": [100] * 1000, "optimizer_s": 10.0, "trial_s_gpu": 3.0, "chain_workers": 4,
+            "latency_samples": [(n, 0.01) for n in range(10, 500, 10)]}            # flat 10 ms latency
+    p8, p1 = bench.project_configs3(proj, gpus=8), bench.project_configs3(proj, gpus=1)
+    assert abs(p8["optimizer_tells_s"] - 182 * 0.01) < 1e-9 and p1["optimizer_tells_s"] == p8["optimizer_tells_s"]
+    # chains: (49471 - 182) refits x 10 ms/refit measured as 10 s per 1000 refits -> 1 x latency, / gpus
+    assert abs(p1["optimizer_chains_s"] - (49471 - 182) * 0.01) < 1e-6
+    assert abs(p8["optimizer_chains_s"] * 8 - p1["optimizer_chains_s"]) < 1e-6
+    assert abs(p8["training_s"] - 256 * 3.0 / 8) < 1e-9
