@@ -90,6 +90,22 @@ def _per_dispatch(rows, counter, match):
     return vals
 
 
+def _kernel_family(name):
+    """'void (anonymous namespace)::conv_dgrad_kernel<3>(...)' -> 'conv_dgrad_kernel<3>'."""
+    n = name.split("::", 1)[1] if "::" in name else name
+    return n.split("(", 1)[0]
+
+
+def _per_kernel_bytes(rows_f, rows_w, match, steps, top=12):
+    """HBM bytes per step by kernel instance (FETCH_SIZE x 2 + WRITE_SIZE), largest first."""
+    by = collections.defaultdict(float)
+    for rows, counter, mult in ((rows_f, "FETCH_SIZE", 2.0), (rows_w, "WRITE_SIZE", 1.0)):
+        for r in rows:
+            if r["Counter_Name"] == counter and match(r["Kernel_Name"]):
+                by[_kernel_family(r["Kernel_Name"])] += mult * 1024.0 * float(r["Counter_Value"]) / steps
+    return dict(sorted(by.items(), key=lambda kv: -kv[1])[:top])
+
+
 def live_pmc(train_trials):
     """HBM traffic measured in this run (MI355X_MICROARCH.md HBM section): separate
     FETCH_SIZE and WRITE_SIZE passes (KiB; FETCH_SIZE doubled -- gfx950 reports half
@@ -120,8 +136,10 @@ def live_pmc(train_trials):
     tr_prog = [os.path.join(ROOT, "scripts", "train_probe.py"), "--steps", "1", "--trials", str(train_trials)]
     try:
         ours = lambda k: "anonymous namespace" in k     # noqa: E731 -- libmpo's kernels, not torch's setup
-        f = _per_dispatch(pmc_pass(["FETCH_SIZE"], tr_prog), "FETCH_SIZE", ours)
-        w = _per_dispatch(pmc_pass(["WRITE_SIZE"], tr_prog), "WRITE_SIZE", ours)
+        rf, rw = pmc_pass(["FETCH_SIZE"], tr_prog), pmc_pass(["WRITE_SIZE"], tr_prog)
+        f = _per_dispatch(rf, "FETCH_SIZE", ours)
+        w = _per_dispatch(rw, "WRITE_SIZE", ours)
+        per_kernel = _per_kernel_bytes(rf, rw, ours, steps)
         fetch = 1024.0 * sum(f.values()) / steps
         write = 1024.0 * sum(w.values()) / steps
         rows = pmc_pass(["SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"], tr_prog)
@@ -135,19 +153,21 @@ def live_pmc(train_trials):
                 den += gui / 8 * 1024
         out["train"] = {"hbm_bytes_per_train_batch": 2.0 * fetch + write, "fetch_size_bytes_raw": fetch,
                         "write_size_bytes": write, "mfma_busy": num / den if den else None,
-                        "per_kernel_mfma_busy": per}
+                        "per_kernel_mfma_busy": per, "per_kernel_hbm_bytes": per_kernel}
     except Exception as e:  # noqa: BLE001
         out["errors"].append(f"train: {e}")
     # DenseNet (configs[4]): 2 warmup + 3 train steps of the 32-member population
     dn_prog = [os.path.join(ROOT, "scripts", "dn_probe.py"), "--steps", "3", "--no-eval"]
     try:
         ours = lambda k: "anonymous namespace" in k     # noqa: E731
-        f = _per_dispatch(pmc_pass(["FETCH_SIZE"], dn_prog), "FETCH_SIZE", ours)
-        w = _per_dispatch(pmc_pass(["WRITE_SIZE"], dn_prog), "WRITE_SIZE", ours)
+        rf, rw = pmc_pass(["FETCH_SIZE"], dn_prog), pmc_pass(["WRITE_SIZE"], dn_prog)
+        f = _per_dispatch(rf, "FETCH_SIZE", ours)
+        w = _per_dispatch(rw, "WRITE_SIZE", ours)
         fetch = 1024.0 * sum(f.values()) / 5
         write = 1024.0 * sum(w.values()) / 5
         out["densenet"] = {"hbm_bytes_per_train_step": 2.0 * fetch + write, "fetch_size_bytes_raw": fetch,
-                           "write_size_bytes": write, "steps": 5}
+                           "write_size_bytes": write, "steps": 5,
+                           "per_kernel_hbm_bytes": _per_kernel_bytes(rf, rw, ours, 5)}
     except Exception as e:  # noqa: BLE001
         out["errors"].append(f"densenet: {e}")
     return out

@@ -24,6 +24,8 @@ waited for when the population that trains it is about to start
   HIP stream (a refit is ~100 latency-bound L-BFGS-B rounds of small kernels;
   several chains keep the GPU busy, and ctypes releases the GIL while a round
   waits on its stream);
+* :class:`ProcessChainExecutor` -- the same with spawned worker processes (no
+  shared GIL for the chains' host-side L-BFGS-B);
 * :class:`DistributedChainExecutor` -- the batches of one population dealt over
   the torch.distributed ranks (LPT on the refit cost), each rank running its
   share on its own worker threads, results all-gathered to rank 0.
@@ -184,6 +186,79 @@ class ThreadChainExecutor:
         for t in self._threads:
             t.join()
         self._threads = []
+
+
+def _process_init(device):
+    """Chain worker process: bind the GPU once (spawned interpreter, fresh HIP context)."""
+    global _WORKER_DEVICE
+    _WORKER_DEVICE = device
+    if device is not None:
+        import torch
+
+        torch.cuda.set_device(torch.device(device))
+
+
+_WORKER_DEVICE = None
+
+
+def _process_run(job):
+    from . import optimizer as O
+
+    O.reset_stats()
+    t0 = time.perf_counter()
+    X, trace = job.run(_WORKER_DEVICE)
+    return X, trace, dict(O.STATS), time.perf_counter() - t0
+
+
+class ProcessChainExecutor:
+    """Runs batches in ``workers`` spawned processes sharing ``device`` (each its own
+    HIP context and hardware queues, and its own interpreter: the chains' host
+    side -- scipy's L-BFGS-B, numpy -- runs without one GIL for all of them).
+    Each batch's refit accounts are merged into this process's STATS."""
+
+    def __init__(self, device=None, workers=4):
+        import multiprocessing as mp
+
+        self.device = None if device is None else str(device)
+        self.workers = int(workers)
+        self._pool = mp.get_context("spawn").Pool(self.workers, initializer=_process_init,
+                                                   initargs=(self.device,))
+        self._seq = 0
+        self.busy_s = 0.0
+        self.wait_s = 0.0
+
+    def submit(self, job):
+        b = LazyBatch(self, job)
+        b.seq = self._seq
+        self._seq += 1
+        b._async = self._pool.apply_async(_process_run, (job,))
+        return b
+
+    def _collect(self, batch):
+        from . import optimizer as O
+
+        try:
+            X, trace, stats, busy = batch._async.get()
+        except BaseException as e:  # noqa: BLE001 -- re-raised by result()
+            batch._set(error=e)
+            return
+        O.merge_stats(stats)
+        self.busy_s += busy
+        batch._set(X, trace)
+
+    def run_now(self, jobs):
+        batches = [self.submit(j) for j in jobs]
+        return [(b.result(), b._trace) for b in batches]
+
+    def wait(self, batch):
+        t0 = time.perf_counter()
+        if not batch.done():
+            self._collect(batch)
+        self.wait_s += time.perf_counter() - t0
+
+    def close(self):
+        self._pool.close()
+        self._pool.join()
 
 
 class DistributedChainExecutor:

@@ -73,6 +73,8 @@ def make_parser():
     p.add_argument("--chain-workers", type=int, default=4,
                    help="concurrent cl_min ask batches per GPU (worker threads, one HIP stream each); "
                         "0 runs every ask inline, as the reference's Coordinator does")
+    p.add_argument("--chain-processes", action="store_true",
+                   help="run the concurrent ask batches in spawned worker processes instead of threads")
     return p
 
 
@@ -112,7 +114,7 @@ def run_search(args, x=None, y=None, log=print, progress=None):
     import torch
 
     from .blocks import DistributedEvaluator, PopulationComm, ShardedScorer, TrialEvaluator
-    from .chains import DistributedChainExecutor, ThreadChainExecutor
+    from .chains import DistributedChainExecutor, ProcessChainExecutor, ThreadChainExecutor
     from .models import BuilderFromFunction, mnist_space, test_mnist
     from .population import synthetic_mnist
     from .scheduler import AskTellScheduler
@@ -152,7 +154,10 @@ def run_search(args, x=None, y=None, log=print, progress=None):
                                progress=progress if (dist is None or dist.get_rank() == 0) else None,
                                loss=args.loss, optimizer=args.optimizer, stopping=stopping)
     local_eval = evaluator
-    chains = ThreadChainExecutor(dev, workers=args.chain_workers) if args.chain_workers > 0 else None
+    chains = None
+    if args.chain_workers > 0:
+        pool = ProcessChainExecutor if args.chain_processes else ThreadChainExecutor
+        chains = pool(dev, workers=args.chain_workers)
     if dist is not None:
         evaluator = DistributedEvaluator(evaluator)
         if chains is not None:
@@ -203,6 +208,7 @@ def run_search(args, x=None, y=None, log=print, progress=None):
         "optimizer_s": tm["ask_s"] + tm["tell_s"] + chain_wait,
         "ask_s": tm["ask_s"], "tell_s": tm["tell_s"], "asks": tm["asks"], "tells": tm["tells"],
         "chain_wait_s": chain_wait, "chain_workers": args.chain_workers,
+        "chain_pool": ("processes" if args.chain_processes else "threads") if chains is not None else None,
         "chain_busy_s": chains.busy_s if chains is not None else 0.0,
         "train_s": local_eval.train_s,
         # headline on TOLD trials (the ones the optimizer saw); the in-flight tail the

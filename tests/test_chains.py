@@ -19,7 +19,7 @@ import torch.multiprocessing as mp
 
 from mpi_opt_amd import optimizer as O
 from mpi_opt_amd.blocks import DistributedEvaluator, PopulationComm
-from mpi_opt_amd.chains import DistributedChainExecutor, LazyBatch, LazyPoint, ThreadChainExecutor
+from mpi_opt_amd.chains import DistributedChainExecutor, LazyBatch, LazyPoint, ProcessChainExecutor, ThreadChainExecutor
 from mpi_opt_amd.models import mnist_space
 from mpi_opt_amd.scheduler import AskTellScheduler
 
@@ -196,3 +196,29 @@ def test_chains_dealt_over_gloo_ranks_equal_sequential(fake_gp, tmp_path):
     assert rounds == len(want["batches"])       # one dispatch of buffered batches per population
     for k in ("told", "foms", "trained", "batches", "refits"):
         assert got[k] == want[k], k
+
+
+def _patched_process_init(device):
+    from mpi_opt_amd import chains
+
+    O.Optimizer._fit_and_propose = fake_fit_and_propose
+    chains._process_init(device)
+
+
+def test_lazy_process_search_equals_sequential(fake_gp, tmp_path, monkeypatch):
+    """ProcessChainExecutor: batches in spawned processes (the CPU surrogate is
+    installed in each worker by its initializer); same search, refit accounts merged."""
+    import random
+
+    from mpi_opt_amd import chains
+
+    random.seed(5)
+    want = _search(str(tmp_path))
+    monkeypatch.setattr(chains, "_process_init", _patched_process_init)
+    ex = ProcessChainExecutor(device=None, workers=2)
+    try:
+        random.seed(5)
+        got = _search(str(tmp_path), ex)
+    finally:
+        ex.close()
+    assert got == want
