@@ -58,7 +58,6 @@ struct LmlArgs {
     double* ws;           // per theta: ws_stride doubles
     long long ws_stride;
     int stop;             // diagnostics only (env MPO_FIT_DEBUG): return after phase 1/2/3/4
-    int pair;             // split sweep: pivot_block_sweep2 (two steps per LDS round, MPO_FIT_PAIR != 0)
     const double* theta_src;  // fused split sweep, host-staged call: theta in pinned host memory (device
                               // view), read by sw_xs_build_kernel and copied to `theta`; else nullptr
 };
@@ -514,338 +513,31 @@ __global__ __launch_bounds__(kFitThreads) void lml_grad_kernel(LmlArgs a) {
 }
 
 // ===========================================================================
-// Block-sweep variant (n <= kSwMaxN): K^-1 and log det K by the symmetric sweep
-// operator over 32-wide pivot blocks, trailing updates on v_mfma_f64_16x16x4.
+// Block sweep (n > kSplitMinN): K^-1 and log det K by the symmetric sweep operator
+// over 32-wide pivot blocks, trailing updates on v_mfma_f64_16x16x4.
 //
 // Sweeping pivot block k of a symmetric A (Goodnight's sweep, block form):
 //     A_kk <- -A_kk^-1,   A_ik <- A_ik A_kk^-1,   A_ij <- A_ij - A_ik A_kk^-1 A_kj
 // for i, j != k; after every block is swept A = -K^-1, and log det K is the sum of
 // the log determinants of the pivot blocks at their sweep (the Schur complements
 // a Cholesky factorisation meets).  Work: n^3 flops, all in rank-32 MFMA updates
-// of the lower triangle (L2-resident, one XCD's L2 per theta); no L^-1, and the
-// pair phase reads K^-1 directly instead of forming L^-T L^-1 entry by entry.
-// Per step (3 barriers):
-//   a. the old block column C = A[:, k] -> LDS (stride 33: conflict-free B reads)
-//   b. wave 0 sweeps the 32x32 pivot block in registers (lane = row, the pivot row
-//      broadcast through LDS), accumulating log det and flagging a non-positive
-//      pivot (sklearn's Cholesky LinAlgError);
-//   c. G = C P^-1 for every 16-row tile outside the block (MFMA) -> workspace;
-//   d. every lower 16x16 tile outside block k: A_IJ -= G_I C_J^T (8 MFMAs, K = 32);
-//      block column k <- G, the pivot block <- -P^-1.
-// Padding rows/columns n..np carry the identity, so they never couple to K.
+// of the lower triangle; no L^-1, and the pair phase reads K^-1 directly instead
+// of forming L^-T L^-1 entry by entry.  Padding rows/columns n..np carry the
+// identity, so they never couple to K.
+//
+// Spread over the device: sw_xs_build_kernel (xs, K; many workgroups), one
+// sw_step_kernel per pivot block (every workgroup sweeps the 32x32 pivot block
+// in its wave 0 -- a non-positive pivot is sklearn's Cholesky LinAlgError --
+// then each wave updates one lower 16x16 tile A_IJ -= G_I C_J^T, G_I = C_I P^-1),
+// sw_alpha_kernel, sw_pairs_final_kernel (gradient pairs, last workgroup sums the
+// partials and writes the LML).  (A single-workgroup form of the same sweep ran
+// every trailing update on one CU: 2.45 ms per launch at n = 500 vs 0.86 ms.)
 constexpr int kSwNb = 32;
-constexpr int kSwLd = kSwNb + 1;
-constexpr int kSwMaxN = 576;   // LDS: np * 33 + 2 * 32 * 33 doubles <= 160 KiB
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 __host__ __device__ inline long long sw_np(int n) { return (n + kSwNb - 1) / kSwNb * kSwNb; }
 
-// per-theta workspace (doubles): xs [n][d] | alpha [np] | A [np][np] | G [np][32]
-__host__ __device__ inline long long sw_ws_doubles(int n, int d) {
-    auto al = [](long long x) { return (x + 31) & ~31LL; };
-    const long long np = sw_np(n);
-    return al((long long)n * d) + al(np) + np * np + np * kSwNb;
-}
-
-template <int DP>
-__global__ __launch_bounds__(kFitThreads) void lml_sweep_kernel(LmlArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double fsm[];
-    const int b = blockIdx.x;
-    const int n = a.n, d = a.d;
-    const int np = (int)sw_np(n);
-    const int nbk = np / kSwNb, ntile = np / 16;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const double* th = a.theta + (long long)b * (d + 2);
-    auto al = [](long long x) { return (x + 31) & ~31LL; };
-    double* ws = a.ws + (long long)b * a.ws_stride;
-    double* xs = ws;
-    double* alpha = xs + al((long long)n * d);
-    double* A = alpha + al(np);                    // [np][np], lower triangle + full diagonal tiles
-    double* G = A + (long long)np * np;            // [np][32]
-    double* Cp = fsm;                              // [np][33] old block column
-    double* Pi = Cp + np * kSwLd;                  // [32][33] P^-1 (then a [32][33] pivot-row area, unused here)
-    __shared__ int fail_s;
-    __shared__ double logdet_s;
-
-    const double amp = exp(th[0]);
-    const double noise = exp(th[d + 1]);
-    double ls[DP];
-#pragma unroll
-    for (int c = 0; c < DP; ++c) ls[c] = c < d ? exp(th[1 + c]) : 1.0;
-
-    // ---- 1. xs = X / ls; K into A (lower triangle and the full diagonal 16x16 tiles)
-    for (int e = tid; e < n * d; e += kFitThreads) {
-        const int c = e % d;
-        double lc = 1.0;
-#pragma unroll
-        for (int q = 0; q < DP; ++q)
-            if (q == c) lc = ls[q];
-        xs[e] = a.X[e] / lc;
-    }
-    if (tid == 0) { fail_s = 0; logdet_s = 0.0; }
-    __syncthreads();
-    for (int i = wave; i < np; i += kFitWaves) {
-        double xi[DP];
-#pragma unroll
-        for (int c = 0; c < DP; ++c) xi[c] = (c < d && i < n) ? xs[i * d + c] : 0.0;
-        const int jend = (i | 15) + 1;             // through the end of i's diagonal tile
-        for (int j = lane; j < jend && j < np; j += 64) {
-            double v;
-            if (i >= n || j >= n) {
-                v = i == j ? 1.0 : 0.0;
-            } else if (i == j) {
-                v = amp * 1.0 + noise + kFitJitter;
-            } else {
-                double r2 = 0.0;
-#pragma unroll
-                for (int c = 0; c < DP; ++c)
-                    if (c < d) {
-                        const double t = xi[c] - xs[j * d + c];
-                        r2 += t * t;
-                    }
-                const double k = sqrt(r2) * kSqrt5;
-                v = amp * ((1.0 + k + k * k / 3.0) * exp(-k));
-            }
-            A[(long long)i * np + j] = v;
-        }
-    }
-    __threadfence_block();
-    __syncthreads();
-    if (a.stop == 1) return;
-
-    // ---- 2. block sweeps
-    for (int k = 0; k < nbk; ++k) {
-        const int k0 = k * kSwNb;
-        // a. old block column (symmetric read from the lower storage)
-        for (int e = tid; e < np * kSwNb; e += kFitThreads) {
-            const int i = e >> 5, c = e & 31, j = k0 + c;
-            Cp[i * kSwLd + c] = i >= j ? A[(long long)i * np + j] : A[(long long)j * np + i];
-        }
-        __syncthreads();
-        // b. wave 0: sweep the pivot block in registers: lane l < 32 holds row l;
-        //    the pivot row is broadcast by v_readlane (wave-uniform SGPR operands),
-        //    so a step has no LDS round trip; log det accumulates as a product of
-        //    pivots (each in [noise, amp + noise]: no over/underflow in 32 steps)
-        if (wave == 0 && a.stop != 6) {   // stop 6: diagnostics only, pivot sweep skipped
-            const int l = lane & 31;
-            double r[kSwNb];
-#pragma unroll
-            for (int j = 0; j < kSwNb; ++j) r[j] = Cp[(k0 + l) * kSwLd + j];
-            double prod = 1.0;
-            int bad = 0;
-#pragma unroll
-            for (int c = 0; c < kSwNb; ++c) {
-                const double p = readlane_f64(r[c], c);
-                if (!(p > 0.0) || !isfinite(p)) bad = bad ? bad : c + 1;
-                prod *= p;
-                const double ip = 1.0 / p;
-                const bool piv = l == c;
-                const double t = r[c] * ip;
-#pragma unroll
-                for (int j = 0; j < kSwNb; ++j) {
-                    if (j == c) continue;
-                    const double pj = readlane_f64(r[j], c);
-                    r[j] = piv ? r[j] * ip : fma(-t, pj, r[j]);
-                }
-                r[c] = piv ? -ip : t;
-            }
-            // r = -P^-1 (row l)
-            if (lane < kSwNb) {
-#pragma unroll
-                for (int j = 0; j < kSwNb; ++j) Pi[l * kSwLd + j] = -r[j];
-            }
-            if (lane == 0) {
-                logdet_s += log(prod);
-                if (bad && !fail_s) fail_s = k0 + bad;
-            }
-        }
-        __syncthreads();
-        // c. G = C P^-1 for the 16-row tiles outside block k (2 column tiles x 8 k-steps)
-        for (int R = wave; R < ntile; R += kFitWaves) {
-            if ((R >> 1) == k) continue;
-            f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-            const int ar = (16 * R + (lane & 15)) * kSwLd + (lane >> 4);
-            const int br = (lane >> 4) * kSwLd + (lane & 15);
-#pragma unroll
-            for (int ks = 0; ks < 8; ++ks) {
-                const double av = Cp[ar + 4 * ks];
-                acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, Pi[br + 4 * ks * kSwLd], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, Pi[br + 4 * ks * kSwLd + 16], acc1, 0, 0, 0);
-            }
-            // stored in A-fragment order for the trailing update: element (row, col)
-            // of row tile R -> Gf[(R*8 + col/4)*64 + row%16 + 16*(col%4)]
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int rr = (lane >> 4) + 4 * q, c0 = lane & 15, c1 = 16 + c0;
-                G[((long long)R * 8 + (c0 >> 2)) * 64 + rr + 16 * (c0 & 3)] = acc0[q];
-                G[((long long)R * 8 + (c1 >> 2)) * 64 + rr + 16 * (c1 & 3)] = acc1[q];
-            }
-        }
-        __threadfence_block();
-        __syncthreads();
-        // d. trailing update of the lower tiles outside block k; block column k <- G,
-        //    pivot block <- -P^-1
-        const int nt_low = ntile * (ntile + 1) / 2;
-        // tiles of this wave, in order; the next tile's C and G fragments are
-        // loaded before the current tile's MFMAs (latency of L2 hides under them)
-        auto tile_of = [&](int t, int& I, int& J) {
-            I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-            while (I * (I + 1) / 2 > t) --I;
-            while ((I + 1) * (I + 2) / 2 <= t) ++I;
-            J = t - I * (I + 1) / 2;
-        };
-        auto live = [&](int t) {
-            int I, J;
-            tile_of(t, I, J);
-            return (I >> 1) != k && (J >> 1) != k;
-        };
-        auto next_live = [&](int t) {
-            for (; t < nt_low; t += kFitWaves)
-                if (live(t)) return t;
-            return nt_low;
-        };
-        int t = a.stop == 7 ? nt_low : next_live(wave);
-        f64x4 cc;
-        double ga[8];
-        auto fetch = [&](int tt) {
-            int I, J;
-            tile_of(tt, I, J);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) cc[q] = A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)];
-#pragma unroll
-            for (int ks = 0; ks < 8; ++ks) ga[ks] = G[((long long)I * 8 + ks) * 64 + lane];
-        };
-        if (t < nt_low) fetch(t);
-        while (t < nt_low) {
-            int I, J;
-            tile_of(t, I, J);
-            f64x4 acc = cc;
-            double av[8];
-#pragma unroll
-            for (int ks = 0; ks < 8; ++ks) av[ks] = ga[ks];
-            const int tn = next_live(t + kFitWaves);
-            if (tn < nt_low) fetch(tn);
-            const int cb = (16 * J + (lane & 15)) * kSwLd + (lane >> 4);
-#pragma unroll
-            for (int ks = 0; ks < 8; ++ks)
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[ks], Cp[cb + 4 * ks], acc, 0, 0, 0);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)] = acc[q];
-            t = tn;
-        }
-        for (int e = tid; e < np * kSwNb; e += kFitThreads) {
-            const int i = e >> 5, c = e & 31, j = k0 + c;
-            if ((i >> 5) == k) {
-                A[(long long)i * np + j] = -Pi[(i - k0) * kSwLd + c];
-            } else {
-                const double gv = G[((long long)(i >> 4) * 8 + (c >> 2)) * 64 + (i & 15) + 16 * (c & 3)];
-                if (i > j) A[(long long)i * np + j] = gv;
-                else A[(long long)j * np + i] = gv;
-            }
-        }
-        __threadfence_block();
-        __syncthreads();
-    }
-    if (a.stop == 2) return;
-    if (fail_s) {  // sklearn: LinAlgError -> (-inf, zeros)
-        if (tid == 0) { a.lml[b] = -INFINITY; a.info[b] = fail_s; }
-        for (int c = tid; c < d + 2; c += kFitThreads) a.grad[(long long)b * (d + 2) + c] = 0.0;
-        return;
-    }
-    auto kinv = [&](int i, int j) -> double {   // (K^-1)_ij = -A (symmetric, lower storage)
-        return i >= j ? -A[(long long)i * np + j] : -A[(long long)j * np + i];
-    };
-
-    // ---- 3. alpha = K^-1 y
-    for (int i = tid; i < n; i += kFitThreads) {
-        double s0 = 0.0, s1 = 0.0;
-        int j = 0;
-        for (; j + 1 < n; j += 2) {
-            s0 += kinv(i, j) * a.y[j];
-            s1 += kinv(i, j + 1) * a.y[j + 1];
-        }
-        if (j < n) s0 += kinv(i, j) * a.y[j];
-        alpha[i] = s0 + s1;
-    }
-    __syncthreads();
-    if (a.stop == 4) return;
-
-    // ---- 4. pairs (i >= j): W_ij dK_ij / dtheta, W = alpha alpha^T - K^-1
-    double g[DP + 2];
-#pragma unroll
-    for (int c = 0; c < DP + 2; ++c) g[c] = 0.0;
-    for (int i = wave; i < n; i += kFitWaves) {
-        const double ai = alpha[i];
-        double xi[DP];
-#pragma unroll
-        for (int c = 0; c < DP; ++c) xi[c] = c < d ? xs[i * d + c] : 0.0;
-        for (int j = lane; j <= i; j += 64) {
-            const double W = (ai * alpha[j] + A[(long long)i * np + j]) * (i == j ? 1.0 : 2.0);
-            // two passes over the dims (distance, then gradient terms) instead of a
-            // D[DP] array: fewer live registers at 1024 threads per workgroup
-            const double* xj = xs + j * d;
-            double r2 = 0.0;
-#pragma unroll
-            for (int c = 0; c < DP; ++c)
-                if (c < d) {
-                    const double t = xi[c] - xj[c];
-                    r2 += t * t;
-                }
-            const double sq = sqrt(5.0 * r2);
-            const double e = exp(-sq);
-            const double Mij = i == j ? 1.0 : (1.0 + sq + sq * sq / 3.0) * e;
-            g[0] += W * (amp * Mij);
-            const double f = W * amp * (5.0 / 3.0) * (sq + 1.0) * e;
-#pragma unroll
-            for (int c = 0; c < DP; ++c)
-                if (c < d) {
-                    const double t = xi[c] - xj[c];
-                    g[1 + c] += f * (t * t);
-                }
-            if (i == j) g[DP + 1] += W * noise;
-        }
-    }
-
-    // ---- 5. fixed-order reduction: lanes (butterfly) -> waves (LDS, in order)
-    __syncthreads();
-    double* red = fsm;  // [kFitWaves][DP + 2]
-#pragma unroll
-    for (int c = 0; c < DP + 2; ++c) {
-        const double v = wave_sum_bcast(g[c]);
-        if (lane == 0) red[wave * (DP + 2) + c] = v;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        double ya = 0.0;
-        for (int i = 0; i < n; ++i) ya += a.y[i] * alpha[i];
-        a.lml[b] = -0.5 * ya - 0.5 * logdet_s - 0.5 * n * kLog2Pi;
-        a.info[b] = 0;
-        double* out = a.grad + (long long)b * (d + 2);
-        for (int c = 0; c < d + 2; ++c) {
-            const int src = c == 0 ? 0 : (c == d + 1 ? DP + 1 : c);
-            double s = 0.0;
-            for (int w = 0; w < kFitWaves; ++w) s += red[w * (DP + 2) + src];
-            out[c] = 0.5 * s;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Split block sweep (n > kSplitMinN): the same sweep as lml_sweep_kernel, spread
-// over the device.  The single-workgroup kernel runs every rank-32 trailing update
-// on ONE CU (2.45 ms per launch at n = 500: the n^3 MFMA work of a theta on 4
-// SIMDs); here each sweep step is two launches --
-//   sw_pivot_kernel   (one wave per theta) pivot block of C_k swept in
-//                     registers, P^-1 -> global (log det, failure flag
-//                     accumulate in the workspace);
-//   sw_update_kernel  (many workgroups per theta, one 16x16 lower tile per wave
-//                     at a time) G_I = C_I P^-1 per wave, A_IJ -= G_I C_J^T
-//                     outside block k, block column k <- G, pivot block <- -P^-1
-// -- bracketed by sw_build_kernel (xs, K; many workgroups) and sw_finish_kernel
-// (alpha, the pair/gradient phase and the LML; one workgroup per theta).  Same
-// arithmetic in the same order as lml_sweep_kernel, so both give the same bits.
 constexpr int kSplitMinN = 48;    // past it the split beats both single-workgroup kernels (0.09 vs 0.20 ms at n = 64)
 constexpr int kUpdThreads = 256;
 constexpr int kUpdTilesPerWave = 1;   // one lower tile per wave: latency-bound steps want many waves
@@ -908,7 +600,7 @@ __global__ __launch_bounds__(256) void sw_xs_kernel(LmlArgs a) {
 }
 
 // grid (np/16, B): K rows [16 bx, 16 bx + 16) -- the lower triangle and the full
-// diagonal 16x16 tiles, identity on the padding (as lml_sweep_kernel phase 1)
+// diagonal 16x16 tiles, identity on the padding
 template <int DP>
 __global__ __launch_bounds__(256) void sw_build_kernel(LmlArgs a) {
     const int b = blockIdx.y, n = a.n, d = a.d, np = (int)sw_np(n);
@@ -1012,14 +704,18 @@ __global__ __launch_bounds__(1024) void sw_xs_build_kernel(LmlArgs a) {
     }
 }
 
-// pivot_block_sweep with two steps per LDS round: the pivot rows c and c + 1 are
-// broadcast together, and every lane forms row c + 1 after step c itself
+// Gauss-Jordan sweep of the 32x32 pivot block rows k0 .. k0+31 of C (row-major
+// [np][32]) by one wave: lane l + 32 h holds columns [16 h, 16 h + 16) of row l,
+// eliminating with the pivot row (not the symmetric column: that measured 10-100x
+// less accurate at cond(K) ~ 1e5).  Two steps per LDS round: the pivot rows c and
+// c + 1 are broadcast together, and every lane forms row c + 1 after step c itself
 // (row2' = fma(-t21, row1, row2), its column c = t21, pv2 = row2'[c + 1]) and the
 // column-(c+1) entry of its own row after step c (colv2' = fma(f1, row1[c+1], colv2),
-// 0 for the zeroed pivot row) with exactly the operations the lanes owning them
-// perform in pivot_block_sweep -- so the result is the same bits with half the LDS
-// round trips (and half the serial latency chains) at 16 more FMAs per two steps.
-// rowb: 64 doubles.
+// 0 for the zeroed pivot row) with exactly the operations the owning lanes perform
+// in a one-step sweep (r03: the same bits, tested against it before that form was
+// removed) -- half the LDS round trips and serial latency chains, 16 more FMAs per
+// two steps.  On return r holds -P^-1 (lane's half row), prod the product of the
+// pivots, bad the first non-positive pivot (1-based) or 0.  rowb: 64 doubles.
 // r = 0 on the active lanes as 16 exec-masked v_mov_b64 (a branch): written as plain
 // stores the compiler if-converts the branch into two v_cndmask_b32 per double
 __device__ __forceinline__ void zero_row(double (&r)[16]) {
@@ -1093,206 +789,15 @@ __device__ __forceinline__ void pivot_block_sweep2(const double* __restrict__ C,
     }
 }
 
-// grid (1, B), one wave: steps a-b of sweep step k (see lml_sweep_kernel) -- the
-// 32x32 pivot block of C_k (written by the build kernel for k = 0, by the previous
-// update kernel after) swept in registers, P^-1 to the workspace.  A single wave
-// keeps the whole register file (r02's 1024-thread pivot kernel capped the sweep
-// at 128 VGPRs and spilled its rows to scratch); G = C P^-1 is formed per tile by
-// sw_update_kernel.
-// Gauss-Jordan sweep of the 32x32 pivot block rows k0 .. k0+31 of C (row-major
-// [np][32]) by one wave: lane l + 32 h holds columns [16 h, 16 h + 16) of row l.
-// At step c the pivot row (lanes c and c + 32) goes through the LDS (rowb, 32
-// doubles) and every lane reads the half it needs (broadcast reads; LDS operations
-// of one wave complete in order); a row's column-c entry comes from its other
-// half-lane by a lane permute.  The same arithmetic in the same order as the
-// readlane form (the pivot row, not the symmetric column: eliminating with the
-// column's rounding measured 10-100x less accurate at cond(K) ~ 1e5), 16 FMAs per
-// lane and step.  On return r holds -P^-1 (lane's half row), prod the product of
-// the pivots, bad the first non-positive pivot (1-based) or 0.
-__device__ __forceinline__ void pivot_block_sweep(const double* __restrict__ C, int k0, double* rowb,
-                                                  double (&r)[16], double& prod, int& bad) {
-    const int lane = threadIdx.x & 63;
-    const int l = lane & 31, h = lane >> 5;
-#pragma unroll
-    for (int jj = 0; jj < 16; ++jj) r[jj] = C[(long long)(k0 + l) * kSwNb + 16 * h + jj];
-    prod = 1.0;
-    bad = 0;
-    const double* rowh = rowb + 16 * h;
-#pragma unroll
-    for (int c = 0; c < kSwNb; ++c) {
-        const int hc = c >> 4, jc = c & 15;
-        const double colv = __shfl(r[jc], l + 32 * hc);   // A[l][c], held by the half-lane of column c
-        const bool piv = l == c;
-        if (piv) {
-            // the pivot row goes to the LDS and its registers to zero, so that the
-            // one update form below gives r * ip on the pivot lanes (fma(ip, pj, 0)
-            // rounds the same product) and fma(-t, pj, r) elsewhere -- no per-element
-            // lane select (r02's form spent two v_cndmask per double on it)
-#pragma unroll
-            for (int jj = 0; jj < 16; ++jj) {
-                rowb[16 * h + jj] = r[jj];
-                r[jj] = 0.0;
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const double pv = rowb[c];
-        if (!(pv > 0.0) || !isfinite(pv)) bad = bad ? bad : c + 1;
-        prod *= pv;
-        const double ip = 1.0 / pv;
-        const double t = colv * ip;
-        const double f = piv ? ip : -t;
-        double pj[16];
-#pragma unroll
-        for (int jj = 0; jj < 16; ++jj) pj[jj] = rowh[jj];
-#pragma unroll
-        for (int jj = 0; jj < 16; ++jj) {
-            const double upd = fma(f, pj[jj], r[jj]);
-            if (jj == jc) r[jj] = h == hc ? (piv ? -ip : t) : upd;
-            else r[jj] = upd;
-        }
-        asm volatile("" ::: "memory");
-    }
-}
-
-// grid (1, B), one wave: steps a-b of sweep step k (see lml_sweep_kernel) -- the
-// 32x32 pivot block of C_k (written by the build kernel for k = 0, by the previous
-// update kernel after) swept in registers, P^-1 to the workspace.  A single wave
-// keeps the whole register file (r02's 1024-thread pivot kernel capped the sweep
-// at 128 VGPRs and spilled its rows to scratch); G = C P^-1 is formed per tile by
-// sw_update_kernel.  (MPO_FIT_FUSE=0 path; sw_step_kernel folds it into the update.)
-__global__ __launch_bounds__(64) void sw_pivot_kernel(LmlArgs a, int k) {
-    const int b = blockIdx.y, k0 = k * kSwNb;
-    const SsPtrs p = ss_ptrs(a, b);
-    __shared__ double rowb[2 * kSwNb];     // the sweep's pivot-row broadcast
-    const int lane = threadIdx.x;
-    if (a.stop == 21 || a.stop == 22) return;   // diagnostics only (MPO_FIT_DEBUG)
-    const int l = lane & 31, h = lane >> 5;
-    double r[16], prod;
-    int bad;
-    if (a.pair) pivot_block_sweep2(p.C(k), k0, rowb, r, prod, bad);
-    else pivot_block_sweep(p.C(k), k0, rowb, r, prod, bad);
-#pragma unroll
-    for (int jj = 0; jj < 16; ++jj) p.P[l * kSwNb + 16 * h + jj] = -r[jj];
-    if (lane == 0) {
-        p.acc[0] += log(prod);
-        if (bad && p.acc[1] == 0.0) p.acc[1] = (double)(k0 + bad);
-    }
-}
-
-// grid (nwg, B), kUpdThreads: steps c-d of sweep step k over this workgroup's
-// waves, one lower 16x16 tile (I, J) per wave at a time.  The wave forms its own
-// G_I = C_I P^-1 (16 MFMAs, the MFMA output turned into the A-operand layout
-// through the wave's LDS slice) instead of reading it from a separate G launch:
-// the same MFMA sequence, so the same bits, one launch per step fewer.  The
-// diagonal tile (I, I) also writes G_I into block column k of A (and row I's
-// entries of C_{k+1}); tile (I, I) of block k writes -P^-1 there.
-__global__ __launch_bounds__(kUpdThreads) void sw_update_kernel(LmlArgs a, int k) {
-    const int b = blockIdx.y, np = (int)sw_np(a.n), ntile = np / 16, k0 = k * kSwNb;
-    const SsPtrs p = ss_ptrs(a, b);
-    const double* Cc = p.C(k);
-    __shared__ double gl[kUpdThreads / 64][16 * kSwNb];   // per wave: G_I, A-operand order
-    // C_{k+1} (next block column, rows i, columns k1 .. k1+32) as its entries are
-    // produced: from the lower entries only (the build kernel's copy of C_0 reads
-    // lower storage for both halves of a diagonal tile), so the bits match that copy
-    const int k1 = k0 + kSwNb;
-    double* Cn = k1 < np ? p.C(k + 1) : nullptr;
-    const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
-    const int gw = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kUpdThreads / 64) + wv));
-    const int nw = gridDim.x * (kUpdThreads / 64);
-    const int nt_low = ntile * (ntile + 1) / 2;
-    double* g = gl[wv];
-    for (int t = gw; t < nt_low; t += nw) {
-        int I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-        while (I * (I + 1) / 2 > t) --I;
-        while ((I + 1) * (I + 2) / 2 <= t) ++I;
-        const int J = t - I * (I + 1) / 2;
-        if ((I >> 1) == k) {
-            if (I == J) {   // rows of block k: -P^-1
-#pragma unroll
-                for (int e = lane; e < 16 * kSwNb; e += 64) {
-                    const int i = 16 * I + (e >> 5), c = e & 31;
-                    p.A[(long long)i * np + k0 + c] = -p.P[(i - k0) * kSwNb + c];
-                }
-            }
-            continue;
-        }
-        if ((J >> 1) == k) continue;
-        // G_I = C_I P^-1 (r02's pivot-kernel G phase, per wave)
-        {
-            double av[8], b0[8], b1[8];
-            const double* ar = Cc + (long long)(16 * I + (lane & 15)) * kSwNb + (lane >> 4);
-            const double* br = p.P + (lane >> 4) * kSwNb + (lane & 15);
-#pragma unroll
-            for (int ks = 0; ks < 8; ++ks) {
-                av[ks] = ar[4 * ks];
-                b0[ks] = br[4 * ks * kSwNb];
-                b1[ks] = br[4 * ks * kSwNb + 16];
-            }
-            f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int ks = 0; ks < 8; ++ks) {
-                acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ks], b0[ks], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ks], b1[ks], acc1, 0, 0, 0);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int rr = (lane >> 4) + 4 * q, c0 = lane & 15, c1 = 16 + c0;
-                g[(c0 >> 2) * 64 + rr + 16 * (c0 & 3)] = acc0[q];
-                g[(c1 >> 2) * 64 + rr + 16 * (c1 & 3)] = acc1[q];
-            }
-        }
-        f64x4 acc;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] = p.A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)];
-        double cb[8];
-        const double* cr = Cc + (long long)(16 * J + (lane & 15)) * kSwNb + (lane >> 4);
-#pragma unroll
-        for (int ks = 0; ks < 8; ++ks) cb[ks] = cr[4 * ks];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's G_I stores (LDS ops of one wave complete in order)
-        double ga[8];
-#pragma unroll
-        for (int ks = 0; ks < 8; ++ks) ga[ks] = g[ks * 64 + lane];
-#pragma unroll
-        for (int ks = 0; ks < 8; ++ks)
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-ga[ks], cb[ks], acc, 0, 0, 0);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) p.A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)] = acc[q];
-        if (Cn && ((J >> 1) == k + 1 || (I >> 1) == k + 1)) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int i = 16 * I + (lane >> 4) + 4 * q, j = 16 * J + (lane & 15);
-                if (i < j) continue;                                    // upper half of a diagonal tile
-                if ((j >> 5) == k + 1) Cn[(long long)i * kSwNb + (j - k1)] = acc[q];
-                if ((i >> 5) == k + 1) Cn[(long long)j * kSwNb + (i - k1)] = acc[q];
-            }
-        }
-        if (I == J) {
-            // block column k, rows 16 I .. 16 I + 15, <- G_I (lower storage: below
-            // block k at A[i][j], above it transposed at A[j][i]); a row of block k+1
-            // also gives row j of C_{k+1}
-#pragma unroll
-            for (int e = lane; e < 16 * kSwNb; e += 64) {
-                const int ri = e >> 5, c = e & 31, i = 16 * I + ri, j = k0 + c;
-                const double gv = g[(c >> 2) * 64 + ri + 16 * (c & 3)];
-                if (i > j) p.A[(long long)i * np + j] = gv;
-                else p.A[(long long)j * np + i] = gv;
-                if (Cn && (i >> 5) == k + 1) Cn[(long long)j * kSwNb + (i - k1)] = gv;
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the G_I reads before the next tile's stores
-    }
-}
-
 // grid (nwg, B), kUpdThreads, nwg * 4 >= the lower tile count (one tile per wave):
 // the whole sweep step k in one launch.  Every workgroup sweeps the 32x32 pivot
-// block of C_k itself (wave 0, pivot_block_sweep: the same instructions on the same
+// block of C_k itself (wave 0, pivot_block_sweep2: the same instructions on the same
 // data, so the same P^-1 bits in every workgroup) into its LDS while the other waves
-// load their tile's operands; then each wave forms G_I = C_I P^-1 and updates its
-// tile exactly as sw_update_kernel does.  Replaces the one-wave sw_pivot_kernel
-// launch and the P round trip through global memory; workgroup 0 keeps the log det
-// and the failure column.
-template <bool PAIR>
+// load their tile's operands; then each wave forms its own G_I = C_I P^-1 (16 MFMAs,
+// turned into the A-operand layout through its LDS slice) and updates its tile; the
+// diagonal tile (I, I) also writes G_I into block column k of A (and row I's entries
+// of C_{k+1}), tile (I, I) of block k writes -P^-1 there.  Workgroup 0 keeps the
+// log det and the failure column.
 __global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlArgs a, int k) {
     const int b = blockIdx.y, np = (int)sw_np(a.n), ntile = np / 16, k0 = k * kSwNb;
     const SsPtrs p = ss_ptrs(a, b);
@@ -1342,8 +847,9 @@ __global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlArgs a, int k) 
             bad = 0;
 #pragma unroll
             for (int jj = 0; jj < 16; ++jj) r[jj] = Cc[(long long)(k0 + l) * kSwNb + 16 * h + jj];
-        } else if constexpr (PAIR) pivot_block_sweep2(Cc, k0, rowb, r, prod, bad);
-        else pivot_block_sweep(Cc, k0, rowb, r, prod, bad);
+        } else {
+            pivot_block_sweep2(Cc, k0, rowb, r, prod, bad);
+        }
 #pragma unroll
         for (int jj = 0; jj < 16; ++jj) Pl[l * kSwNb + 16 * h + jj] = -r[jj];
         if (blockIdx.x == 0 && lane == 0) {
@@ -1454,7 +960,7 @@ __global__ __launch_bounds__(256) void sw_alpha_kernel(LmlArgs a) {
 constexpr int kPairGroups = 64;
 
 // grid (kPairGroups, B), 256 threads: pairs i >= j of rows i = gw (mod waves),
-// W_ij dK_ij/dtheta (as lml_sweep_kernel phase 4); one partial per workgroup
+// W_ij dK_ij/dtheta; one partial per workgroup
 template <int DP>
 __global__ __launch_bounds__(256) void sw_pairs_kernel(LmlArgs a, double* __restrict__ partials) {
     __shared__ double red[4][DP + 2];
@@ -1642,11 +1148,11 @@ int launch_split(const LmlArgs& a, int B, hipStream_t s) {
     const int np = (int)sw_np(a.n), nbk = np / kSwNb, ntile = np / 16;
     const int nt_low = ntile * (ntile + 1) / 2;
     const int nwg = std::max(1, (nt_low + 4 * kUpdTilesPerWave - 1) / (4 * kUpdTilesPerWave));
-    // MPO_FIT_FUSE=0: the r03 launch sequence (separate xs / pivot / final kernels)
-    const char* fe = getenv("MPO_FIT_FUSE");
-    const bool fuse = !(fe && fe[0] == '0');
+    // the fused build (sw_xs_build_kernel) and finish (sw_pairs_final_kernel) while
+    // the workgroup's xs rows fit 64 KiB of LDS; past it separate xs / build / pairs
+    // / final launches
     const size_t xs_lds = (size_t)np * DP * sizeof(double);
-    const bool fuse_build = fuse && xs_lds <= 64 * 1024;
+    const bool fuse_build = xs_lds <= 64 * 1024;
     double* partials = a.ws + (long long)B * a.ws_stride;   // [B][kPairGroups][DP + 2]
     if (fuse_build) {
         auto kb = sw_xs_build_kernel<DP>;
@@ -1661,16 +1167,8 @@ int launch_split(const LmlArgs& a, int B, hipStream_t s) {
         MPO_LAUNCH_CHECK();
     }
     for (int k = 0; k < nbk; ++k) {
-        if (fuse) {
-            if (a.pair) hipLaunchKernelGGL(sw_step_kernel<true>, dim3(nwg, B), dim3(kUpdThreads), 0, s, a, k);
-            else hipLaunchKernelGGL(sw_step_kernel<false>, dim3(nwg, B), dim3(kUpdThreads), 0, s, a, k);
-            MPO_LAUNCH_CHECK();
-        } else {
-            hipLaunchKernelGGL(sw_pivot_kernel, dim3(1, B), dim3(64), 0, s, a, k);
-            MPO_LAUNCH_CHECK();
-            hipLaunchKernelGGL(sw_update_kernel, dim3(nwg, B), dim3(kUpdThreads), 0, s, a, k);
-            MPO_LAUNCH_CHECK();
-        }
+        hipLaunchKernelGGL(sw_step_kernel, dim3(nwg, B), dim3(kUpdThreads), 0, s, a, k);
+        MPO_LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(sw_alpha_kernel, dim3(ntile, B), dim3(256), 0, s, a);
     MPO_LAUNCH_CHECK();
@@ -1695,42 +1193,22 @@ inline int fit_dp(int d) {
     return -1;
 }
 
-template <int DP>
-int launch_sweep(const LmlArgs& a, int B, hipStream_t s) {
-    auto kern = lml_sweep_kernel<DP>;
-    const size_t lds = ((size_t)sw_np(a.n) * kSwLd + 2 * kSwNb * kSwLd) * sizeof(double);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3(B), dim3(kFitThreads), lds, s, a);
-    MPO_LAUNCH_CHECK();
-    return MPO_OK;
-}
-
 // which LML kernel: the LDS-packed Cholesky kernel for n <= kSplitMinN (small,
-// latency-bound factors), the split block sweep past it (0.30 / 0.35 / 0.87 ms
-// per launch at n = 200 / 256 / 500 against 0.44 / 0.60 / 2.45 for the
-// single-workgroup sweep and 0.68 for the LDS Cholesky at 200: scripts/fit_probe.py).
-// MPO_FIT_KERNEL = panel / sweep / split forces one.
-constexpr int kSwMinN = 192;
-inline bool use_sweep(int n) {
-    const char* e = getenv("MPO_FIT_KERNEL");
-    if (e && std::string(e) == "panel" && n <= kFitLdsMaxN) return false;
-    if (e && std::string(e) == "sweep" && n <= kSwMaxN) return true;
-    if (e && std::string(e) == "split") return false;
-    return n > kSwMinN && n <= std::min(kSwMaxN, kSplitMinN);
-}
+// latency-bound factors), the split block sweep past it (0.09 vs 0.20 ms at n = 64,
+// 0.30 ms at n = 200 against 0.68 for the Cholesky kernel: scripts/fit_probe.py).
+// MPO_FIT_KERNEL = panel / split forces one (tests: each kernel outside its range).
 // the split sweep: n > kSplitMinN (MPO_FIT_KERNEL=split forces it for n > 16)
 inline bool use_split(int n) {
     const char* e = getenv("MPO_FIT_KERNEL");
     if (e && std::string(e) == "split") return n > 16 && n <= kFitMaxN;
-    if (e && (std::string(e) == "sweep" || std::string(e) == "panel")) return false;
+    if (e && std::string(e) == "panel" && n <= kFitLdsMaxN) return false;
     return n > kSplitMinN;
 }
 
 // the fused split sweep (launch_split's fuse_build): the host-staged call may hand it theta
 // and the outputs in pinned host memory
 inline bool fit_fused_split(int n, int dp) {
-    const char* fe = getenv("MPO_FIT_FUSE");
-    return use_split(n) && !(fe && fe[0] == '0') && (size_t)sw_np(n) * dp * sizeof(double) <= 64 * 1024;
+    return use_split(n) && (size_t)sw_np(n) * dp * sizeof(double) <= 64 * 1024;
 }
 
 template <bool kLds, int DP>
@@ -1749,8 +1227,7 @@ extern "C" {
 
 size_t mpo_gp_lml_ws_bytes(int n, int d, int batch) {
     if (n <= 0 || n > kFitMaxN || fit_dp(d) < 0 || batch <= 0) return 0;
-    const long long per = std::max(std::max(fit_ws_doubles(n, d, n <= kFitLdsMaxN), n <= kSwMaxN ? sw_ws_doubles(n, d) : 0LL),
-                                   ss_ws_doubles(n, d));
+    const long long per = std::max(fit_ws_doubles(n, d, n <= kFitLdsMaxN), ss_ws_doubles(n, d));
     return ((size_t)per * batch + (size_t)batch * kPairGroups * 34) * sizeof(double) + 256;   // + pair partials
 }
 
@@ -1778,15 +1255,10 @@ static int lml_grad_impl(const double* X, const double* y_norm, int n, int d, co
                   ws_bytes, mpo_gp_lml_ws_bytes(n, d, batch));
     const bool use_lds = n <= kFitLdsMaxN;
     const bool split = use_split(n);
-    const bool sweep = !split && use_sweep(n);
     LmlArgs a{X, y_norm, n, d, theta, lml, grad, info,
               reinterpret_cast<double*>(mpo::align_up(reinterpret_cast<uintptr_t>(ws), 256)),
-              split ? ss_ws_doubles(n, d) : sweep ? sw_ws_doubles(n, d) : fit_ws_doubles(n, d, use_lds), 0};
+              split ? ss_ws_doubles(n, d) : fit_ws_doubles(n, d, use_lds), 0};
     if (const char* e = getenv("MPO_FIT_DEBUG")) a.stop = atoi(e);
-    {
-        const char* e = getenv("MPO_FIT_PAIR");
-        a.pair = !(e && e[0] == '0');
-    }
     a.theta_src = split && fit_fused_split(n, dp) ? theta_src : nullptr;
     MPO_CHECK_ARG(!theta_src || a.theta_src, "mpo_gp_lml_grad: a host theta source needs the fused split sweep");
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1798,15 +1270,6 @@ static int lml_grad_impl(const double* X, const double* y_norm, int n, int d, co
             case 12: return launch_split<12>(a, batch, s);
             case 16: return launch_split<16>(a, batch, s);
             default: return launch_split<32>(a, batch, s);
-        }
-    }
-    if (sweep) {
-        switch (dp) {
-            case 4: return launch_sweep<4>(a, batch, s);
-            case 8: return launch_sweep<8>(a, batch, s);
-            case 12: return launch_sweep<12>(a, batch, s);
-            case 16: return launch_sweep<16>(a, batch, s);
-            default: return launch_sweep<32>(a, batch, s);
         }
     }
     if (use_lds) {
@@ -1852,10 +1315,8 @@ int mpo_gp_lml_grad_host(const double* X, const double* y_norm, int n, int d, co
     // Pinned host buffers on the fused split sweep: the first kernel reads theta from
     // the host copy and the last writes lml | grad | info straight into out_host --
     // no copy launches around the round (two of ~20 launches, ~7 us at n = 256).
-    // MPO_FIT_HOSTIO=0 keeps the copies.
     const int dp = fit_dp(d);
-    const char* he = getenv("MPO_FIT_HOSTIO");
-    if (dp > 0 && fit_fused_split(n, dp) && !(he && he[0] == '0')) {
+    if (dp > 0 && fit_fused_split(n, dp)) {
         hipPointerAttribute_t ta{}, oa{};
         if (hipPointerGetAttributes(&ta, theta_host) == hipSuccess && ta.type == hipMemoryTypeHost && ta.devicePointer &&
             hipPointerGetAttributes(&oa, out_host) == hipSuccess && oa.type == hipMemoryTypeHost && oa.devicePointer) {

@@ -1,8 +1,8 @@
 """Time the device GP refit at several n: the LML kernel alone (HIP events, B=3
 thetas per launch, the three L-BFGS-B starts) and a whole skopt refit
 (launches x per-launch + the host L-BFGS-B).  --kernels picks the LML
-kernels compared (MPO_FIT_KERNEL): panel (LDS Cholesky, n <= 200), sweep
-(single-workgroup block sweep, n <= 576), split (multi-workgroup block sweep)."""
+kernels compared (MPO_FIT_KERNEL): panel (LDS Cholesky, n <= 200), split
+(multi-workgroup block sweep)."""
 import argparse
 import os
 import sys
@@ -19,7 +19,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, nargs="+", default=[200, 256, 500])
 ap.add_argument("--d", type=int, default=10)
 ap.add_argument("--reps", type=int, default=2)
-ap.add_argument("--kernels", nargs="+", default=["sweep", "panel"])
+ap.add_argument("--kernels", nargs="+", default=["split", "panel"])
 ap.add_argument("--phases", action="store_true", help="kernel time up to each MPO_FIT_DEBUG stop (1 K, 2 factor, 4 alpha)")
 a = ap.parse_args()
 
@@ -41,9 +41,9 @@ def kernel_ms(dev, T, reps=20):
 for n in a.n:
     X, y = synthetic.gp_problem(n, a.d, 0)
     for kern in a.kernels:
-        if (kern == "panel" and n > 200) or (kern == "sweep" and n > 576):
+        if kern == "panel" and n > 200:
             continue
-        os.environ["MPO_FIT_KERNEL"] = kern   # sweep | panel | split
+        os.environ["MPO_FIT_KERNEL"] = kern   # panel | split
         dev = DeviceLML(X, normalize_targets(y)[0], device="cuda:0")
         T = np.zeros((3, a.d + 2))
         T[1] += 0.5

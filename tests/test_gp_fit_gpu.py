@@ -1,10 +1,9 @@
 """Device GP refit (``mpo_gp_lml_grad`` + the lockstep L-BFGS-B driver) against
 scikit-learn's own outputs (golden ``gp_lml.npz``, made by
 ``tests/golden/make_lml_golden.py``).  n > 48 runs the split block sweep (one
-pivot launch and one many-workgroup update launch per 32-wide block; the
-single-workgroup sweep is the MPO_FIT_KERNEL=sweep variant); n = 256 and 500 are the sizes a
+many-workgroup step launch per 32-wide pivot block); n = 256 and 500 are the sizes a
 256-trial search reaches (real points plus the cl_min lies of a batch ask);
-MPO_FIT_KERNEL=panel / sweep / split re-checks each kernel outside its range."""
+MPO_FIT_KERNEL=panel / split re-checks each kernel outside its range."""
 import os
 import time
 
@@ -25,7 +24,7 @@ SWEEP_MIN_N = 48      # csrc/gp_fit.hip kSplitMinN: above it the split block swe
 
 def _sweep(n):
     k = os.environ.get("MPO_FIT_KERNEL")
-    return k in ("sweep", "split") or (k != "panel" and SWEEP_MIN_N < n)
+    return k == "split" or (k != "panel" and SWEEP_MIN_N < n)
 
 
 def _rel_tol(X, theta):
@@ -74,8 +73,7 @@ def test_batching_does_not_change_results(name):
         assert l1[0] == lml[b] and np.array_equal(g1[0], grad[b])
 
 
-@pytest.mark.parametrize("name,kernel", [("n200_d10", "panel"), ("n130_d6", "panel"), ("n57_d3", "sweep"),
-                                         ("n12_d5", "sweep"), ("n200_d10", "sweep"), ("n256_d10", "sweep")])
+@pytest.mark.parametrize("name,kernel", [("n200_d10", "panel"), ("n130_d6", "panel"), ("n57_d3", "split")])
 def test_other_kernel_still_matches_sklearn(name, kernel, monkeypatch):
     """Each LML kernel outside its default range: the Cholesky kernel at n <= 200,
     the block sweep at small n (one pivot block with identity padding)."""
@@ -89,25 +87,7 @@ def test_split_sweep_at_small_n_matches_sklearn(name, monkeypatch):
     test_lml_and_gradient_match_sklearn(name)
 
 
-@pytest.mark.parametrize("name", ["n230_d4", "n256_d10", "n500_d10"])
-def test_split_sweep_agrees_with_the_single_workgroup_sweep(name, monkeypatch):
-    """The split sweep runs the single-workgroup kernel's sweep arithmetic in the
-    same order (same factor bits); alpha and the gradient pairs are summed in a
-    different fixed order, so the outputs agree to rounding, far inside the
-    sklearn bound."""
-    dev, _ = _lml(name)
-    T = G[name + "_theta"]
-    monkeypatch.setenv("MPO_FIT_KERNEL", "sweep")
-    l1, g1, i1 = dev.evaluate(T)
-    monkeypatch.setenv("MPO_FIT_KERNEL", "split")
-    l2, g2, i2 = dev.evaluate(T)
-    assert np.array_equal(i1, i2)
-    assert np.max(np.abs(l1 - l2) / np.abs(l1)) < 1e-11
-    for b in range(len(T)):
-        assert np.max(np.abs(g1[b] - g2[b])) <= 1e-9 * max(1.0, np.max(np.abs(g1[b])))
-
-
-@pytest.mark.parametrize("kernel", ["sweep", "split"])
+@pytest.mark.parametrize("kernel", ["split"])
 def test_non_finite_theta_reports_failure_in_sweeps(kernel, monkeypatch):
     monkeypatch.setenv("MPO_FIT_KERNEL", kernel)
     dev, _ = _lml("n230_d4")
@@ -147,24 +127,7 @@ def test_device_fit_matches_sklearn_fit(name):
     assert np.max(np.abs(theta - ref)) <= 1e-3, (theta, ref)
 
 
-@pytest.mark.parametrize("name", ["n57_d3", "n130_d6", "n230_d4", "n256_d10", "n500_d10"])
-def test_fused_split_sweep_is_bit_identical_to_the_launch_sequence(name, monkeypatch):
-    """r03: sw_step_kernel (every workgroup sweeps the pivot block itself),
-    sw_xs_build_kernel and sw_pairs_final_kernel (last-arriving workgroup sums the
-    partials) reproduce the separate xs / build / pivot / update / pairs / final
-    launches bit for bit; repeated calls re-arm the arrival counter."""
-    dev, _ = _lml(name)
-    T = G[name + "_theta"]
-    monkeypatch.setenv("MPO_FIT_FUSE", "0")
-    l0, g0, i0 = dev.evaluate(T)
-    monkeypatch.setenv("MPO_FIT_FUSE", "1")
-    for _ in range(3):
-        l1, g1, i1 = dev.evaluate(T)
-        assert np.array_equal(i0, i1) and np.array_equal(l0, l1) and np.array_equal(g0, g1)
-
-
-def test_fused_split_sweep_reports_failure(monkeypatch):
-    monkeypatch.setenv("MPO_FIT_FUSE", "1")
+def test_fused_split_sweep_reports_failure():
     dev, _ = _lml("n230_d4")
     T = G["n230_d4_theta"][:3].copy()
     T[1, 0] = np.nan
@@ -175,33 +138,14 @@ def test_fused_split_sweep_reports_failure(monkeypatch):
     assert l2[0] == lml[2] and np.array_equal(g2[0], grad[2])
 
 
-@pytest.mark.parametrize("fuse", ["0", "1"])
-@pytest.mark.parametrize("name", ["n57_d3", "n130_d6", "n230_d4", "n256_d10", "n500_d10"])
-def test_paired_pivot_sweep_is_bit_identical(name, fuse, monkeypatch):
-    """r03: pivot_block_sweep2 (two sweep steps per LDS broadcast round, every lane
-    forming row c + 1 after step c and its own column-(c+1) entry itself) runs the
-    one-step sweep's operations on the same operands: the same bits (MPO_FIT_PAIR=0
-    is the one-step sweep), in both the fused and the launch-sequence forms."""
-    monkeypatch.setenv("MPO_FIT_FUSE", fuse)
-    dev, _ = _lml(name)
-    T = G[name + "_theta"]
-    monkeypatch.setenv("MPO_FIT_PAIR", "0")
-    l0, g0, i0 = dev.evaluate(T)
-    monkeypatch.setenv("MPO_FIT_PAIR", "1")
-    l1, g1, i1 = dev.evaluate(T)
-    assert np.array_equal(i0, i1) and np.array_equal(l0, l1) and np.array_equal(g0, g1)
-
-
 @pytest.mark.parametrize("name", ["n130_d6", "n500_d10"])
-def test_host_staged_direct_io_is_bit_identical(name, monkeypatch):
-    """r03: on the fused split sweep the host-staged call hands the kernels theta and
-    the output rows in pinned host memory (no copy launches); MPO_FIT_HOSTIO=0 keeps
-    the copies.  Same bits, repeated calls included, and a failed theta still reports."""
+def test_repeated_host_staged_calls_are_bit_identical(name):
+    """The host-staged call (theta and the output rows in pinned host memory, the
+    arrival counter of the last-workgroup sum re-armed per call): repeated calls
+    give the same bits, and a failed theta still reports."""
     dev, _ = _lml(name)
     T = G[name + "_theta"]
-    monkeypatch.setenv("MPO_FIT_HOSTIO", "0")
     l0, g0, i0 = dev.evaluate(T)
-    monkeypatch.setenv("MPO_FIT_HOSTIO", "1")
     for _ in range(3):
         l1, g1, i1 = dev.evaluate(T)
         assert np.array_equal(i0, i1) and np.array_equal(l0, l1) and np.array_equal(g0, g1)
