@@ -38,6 +38,7 @@
 #include <cstdlib>
 #include <memory>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 namespace {
@@ -477,66 +478,93 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
     auto advance = [&](int& ky, int& kx, int& cb) {
         if (++cb == CB) { cb = 0; if (++kx == ux1) { kx = ux0; ++ky; } }
     };
-    // A fragments of a group: 4 k-steps x 4 tiles, read from the LDS image one group
-    // ahead of their MFMAs (like the B fragments), so no MFMA waits on its own reads
-    auto readA = [&](int ky, int kx, int cb, float (&av)[4][4]) {
-        const int coff = cb * 16 + krow;
+    // A fragments of a group (4 k-steps x the wave's tiles) are read from the LDS image
+    // one group ahead of their MFMAs (like the B fragments), so no MFMA waits on its own reads
+    // The group loop, compiled per tile count TPW (the wave's tiles 0..TPW-1 all exist):
+    // a group whose tap is live for every tile of the wave and whose channel block is
+    // full (the common case away from the image border) runs its 4 x TPW x NT MFMAs
+    // straight, with no per-MFMA branch; only border groups take the guarded path.
+    // The MFMA sequence per accumulator is the same on both paths (same bits).
+    auto run = [&](auto tpw_c) {
+        constexpr int TPW = decltype(tpw_c)::value;
+        auto readA = [&](int ky, int kx, int cb, float (&av)[4][4]) {
+            const int coff = cb * 16 + krow;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int ry = py[i] + ky, cx = px[i] + kx;
-            const int base = ((unsigned)ry < (unsigned)rows && (unsigned)cx < (unsigned)H2)
-                                 ? ry * RS + cx * Fp + coff : zoff + krow;   // halo -> zero block
+            for (int i = 0; i < TPW; ++i) {
+                const int ry = py[i] + ky, cx = px[i] + kx;
+                const int base = ((unsigned)ry < (unsigned)rows && (unsigned)cx < (unsigned)H2)
+                                     ? ry * RS + cx * Fp + coff : zoff + krow;   // halo -> zero block
 #pragma unroll
-            for (int u = 0; u < 4; ++u) av[u][i] = img[base + u * 4];
-        }
-    };
-    auto compute = [&](int ky, int kx, int cb, const float (&av)[4][4], const float (&bw)[4][NT]) {
-        bool live[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            live[i] = has[i] && ky >= kylo[i] && ky < kyhi[i] && kx >= kxlo[i] && kx < kxhi[i];
-        const int nu = min(4, (F4 - cb * 16) >> 2);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (u >= nu) break;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                if (!live[i]) continue;
-#pragma unroll
-                for (int j = 0; j < NT; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][i], bw[u][j], acc[i][j], 0, 0, 0);
+                for (int u = 0; u < 4; ++u) av[u][i] = img[base + u * 4];
             }
+        };
+        auto compute = [&](int ky, int kx, int cb, const float (&av)[4][4], const float (&bw)[4][NT]) {
+            bool live[4];
+            bool all = (F4 - cb * 16) >= 16;
+#pragma unroll
+            for (int i = 0; i < TPW; ++i) {
+                live[i] = ky >= kylo[i] && ky < kyhi[i] && kx >= kxlo[i] && kx < kxhi[i];
+                all = all && live[i];
+            }
+            if (all) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int i = 0; i < TPW; ++i)
+#pragma unroll
+                        for (int j = 0; j < NT; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][i], bw[u][j], acc[i][j], 0, 0, 0);
+                return;
+            }
+            const int nu = min(4, (F4 - cb * 16) >> 2);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (u >= nu) break;
+#pragma unroll
+                for (int i = 0; i < TPW; ++i) {
+                    if (!live[i]) continue;
+#pragma unroll
+                    for (int j = 0; j < NT; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][i], bw[u][j], acc[i][j], 0, 0, 0);
+                }
+            }
+        };
+        float b0[4][NT], b1[4][NT], a0[4][4], a1[4][4];
+        int cky = uy0, ckx = ux0, ccb = 0;   // group g
+        int nky = uy0, nkx = ux0, ncb = 0;   // group g + 1
+        if (ngroups) {
+            load_group(cky, ckx, ccb, b0);
+            readA(cky, ckx, ccb, a0);
+            advance(nky, nkx, ncb);
+        }
+        for (int g = 0; g < ngroups; g += 2) {
+            if (g + 1 < ngroups) {
+                load_group(nky, nkx, ncb, b1);
+                readA(nky, nkx, ncb, a1);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            compute(cky, ckx, ccb, a0, b0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (g + 1 >= ngroups) break;
+            cky = nky; ckx = nkx; ccb = ncb;
+            advance(nky, nkx, ncb);
+            if (g + 2 < ngroups) {
+                load_group(nky, nkx, ncb, b0);
+                readA(nky, nkx, ncb, a0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            compute(cky, ckx, ccb, a1, b1);
+            __builtin_amdgcn_sched_barrier(0);
+            cky = nky; ckx = nkx; ccb = ncb;
+            advance(nky, nkx, ncb);
         }
     };
-    float b0[4][NT], b1[4][NT], a0[4][4], a1[4][4];
-    int cky = uy0, ckx = ux0, ccb = 0;   // group g
-    int nky = uy0, nkx = ux0, ncb = 0;   // group g + 1
-    if (ngroups) {
-        load_group(cky, ckx, ccb, b0);
-        readA(cky, ckx, ccb, a0);
-        advance(nky, nkx, ncb);
-    }
-    for (int g = 0; g < ngroups; g += 2) {
-        if (g + 1 < ngroups) {
-            load_group(nky, nkx, ncb, b1);
-            readA(nky, nkx, ncb, a1);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        compute(cky, ckx, ccb, a0, b0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (g + 1 >= ngroups) break;
-        cky = nky; ckx = nkx; ccb = ncb;
-        advance(nky, nkx, ncb);
-        if (g + 2 < ngroups) {
-            load_group(nky, nkx, ncb, b0);
-            readA(nky, nkx, ncb, a0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        compute(cky, ckx, ccb, a1, b1);
-        __builtin_amdgcn_sched_barrier(0);
-        cky = nky; ckx = nkx; ccb = ncb;
-        advance(nky, nkx, ncb);
-    }
+    // this wave's tile count: tiles [wave * per, min(T, wave * per + per))
+    const int mine = __builtin_amdgcn_readfirstlane(max(0, min(per, T - wave * per)));
+    if (mine >= 4) run(std::integral_constant<int, 4>{});
+    else if (mine == 3) run(std::integral_constant<int, 3>{});
+    else if (mine == 2) run(std::integral_constant<int, 2>{});
+    else if (mine == 1) run(std::integral_constant<int, 1>{});
 
     // ---- epilogue: accumulator row p = krow*4 + r is tile pixel (p>>2, p&3)
 #pragma unroll
