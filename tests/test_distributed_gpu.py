@@ -150,3 +150,67 @@ def test_sharded_optimizer_scoring_matches_single_gpu():
     assert dist_out[1] == [list(b) for b in batch]
     opt.tell(list(batch[0]), 0.5)
     assert dist_out[2] == list(opt.ask())
+
+
+def _search_args(workers):
+    from mpi_opt_amd import search
+
+    return search.make_parser().parse_args(
+        ["--world-size", "13", "--block-size", "2", "--n-fold", "2", "--num-iterations", "18", "--epochs", "1",
+         "--n-samples", "1000", "--chain-workers", str(workers)])
+
+
+def _search_worker(rank, world, port, tmp, q):
+    import random
+
+    import torch.distributed as dist
+
+    from mpi_opt_amd import search
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK="0")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    random.seed(11)
+    args = _search_args(2)
+    args.checkpoint = os.path.join(tmp, f"d{rank}.pkl")
+    rep = search.run_search(args)
+    if rank == 0:
+        q.put({k: rep[k] for k in ("told_params", "told_foms", "trained_params", "populations")} |
+              {"refits": rep["gp"]["refits"]})
+    else:
+        q.put("served")
+    dist.destroy_process_group()
+
+
+def test_search_with_chains_over_two_ranks_matches_one_process(tmp_path):
+    """The search CLI's distributed path with the GP in the loop: 2 gloo ranks on
+    cuda:0 train LPT shards of each population and run LPT shares of its cl_min
+    ask batches (DistributedChainExecutor over 2 worker threads per rank); the told
+    points, FOMs, trained trials and refit count equal one process asking inline."""
+    import random
+
+    import torch.multiprocessing as mp
+
+    from mpi_opt_amd import optimizer as O
+    from mpi_opt_amd import search
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_search_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=280) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    dist_out = next(g for g in got if g != "served")
+    random.seed(11)
+    args = _search_args(0)
+    args.checkpoint = str(tmp_path / "s.pkl")
+    O.reset_stats()
+    rep = search.run_search(args)
+    assert dist_out["populations"] == rep["populations"] == [6, 6, 6]
+    assert dist_out["told_params"] == rep["told_params"] and dist_out["told_foms"] == rep["told_foms"]
+    assert dist_out["trained_params"] == rep["trained_params"]
+    assert dist_out["refits"] == rep["gp"]["refits"]
