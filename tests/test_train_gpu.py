@@ -22,6 +22,15 @@ MEMBERS = [
 ]
 N_SAMPLES, N_FOLD, BATCH = 500, 5, 100
 
+# ((F, k, p, dense, lr, dropout, fold), loss, optimizer): the mpi_learn --loss /
+# --optimizer choices beside the reference's binary_crossentropy + adam
+OPTION_MEMBERS = [
+    ((12, 3, 2, 64, 1e-3, 0.25, 0), "categorical_crossentropy", "adam"),
+    ((20, 5, 3, 80, 5e-2, 0.1, 1), "binary_crossentropy", "sgd"),
+    ((33, 4, 2, 100, 5e-2, 0.25, 2), "categorical_crossentropy", "sgd"),
+    ((17, 2, 4, 50, 2e-3, 0.5, 3), "binary_crossentropy", "adam"),
+]
+
 
 def dataset(seed=0):
     rng = np.random.RandomState(seed)
