@@ -428,7 +428,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
     // contiguous tiles per wave (neighbours along a band share most live taps, so the
     // wave's union tap rectangle wastes fewer groups than a round-robin spread)
     const int per = (T + 3) >> 2;
-    int py[4], px[4], kylo[4], kyhi[4], kxlo[4], kxhi[4];
+    int py[4], px[4], pbase[4], kylo[4], kyhi[4], kxlo[4], kxhi[4];
     bool has[4];
     int uy0 = k, uy1 = 0, ux0 = k, ux1 = 0;
     const int dy = (lane & 15) >> 2, dx = lane & 3;
@@ -452,6 +452,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
         const bool pix = y < ty1 && x < tx1;
         py[i] = pix ? y - pad - gy_lo : -(1 << 20);   // an invalid output pixel never reads the image
         px[i] = x - pad;
+        pbase[i] = pix ? py[i] * RS + px[i] * Fp + krow : 0;   // + the tap's offset when in range
     }
     f32x4 acc[4][NT];
 #pragma unroll
@@ -468,7 +469,9 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
     constexpr int N16 = NT * 16;
     auto load_group = [&](int ky, int kx, int cb, float (&dst)[4][NT]) {
         // w2t is [k*k][F4][N16], zero padded (+16 rows of slack): no bounds select,
-        // so the loads stay in flight until the MFMAs of the group consume them
+        // so the loads stay in flight until the MFMAs of the group consume them.  The
+        // prefetch past the last group (ky = uy1 <= k) is clamped into the array.
+        ky = min(ky, k - 1);
         const float* src = W + ((long long)(a.debug == 4 ? (cb & 1) * 16 : (ky * k + kx) * F4 + cb * 16) + krow) * N16 + kcol;
 #pragma unroll
         for (int u = 0; u < 4; ++u)
@@ -488,12 +491,11 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
     auto run = [&](auto tpw_c) {
         constexpr int TPW = decltype(tpw_c)::value;
         auto readA = [&](int ky, int kx, int cb, float (&av)[4][4]) {
-            const int coff = cb * 16 + krow;
+            const int toff = ky * RS + kx * Fp + cb * 16;   // wave-uniform
 #pragma unroll
             for (int i = 0; i < TPW; ++i) {
-                const int ry = py[i] + ky, cx = px[i] + kx;
-                const int base = ((unsigned)ry < (unsigned)rows && (unsigned)cx < (unsigned)H2)
-                                     ? ry * RS + cx * Fp + coff : zoff + krow;   // halo -> zero block
+                const int base = ((unsigned)(py[i] + ky) < (unsigned)rows && (unsigned)(px[i] + kx) < (unsigned)H2)
+                                     ? pbase[i] + toff : zoff + krow;   // halo -> zero block
 #pragma unroll
                 for (int u = 0; u < 4; ++u) av[u][i] = img[base + u * 4];
             }
@@ -537,21 +539,20 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
             readA(cky, ckx, ccb, a0);
             advance(nky, nkx, ncb);
         }
+        // the prefetch of group g + 1 is unconditional (past the end it reads clamped
+        // weights and halo zeros, never used): every path into a group's MFMAs then has
+        // the same loads in flight, and the compiler's vmcnt waits stay one group ahead
         for (int g = 0; g < ngroups; g += 2) {
-            if (g + 1 < ngroups) {
-                load_group(nky, nkx, ncb, b1);
-                readA(nky, nkx, ncb, a1);
-            }
+            load_group(nky, nkx, ncb, b1);
+            readA(nky, nkx, ncb, a1);
             __builtin_amdgcn_sched_barrier(0);
             compute(cky, ckx, ccb, a0, b0);
             __builtin_amdgcn_sched_barrier(0);
             if (g + 1 >= ngroups) break;
             cky = nky; ckx = nkx; ccb = ncb;
             advance(nky, nkx, ncb);
-            if (g + 2 < ngroups) {
-                load_group(nky, nkx, ncb, b0);
-                readA(nky, nkx, ncb, a0);
-            }
+            load_group(nky, nkx, ncb, b0);
+            readA(nky, nkx, ncb, a0);
             __builtin_amdgcn_sched_barrier(0);
             compute(cky, ckx, ccb, a1, b1);
             __builtin_amdgcn_sched_barrier(0);
