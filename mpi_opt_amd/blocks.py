@@ -243,6 +243,7 @@ class PopulationComm:
         # per population: (seconds since the previous population finished, seconds waiting for
         # its lazy ask batches, seconds training it, trials) -- the search's timeline
         self.timeline = []
+        self.on_population = None   # optional callback(index, timeline entry) after each population
         import time
 
         self._t_last = time.perf_counter()
@@ -289,6 +290,8 @@ class PopulationComm:
         t2 = time.perf_counter()
         self.timeline.append((t0 - self._t_last, t1 - t0, t2 - t1, len(params)))
         self._t_last = t2
+        if self.on_population is not None:
+            self.on_population(len(self.timeline) - 1, self.timeline[-1])
         self.batches.append(len(params))
         self.trained_params.extend(params)
         for b, f in zip(blocks, foms):

@@ -170,6 +170,14 @@ def run_search(args, x=None, y=None, log=print, progress=None):
                     chains.close()
             return None
     comm = PopulationComm(num_blocks, args.block_size, evaluator)
+
+    def _population_done(i, entry):
+        from . import optimizer as _o
+
+        log(f"population {i}: {entry[3]} trials; {entry[0]:.1f} s before it, {entry[1]:.1f} s waiting for ask "
+            f"batches, {entry[2]:.1f} s training; {_o.STATS['refits']} refits so far")
+
+    comm.on_population = _population_done
     opt_kw = {"device": dev, "acq_optimizer_kwargs": {"n_points": args.ei_candidates}}
     if chains is not None:
         opt_kw["chain_executor"] = chains                 # ask batches run concurrently (mpi_opt_amd.chains)

@@ -34,9 +34,11 @@ def members_of(params):
     return out
 
 
-def run(variant, pops, x, y, steps=60, evals=10):
+def run(variant, pops, x, y, steps=60, evals=10, profile=False):
     # a variant is "base" or MPO_POP_PLAN's "key=value,..." (planner overrides, csrc/cnn.hip plan_knob)
     env = {} if variant == "base" else {"MPO_POP_PLAN": variant}
+    if profile:
+        env["MPO_POP_PROFILE"] = "1"   # per-launch HIP events (adds a little host time per step)
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     res = []
@@ -60,6 +62,14 @@ def run(variant, pops, x, y, steps=60, evals=10):
             torch.cuda.synchronize()
             t2 = time.perf_counter()
             res.append(((t1 - t0) / steps * 1e3, (t2 - t1) / evals * 1e3, float(eng.loss.mean())))
+            if profile:
+                prof = eng.profile(reset=True)
+                groups = {}
+                for k, ms in prof.items():
+                    groups[k.split("/")[0]] = groups.get(k.split("/")[0], 0.0) + ms / (steps + evals + 3)
+                print(f"   {variant} population of {len(members)} members, device ms per step: "
+                      + "  ".join(f"{k}={v:.3f}" for k, v in sorted(groups.items(), key=lambda kv: -kv[1])),
+                      flush=True)
             del eng
     finally:
         for k, v in old.items():
@@ -76,6 +86,8 @@ def main():
     for p in pops:
         print("population", [[round(float(v), 3) for v in q] for q in p], flush=True)
     variants = sys.argv[1:] or ["base"]
+    for v in variants:
+        run(v, pops, x, y, steps=20, evals=5, profile=True)
     for rep in range(2):
         for v in variants:
             res = run(v, pops, x, y)
