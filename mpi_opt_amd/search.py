@@ -102,7 +102,7 @@ def block_layout(world_size, block_size):
     return divmod(world_size - 1, block_size)
 
 
-def run_search(args, x=None, y=None, log=print, progress=None):
+def run_search(args, x=None, y=None, log=print, progress=None, on_population=None):
     """Run the option3 search for parsed ``args``; returns a report dict (rank 0)
     or None (ranks > 0, which serve their shards until rank 0 is done).
 
@@ -176,6 +176,8 @@ def run_search(args, x=None, y=None, log=print, progress=None):
 
         log(f"population {i}: {entry[3]} trials; {entry[0]:.1f} s before it, {entry[1]:.1f} s waiting for ask "
             f"batches, {entry[2]:.1f} s training; {_o.STATS['refits']} refits so far")
+        if on_population is not None:
+            on_population(i, entry, dict(_o.STATS))
 
     comm.on_population = _population_done
     opt_kw = {"device": dev, "acq_optimizer_kwargs": {"n_points": args.ei_candidates}}

@@ -26,10 +26,21 @@ def main():
     def log(*m):
         print(f"[{time.perf_counter() - t0:7.1f} s]", *m, file=sys.stderr, flush=True)
 
+    partial = {"argv": argv, "populations": []}
+
+    def population_done(i, entry, stats):
+        # a partial report after every population (a run cut short still leaves its timeline)
+        partial["populations"].append({"index": i, "trials": entry[3], "before_s": entry[0], "wait_s": entry[1],
+                                       "train_s": entry[2], "t_s": time.perf_counter() - t0,
+                                       "refits": stats["refits"], "refit_n_sum": stats["n_sum"],
+                                       "refit_s": stats["refit_s"], "propose_s": stats["propose_s"]})
+        with open(out_path + ".partial", "w") as fh:
+            json.dump(partial, fh, indent=1, default=float)
+
     with tempfile.TemporaryDirectory() as tmp:
         if args.checkpoint == "coordinator.pkl":
             args.checkpoint = os.path.join(tmp, "coordinator.pkl")
-        rep = search.run_search(args, log=log, progress=log)
+        rep = search.run_search(args, log=log, progress=log, on_population=population_done)
     if rep is None:
         return 0
     rep["argv"] = argv
