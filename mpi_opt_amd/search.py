@@ -73,8 +73,9 @@ def make_parser():
     p.add_argument("--chain-workers", type=int, default=4,
                    help="concurrent cl_min ask batches per GPU (worker threads, one HIP stream each); "
                         "0 runs every ask inline, as the reference's Coordinator does")
-    p.add_argument("--chain-processes", action="store_true",
-                   help="run the concurrent ask batches in spawned worker processes instead of threads")
+    p.add_argument("--chain-processes", type=int, default=0,
+                   help="spawned chain worker processes per GPU, each running --chain-workers batches at "
+                        "a time (0: worker threads in this process)")
     return p
 
 
@@ -156,8 +157,10 @@ def run_search(args, x=None, y=None, log=print, progress=None, on_population=Non
     local_eval = evaluator
     chains = None
     if args.chain_workers > 0:
-        pool = ProcessChainExecutor if args.chain_processes else ThreadChainExecutor
-        chains = pool(dev, workers=args.chain_workers)
+        if args.chain_processes > 0:
+            chains = ProcessChainExecutor(dev, workers=args.chain_processes, threads=args.chain_workers)
+        else:
+            chains = ThreadChainExecutor(dev, workers=args.chain_workers)
     if dist is not None:
         evaluator = DistributedEvaluator(evaluator)
         if chains is not None:
@@ -218,7 +221,8 @@ def run_search(args, x=None, y=None, log=print, progress=None, on_population=Non
         "optimizer_s": tm["ask_s"] + tm["tell_s"] + chain_wait,
         "ask_s": tm["ask_s"], "tell_s": tm["tell_s"], "asks": tm["asks"], "tells": tm["tells"],
         "chain_wait_s": chain_wait, "chain_workers": args.chain_workers,
-        "chain_pool": ("processes" if args.chain_processes else "threads") if chains is not None else None,
+        "chain_pool": (f"{args.chain_processes} processes x {args.chain_workers} threads" if args.chain_processes
+                       else f"{args.chain_workers} threads") if chains is not None else None,
         "chain_busy_s": chains.busy_s if chains is not None else 0.0,
         "train_s": local_eval.train_s,
         # headline on TOLD trials (the ones the optimizer saw); the in-flight tail the

@@ -215,10 +215,11 @@ def test_lazy_process_search_equals_sequential(fake_gp, tmp_path, monkeypatch):
     random.seed(5)
     want = _search(str(tmp_path))
     monkeypatch.setattr(chains, "_process_init", _patched_process_init)
-    ex = ProcessChainExecutor(device=None, workers=2)
-    try:
-        random.seed(5)
-        got = _search(str(tmp_path), ex)
-    finally:
-        ex.close()
-    assert got == want
+    for workers, threads in ((2, 1), (2, 3)):
+        ex = ProcessChainExecutor(device=None, workers=workers, threads=threads)
+        try:
+            random.seed(5)
+            got = _search(str(tmp_path), ex)
+        finally:
+            ex.close()
+        assert got == want, (workers, threads)
