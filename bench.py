@@ -96,14 +96,17 @@ def _kernel_family(name):
     return n.split("(", 1)[0]
 
 
-def _per_kernel_bytes(rows_f, rows_w, match, steps, top=12):
-    """HBM bytes per step by kernel instance (FETCH_SIZE x 2 + WRITE_SIZE), largest first."""
+def _per_kernel_bytes(rows_f, rows_w, match, steps, top=12, family=False):
+    """HBM bytes per step by kernel instance (FETCH_SIZE x 2 + WRITE_SIZE), largest
+    first; ``family`` sums the template instances of a kernel (all of them, no top cut)."""
     by = collections.defaultdict(float)
     for rows, counter, mult in ((rows_f, "FETCH_SIZE", 2.0), (rows_w, "WRITE_SIZE", 1.0)):
         for r in rows:
             if r["Counter_Name"] == counter and match(r["Kernel_Name"]):
-                by[_kernel_family(r["Kernel_Name"])] += mult * 1024.0 * float(r["Counter_Value"]) / steps
-    return dict(sorted(by.items(), key=lambda kv: -kv[1])[:top])
+                name = _kernel_family(r["Kernel_Name"])
+                by[name.split("<", 1)[0] if family else name] += mult * 1024.0 * float(r["Counter_Value"]) / steps
+    items = sorted(by.items(), key=lambda kv: -kv[1])
+    return dict(items if family else items[:top])
 
 
 def live_pmc(train_trials):
@@ -140,6 +143,7 @@ def live_pmc(train_trials):
         f = _per_dispatch(rf, "FETCH_SIZE", ours)
         w = _per_dispatch(rw, "WRITE_SIZE", ours)
         per_kernel = _per_kernel_bytes(rf, rw, ours, steps)
+        per_family = _per_kernel_bytes(rf, rw, ours, steps, family=True)
         fetch = 1024.0 * sum(f.values()) / steps
         write = 1024.0 * sum(w.values()) / steps
         rows = pmc_pass(["SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"], tr_prog)
@@ -153,7 +157,8 @@ def live_pmc(train_trials):
                 den += gui / 8 * 1024
         out["train"] = {"hbm_bytes_per_train_batch": 2.0 * fetch + write, "fetch_size_bytes_raw": fetch,
                         "write_size_bytes": write, "mfma_busy": num / den if den else None,
-                        "per_kernel_mfma_busy": per, "per_kernel_hbm_bytes": per_kernel}
+                        "per_kernel_mfma_busy": per, "per_kernel_hbm_bytes": per_kernel,
+                        "per_family_hbm_bytes": per_family}
     except Exception as e:  # noqa: BLE001
         out["errors"].append(f"train: {e}")
     # DenseNet (configs[4]): 2 warmup + 3 train steps of the 32-member population
@@ -167,7 +172,8 @@ def live_pmc(train_trials):
         write = 1024.0 * sum(w.values()) / 5
         out["densenet"] = {"hbm_bytes_per_train_step": 2.0 * fetch + write, "fetch_size_bytes_raw": fetch,
                            "write_size_bytes": write, "steps": 5,
-                           "per_kernel_hbm_bytes": _per_kernel_bytes(rf, rw, ours, 5)}
+                           "per_kernel_hbm_bytes": _per_kernel_bytes(rf, rw, ours, 5),
+                           "per_family_hbm_bytes": _per_kernel_bytes(rf, rw, ours, 5, family=True)}
     except Exception as e:  # noqa: BLE001
         out["errors"].append(f"densenet: {e}")
     return out
@@ -469,8 +475,20 @@ def bench_train(args, torch, dist, ws, rank, dev):
     flops = (ratio * B * sum(m.flops_per_sample_train() for m in members)
              + B * sum(m.flops_per_sample_fwd() for m in members))
     achieved = flops / (t_gpu / args.train_steps) / 1e12
-    algo_bytes = sum(m.hbm_bytes_train(B) for m in members)          # per train batch
+    # per train batch: the every-tensor-once floor, and each kernel's own minimum
+    # (slabs of the deterministic split-K weight gradients and flip_w2's copies included)
+    floor_bytes = sum(m.hbm_bytes_train(B) for m in members)
+    by_kernel = collections.defaultdict(float)
+    for m in members:
+        for k, v in m.hbm_bytes_train_by_kernel(B).items():
+            by_kernel[k] += v
+    algo_bytes = sum(by_kernel.values())
     pmc = (args.pmc or {}).get("train") if n_trials == 64 else None
+    if pmc and pmc.get("per_family_hbm_bytes"):
+        fam = pmc["per_family_hbm_bytes"]
+        pmc["per_family_vs_model"] = {k: {"measured": fam.get(k, 0.0), "model": v,
+                                          "ratio": fam.get(k, 0.0) / v if v else None}
+                                      for k, v in sorted(by_kernel.items(), key=lambda kv: -fam.get(kv[0], 0.0))}
     return {
         "metric": "MNIST-CNN trials/hour (5-fold CV, 10 epochs, 60k samples/trial-fold split)",
         "value": trials_per_hour, "unit": "trials/hour", "n_gpus": ws, "steps": args.train_steps,
@@ -487,6 +505,9 @@ def bench_train(args, torch, dist, ws, rank, dev):
                      "traffic": pmc["hbm_bytes_per_train_batch"] if pmc else None,
                      "traffic_unit": "HBM bytes per train batch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, this run)",
                      "algorithmic_hbm_bytes_per_train_batch": algo_bytes,
+                     "algorithmic_model": "per-kernel minimum (mpi_opt_amd.population.TrialSpec."
+                                          "hbm_bytes_train_by_kernel)",
+                     "every_tensor_once_hbm_bytes_per_train_batch": floor_bytes,
                      "algorithmic_flops_per_step": flops,
                      "pmc": pmc},
         "_trials": trials,
@@ -518,7 +539,7 @@ def bench_densenet(args, torch, dist, ws, rank, dev):
     CIFAR-10-shape data; each trial trains 10 epochs on the option3 70/30 split of
     50 000 samples (350 train + 150 validation batches of 100 per epoch)."""
     from mpi_opt_amd.densenet import DenseNetArch, DenseNetPopulation, flops_per_sample_fwd, \
-        flops_per_sample_train, hbm_bytes_train, synthetic_cifar
+        flops_per_sample_train, hbm_bytes_train, hbm_bytes_train_by_kernel, synthetic_cifar
     from mpi_opt_amd.population import kfold_split
 
     n_trials, B = args.dn_trials, 100
@@ -569,8 +590,18 @@ def bench_densenet(args, torch, dist, ws, rank, dev):
     trials_per_hour = ws * n_trials * 3600.0 / (t_macro * 50 * 10)
     flops = n_trials * B * (7 * flops_per_sample_train(pop.layers) + 3 * flops_per_sample_fwd(pop.layers))
     achieved = flops / (t_gpu / args.train_steps) / 1e12
-    algo_bytes = n_trials * hbm_bytes_train(pop.layers, B, pop.n_params)      # per train step
+    # per train step: the every-tensor-once lower bound, and each kernel's own minimum
+    # with the passes training-mode BatchNorm needs (statistics before use, reduce
+    # before apply) -- the model the measured traffic is held against
+    floor_bytes = n_trials * hbm_bytes_train(pop.layers, B, pop.n_params)
+    by_kernel = {k: n_trials * v for k, v in hbm_bytes_train_by_kernel(pop.layers, B, pop.n_params).items()}
+    algo_bytes = sum(by_kernel.values())
     pmc = (args.pmc or {}).get("densenet") if n_trials == 32 else None
+    if pmc and pmc.get("per_family_hbm_bytes"):
+        fam = pmc["per_family_hbm_bytes"]
+        pmc["per_family_vs_model"] = {k: {"measured": fam.get(k, 0.0), "model": v,
+                                          "ratio": fam.get(k, 0.0) / v if v else None}
+                                      for k, v in sorted(by_kernel.items(), key=lambda kv: -fam.get(kv[0], 0.0))}
     return {
         "metric": "DenseNet trials/hour (CIFAR-10 shape, 10 epochs, 70/30 split of 50k samples)",
         "value": trials_per_hour, "unit": "trials/hour", "n_gpus": ws, "steps": args.train_steps,
@@ -585,7 +616,10 @@ def bench_densenet(args, torch, dist, ws, rank, dev):
                      "frac": achieved / FP32_PEAK_TFLOPS,
                      "traffic": pmc["hbm_bytes_per_train_step"] if pmc else None,
                      "traffic_unit": "HBM bytes per train step (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, this run)",
-                     "algorithmic_hbm_bytes_per_train_step": algo_bytes, "pmc": pmc,
+                     "algorithmic_hbm_bytes_per_train_step": algo_bytes,
+                     "algorithmic_model": "per-kernel minimum incl. training-mode BatchNorm passes "
+                                          "(mpi_opt_amd.densenet.hbm_bytes_train_by_kernel)",
+                     "every_tensor_once_hbm_bytes_per_train_step": floor_bytes, "pmc": pmc,
                      "algorithmic_flops_per_step": flops},
     }
 

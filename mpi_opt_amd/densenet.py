@@ -17,6 +17,7 @@ averages in evaluation; the figure of merit is the fold's validation loss
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 from dataclasses import dataclass
 
@@ -161,6 +162,59 @@ def hbm_bytes_train(layers, batch, n_params):
             q = (ly["H"] // 2) * (ly["W"] // 2) * ly["cout"]
             per_sample += 2 * (hw * ly["cout"] + q)                    # AvgPool2 forward + backward
     return 4 * (batch * per_sample + 8 * n_params)
+
+
+def hbm_bytes_train_by_kernel(layers, batch, n_params):
+    """Each DenseNet kernel family's own minimal HBM bytes for one train step of one
+    member (f32; the kernels of csrc/densenet.hip as ``enqueue_forward`` /
+    ``enqueue_backward`` launch them, every operand read once and every result
+    written once per launch).  Unlike :func:`hbm_bytes_train` it counts the passes
+    training-mode BatchNormalization needs by its data dependencies: the batch
+    statistics of a site are read before any consumer can normalise (only the new
+    growth channels -- totals carried over), and the backward's (sum dy, sum dy*xhat)
+    reductions precede dx, so the reduce pass reads (dz, x) and the apply pass reads
+    (dz, x[, dcat]) and writes dcat.  Weights, slabs and the per-row statistics are
+    L2-sized and omitted; parameters as in :func:`hbm_bytes_train` (8 passes).
+    Returns {family: bytes} (family = kernel name without template arguments)."""
+    by = collections.defaultdict(float)
+    prev = None
+    for ly in layers:
+        hw, cin, cout = ly["H"] * ly["W"], ly["cin"], ly["cout"]
+        kind = ly["kind"]
+        if kind == "conv0":
+            by["dn_conv_kernel"] += hw * (cin + cout)                 # forward
+            by["dn_wgrad3_kernel"] += hw * (cin + cout)               # backward: x, dOut
+            prev = ly
+            continue
+        c0 = prev["cin"] if (prev is not None and prev["kind"] == "dense" and prev["stage"] == ly["stage"]
+                             and prev["cin"] + prev["cout"] == cin) else 0
+        by["dn_bn_stats_kernel"] += hw * (cin - c0)
+        if kind == "head":
+            by["dn_bn_apply_kernel"] += 2 * hw * cin                  # z stored for the GAP
+            by["dn_head_fwd_kernel"] += hw * cin
+            by["dn_bn_bwd_reduce_kernel"] += hw * cin                 # x (dz is the broadcast GAP gradient)
+            by["dn_bn_bwd_apply_kernel"] += 2 * hw * cin              # x in, dcat out
+            prev = ly
+            continue
+        if kind == "dense":
+            by["dn_conv_kernel"] += hw * (cin + cout)                 # forward: cat in, growth slice out
+            by["dn_wgrad3_kernel"] += hw * (cin + cout)
+            by["dn_conv_kernel"] += hw * (cout + cin)                 # input gradient: dOut in, dz out
+            by["dn_bn_bwd_reduce_kernel"] += 2 * hw * cin             # dz, x
+            by["dn_bn_bwd_apply_kernel"] += 4 * hw * cin              # dz, x, dcat in; dcat out
+        else:                                                         # transition
+            q = (ly["H"] // 2) * (ly["W"] // 2) * cout
+            by["dn_conv_kernel"] += hw * (cin + cout)
+            by["dn_pool_fwd_kernel"] += hw * cout + q
+            by["dn_pool_bwd_kernel"] += q + hw * cout
+            by["dn_wgrad1_kernel"] += hw * (cin + cout)
+            by["dn_conv_kernel"] += hw * (cout + cin)
+            by["dn_bn_bwd_reduce_kernel"] += 2 * hw * cin
+            by["dn_bn_bwd_apply_kernel"] += 3 * hw * cin              # dz, x in; dcat stored
+        prev = ly
+    out = {k: 4.0 * batch * v for k, v in by.items()}
+    out["dn_adam_kernel"] = 4.0 * 8 * n_params
+    return out
 
 
 class DenseNetPopulation:

@@ -94,6 +94,39 @@ class TrialSpec:
         return 4 * (batch * per_sample + 8 * n_params)
 
 
+    def hbm_bytes_train_by_kernel(self, batch, spg=(4, 4)):
+        """Each csrc/cnn.hip kernel family's own minimal HBM bytes for one train step
+        of this member (f32; every operand read once and every result written once
+        per launch, as ``mpo_pop_train_step`` launches them).  Beyond
+        :meth:`hbm_bytes_train` it keeps the traffic the algorithm's kernel split
+        implies: the weight gradients' partial slabs (one per ``spg`` samples,
+        written by the wgrad kernels, read by ``wgrad_reduce``) and ``flip_w2``'s
+        padded / rotated weight copies.  Returns {family: bytes}."""
+        F, D, k = self.nb_filters, self.dense, self.kernel_size
+        g = self.geometry()
+        a1, a2, K1 = g["H1"] ** 2 * F, g["H2"] ** 2 * F, g["K1"]
+        img = IMG * IMG
+        n_params = sum(int(np.prod(s)) for s in self.param_shapes().values())
+        g1, g2 = -(-batch // spg[0]), -(-batch // spg[1])
+        slab1, slab2 = g1 * (k * k + 1) * F, g2 * (k * k * F + 1) * F
+        per = {
+            "conv_img_kernel": batch * ((img + a1) + (a1 + a2)),                   # conv1, conv2 forward
+            "pool_fwd_kernel": batch * (a2 + K1 + K1 / 4),                         # a2 in; pooled + u8 argmax out
+            "dense_kernel": batch * (K1 + 2 * D + D + NUM_CLASSES                  # D1, D2 forward
+                                     + D + NUM_CLASSES + NUM_CLASSES + 2 * D        # D2 wgrad, dgrad (+ gates)
+                                     + K1 + D + D + K1),                            # D1 wgrad, dgrad
+            "softmax_bce_kernel": batch * 2 * NUM_CLASSES,
+            "pool_bwd_kernel": batch * (K1 + K1 / 4 + a2 + a2),                     # dp, argmax, a2 mask in; dz2 out
+            "conv_wgrad_kernel": batch * (a1 + a2) + slab2,                        # a1, dz2 in; slabs out
+            "conv_dgrad_kernel": batch * (a2 + a1 + a1),                           # dz2, a1 mask in; dz1 out
+            "conv1_wgrad_kernel": batch * (img + a1) + slab1,
+            "wgrad_reduce_kernel": slab1 + slab2 + (k * k + 1) * F + (k * k * F + 1) * F,
+            "flip_w2_kernel": 3 * k * k * F * F + k * k * F,                       # w2 (w1) in; padded + rotated out
+            "adam_kernel": 7 * n_params,                                            # p, g, m, v in; p, m, v out
+        }
+        return {name: 4.0 * v for name, v in per.items()}
+
+
 MpoCnnSpec = _lib.MpoCnnSpec
 MpoPopSizes = _lib.MpoPopSizes
 
