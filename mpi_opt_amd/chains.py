@@ -48,6 +48,7 @@ class LazyBatch:
         self._error = None
         self._done = threading.Event()
         self.seq = None             # submission number (executor bookkeeping)
+        self.run_s = None           # seconds the batch ran on its worker
 
     def __len__(self):
         return self.job.n_points
@@ -127,6 +128,7 @@ class ThreadChainExecutor:
         self._seq = 0
         self.busy_s = 0.0           # summed worker seconds spent in chains
         self.wait_s = 0.0           # seconds callers blocked waiting for a batch
+        self.durations = []         # (submission number, seconds) per finished batch
         self._lock = threading.Lock()
         if start:
             for w in range(self.workers):
@@ -154,11 +156,13 @@ class ThreadChainExecutor:
                         stream.synchronize()
                 else:
                     X, trace = batch.job.run(self.device)
+                batch.run_s = time.perf_counter() - t0
                 batch._set(X, trace)
             except BaseException as e:  # noqa: BLE001 -- re-raised by result()
                 batch._set(error=e)
             with self._lock:
                 self.busy_s += time.perf_counter() - t0
+                self.durations.append((batch.seq, batch.run_s))
 
     def submit(self, job):
         b = LazyBatch(self, job)
@@ -232,7 +236,7 @@ def _process_main(init, device, threads, in_q, out_q):
                 except Exception:  # noqa: BLE001 -- an unpicklable error travels as its repr
                     err = RuntimeError(repr(err))
             busy = local.busy_s
-            out_q.put((seq, b._X, b._trace, err, _take_stats(), busy - busy0))
+            out_q.put((seq, b._X, b._trace, err, _take_stats(), busy - busy0, b.run_s))
             busy0 = busy
 
     reporter = threading.Thread(target=report, daemon=True)
@@ -273,6 +277,7 @@ class ProcessChainExecutor:
         self._lock = threading.Lock()
         self.busy_s = 0.0
         self.wait_s = 0.0
+        self.durations = []
         self._collector = threading.Thread(target=self._collect, daemon=True)
         self._collector.start()
 
@@ -295,11 +300,13 @@ class ProcessChainExecutor:
             if msg is None:
                 live -= 1
                 continue
-            seq, X, trace, err, stats, busy = msg
+            seq, X, trace, err, stats, busy, run_s = msg
             O.merge_stats(stats)
             with self._lock:
                 self.busy_s += busy
+                self.durations.append((seq, run_s))
                 b = self._batches.pop(seq)
+            b.run_s = run_s
             b._set(X, trace, err)
 
     def submit(self, job):

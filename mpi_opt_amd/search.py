@@ -224,6 +224,9 @@ def run_search(args, x=None, y=None, log=print, progress=None, on_population=Non
         "chain_pool": (f"{args.chain_processes} processes x {args.chain_workers} threads" if args.chain_processes
                        else f"{args.chain_workers} threads") if chains is not None else None,
         "chain_busy_s": chains.busy_s if chains is not None else 0.0,
+        # seconds each ask batch ran on its worker, in submission order (one per ask)
+        "chain_run_s": [d for _, d in sorted(getattr(chains, "durations", []) or
+                                             getattr(getattr(chains, "local", None), "durations", []))],
         "train_s": local_eval.train_s,
         # headline on TOLD trials (the ones the optimizer saw); the in-flight tail the
         # exit barrier trains (coordinator.py:98-101 never tells it) is reported apart
