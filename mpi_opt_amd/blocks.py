@@ -229,9 +229,14 @@ class _Request:
 class PopulationComm:
     """MPI-communicator stand-in for :class:`Coordinator` (size = 1 + blocks x block_size)."""
 
-    def __init__(self, num_blocks, block_size, evaluator, train_tail=True):
+    def __init__(self, num_blocks, block_size, evaluator, train_tail=True, chunks=1):
         self.num_blocks, self.block_size, self.evaluator = num_blocks, block_size, evaluator
         self.train_tail = train_tail
+        # chunks > 1: a population trains in that many parts, each as soon as its own
+        # lazy ask batches resolve, so the later batches run while the earlier parts
+        # train.  A member's training does not depend on its population (bit-identical
+        # alone or in any population), so FOMs, tells and asks are unchanged.
+        self.chunks = max(1, int(chunks))
         self.received = {}       # rank -> last params
         self.pending = {}        # block -> params launched, not yet trained
         self.results = {}        # block -> fom
@@ -284,11 +289,20 @@ class PopulationComm:
 
         t0 = time.perf_counter()
         blocks = sorted(self.pending)
-        params = resolve_all([self.pending.pop(b) for b in blocks])
-        t1 = time.perf_counter()
-        foms = self.evaluator.evaluate(params)
+        points = [self.pending.pop(b) for b in blocks]
+        k = min(self.chunks, len(points))
+        cuts = [len(points) * i // k for i in range(k + 1)]
+        params, foms, wait = [], [], 0.0
+        for c0, c1 in zip(cuts[:-1], cuts[1:]):
+            # block order is the order the ask batches were submitted in
+            tw = time.perf_counter()
+            part = resolve_all(points[c0:c1])
+            wait += time.perf_counter() - tw
+            params.extend(part)
+            foms.extend(self.evaluator.evaluate(part))
         t2 = time.perf_counter()
-        self.timeline.append((t0 - self._t_last, t1 - t0, t2 - t1, len(params)))
+        t1 = t0 + wait
+        self.timeline.append((t0 - self._t_last, wait, t2 - t1, len(params)))
         self._t_last = t2
         if self.on_population is not None:
             self.on_population(len(self.timeline) - 1, self.timeline[-1])

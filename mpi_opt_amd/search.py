@@ -73,6 +73,9 @@ def make_parser():
     p.add_argument("--chain-workers", type=int, default=4,
                    help="concurrent cl_min ask batches per GPU (worker threads, one HIP stream each); "
                         "0 runs every ask inline, as the reference's Coordinator does")
+    p.add_argument("--population-chunks", type=int, default=1, dest="population_chunks",
+                   help="train each population in this many parts, each as soon as its ask batches "
+                        "resolve (overlaps the remaining batches with training; results unchanged)")
     p.add_argument("--chain-processes", type=int, default=0,
                    help="spawned chain worker processes per GPU, each running --chain-workers batches at "
                         "a time (0: worker threads in this process)")
@@ -172,7 +175,7 @@ def run_search(args, x=None, y=None, log=print, progress=None, on_population=Non
                 if chains is not None:
                     chains.close()
             return None
-    comm = PopulationComm(num_blocks, args.block_size, evaluator)
+    comm = PopulationComm(num_blocks, args.block_size, evaluator, chunks=args.population_chunks)
 
     def _population_done(i, entry):
         from . import optimizer as _o
@@ -221,6 +224,7 @@ def run_search(args, x=None, y=None, log=print, progress=None, on_population=Non
         "optimizer_s": tm["ask_s"] + tm["tell_s"] + chain_wait,
         "ask_s": tm["ask_s"], "tell_s": tm["tell_s"], "asks": tm["asks"], "tells": tm["tells"],
         "chain_wait_s": chain_wait, "chain_workers": args.chain_workers,
+        "population_chunks": args.population_chunks,
         "chain_pool": (f"{args.chain_processes} processes x {args.chain_workers} threads" if args.chain_processes
                        else f"{args.chain_workers} threads") if chains is not None else None,
         "chain_busy_s": chains.busy_s if chains is not None else 0.0,

@@ -53,9 +53,9 @@ class InstantEval:
         return [float((p[0] * 0.013 + p[1] * 0.07 + p[3] * 0.001 + p[4]) % 1.0) for p in params]
 
 
-def _search(tmp, executor=None, world=9, block=2, iters=24):
+def _search(tmp, executor=None, world=9, block=2, iters=24, chunks=1):
     nb = (world - 1) // block
-    comm = PopulationComm(nb, block, InstantEval())
+    comm = PopulationComm(nb, block, InstantEval(), chunks=chunks)
     kw = {"chain_executor": executor} if executor is not None else {}
     O.reset_stats()
     sched = AskTellScheduler(comm, nb, mnist_space(), checkpoint=os.path.join(tmp, "c.pkl"), optimizer_kwargs=kw)
@@ -223,3 +223,21 @@ def test_lazy_process_search_equals_sequential(fake_gp, tmp_path, monkeypatch):
         finally:
             ex.close()
         assert got == want, (workers, threads)
+
+
+def test_chunked_populations_equal_whole_populations(fake_gp, tmp_path):
+    """--population-chunks: a population trained in parts, each as soon as its own
+    ask batches resolve, leaves the search unchanged (told points, FOMs, trained
+    trials, refits); the timeline still has one entry per population."""
+    import random
+
+    random.seed(5)
+    want = _search(str(tmp_path), world=17, iters=40)
+    for chunks in (2, 3, 8):
+        ex = ThreadChainExecutor(device=None, workers=3)
+        try:
+            random.seed(5)
+            got = _search(str(tmp_path), ex, world=17, iters=40, chunks=chunks)
+        finally:
+            ex.close()
+        assert got == want, chunks
