@@ -428,7 +428,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
     // contiguous tiles per wave (neighbours along a band share most live taps, so the
     // wave's union tap rectangle wastes fewer groups than a round-robin spread)
     const int per = (T + 3) >> 2;
-    int py[4], px[4], pbase[4], kylo[4], kyhi[4], kxlo[4], kxhi[4];
+    int py[4], px[4], kylo[4], kyhi[4], kxlo[4], kxhi[4];
     bool has[4];
     int uy0 = k, uy1 = 0, ux0 = k, ux1 = 0;
     const int dy = (lane & 15) >> 2, dx = lane & 3;
@@ -452,7 +452,6 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
         const bool pix = y < ty1 && x < tx1;
         py[i] = pix ? y - pad - gy_lo : -(1 << 20);   // an invalid output pixel never reads the image
         px[i] = x - pad;
-        pbase[i] = pix ? py[i] * RS + px[i] * Fp + krow : 0;   // + the tap's offset when in range
     }
     f32x4 acc[4][NT];
 #pragma unroll
@@ -461,124 +460,84 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
         for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     __syncthreads();  // image staged; no further barriers
 
-    // K order: tap row ky, then the row's taps kx in [ux0, ux1) and their channel
-    // quads (4 channels = one MFMA k-step) -- per tap row a run of nx * q quads, whose
-    // weight rows are contiguous in w2t ([k*k][F4][N16]).  A group is 4 consecutive
-    // quads of a run (it may straddle two taps); the run's last group is padded with
-    // quads whose A fragment is the zero block.  A tile whose taps are all dead for a
-    // group skips its MFMAs (wave-uniform); within a live group a dead tap reads the
-    // zero block (its pixels are all halo), an exact no-op.  So every tile gets the
-    // same k-step sequence as a per-tap, per-channel-block walk, with ~2.5% extra
-    // MFMAs and no per-k-step branch.  Weights stream from L2 and A fragments come
-    // from the LDS image one group ahead (ping-pong registers, loop unrolled by two).
-    const int q = F4 >> 2;                       // channel quads per tap
+    // Weight fragments straight from L2: group = (tap, 16-channel block), 4 k-steps;
+    // ping-pong register buffers (loop unrolled by two), loads unconditional.
+    const int CB = (F4 + 15) >> 4;
     const int nx = ux1 - ux0;
-    const int L = nx * q;                        // quads per tap row
-    const int G = (L + 3) >> 2;                  // groups per tap row
-    const int ngroups = (uy1 > uy0 && nx > 0 && a.debug != 1) ? (uy1 - uy0) * G : 0;
+    const int ngroups = (uy1 > uy0 && nx > 0 && a.debug != 1) ? (uy1 - uy0) * nx * CB : 0;
     constexpr int N16 = NT * 16;
-    // group state: tap row ky, first quad j of the run, its tap kx0 and channel quad c0
-    struct Grp { int ky, j, kx0, c0; };
-    auto advance = [&](Grp& g) {
-        g.j += 4;
-        if (g.j >= L) { g.j = 0; g.kx0 = ux0; g.c0 = 0; ++g.ky; return; }
-        g.c0 += 4;
-        while (g.c0 >= q) { g.c0 -= q; ++g.kx0; }
-    };
-    auto load_group = [&](const Grp& g, float (&dst)[4][NT]) {
-        // 16 contiguous weight rows (quads past the run read the next taps' rows or the
-        // 16 slack rows, finite, against a zero A); the prefetch past the last group
-        // (ky = uy1 <= k) is clamped into the array.  Loads unconditional, so they stay
-        // in flight until the group's MFMAs consume them.
-        const int ky = min(g.ky, k - 1);
-        const float* src = W + ((long long)((ky * k + ux0) * F4 + 4 * g.j) + krow) * N16 + kcol;
+    auto load_group = [&](int ky, int kx, int cb, float (&dst)[4][NT]) {
+        // w2t is [k*k][F4][N16], zero padded (+16 rows of slack): no bounds select,
+        // so the loads stay in flight until the MFMAs of the group consume them
+        const float* src = W + ((long long)(a.debug == 4 ? (cb & 1) * 16 : (ky * k + kx) * F4 + cb * 16) + krow) * N16 + kcol;
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
-            for (int jn = 0; jn < NT; ++jn) dst[u][jn] = src[u * 4 * N16 + jn * 16];
+            for (int j = 0; j < NT; ++j) dst[u][j] = src[u * 4 * N16 + j * 16];
     };
-    auto run = [&](auto tpw_c) {
-        constexpr int TPW = decltype(tpw_c)::value;
-        // (tap kx, LDS offset) of the group's quads; quads past the run get kx = -1 << 20
-        auto quads = [&](const Grp& g, int (&kxu)[4], int (&off)[4]) {
-            int kx = g.kx0, c = g.c0;
+    auto advance = [&](int& ky, int& kx, int& cb) {
+        if (++cb == CB) { cb = 0; if (++kx == ux1) { kx = ux0; ++ky; } }
+    };
+    // A fragments of a group: 4 k-steps x 4 tiles, read from the LDS image one group
+    // ahead of their MFMAs (like the B fragments), so no MFMA waits on its own reads
+    auto readA = [&](int ky, int kx, int cb, float (&av)[4][4]) {
+        const int coff = cb * 16 + krow;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const bool in = g.j + u < L;
-                kxu[u] = in ? kx : -(1 << 20);
-                off[u] = g.ky * RS + kx * Fp + 4 * c;
-                if (++c == q) { c = 0; ++kx; }
-            }
-        };
-        auto readA = [&](const Grp& g, float (&av)[4][4]) {
-            int kxu[4], off[4];
-            quads(g, kxu, off);
+        for (int i = 0; i < 4; ++i) {
+            const int ry = py[i] + ky, cx = px[i] + kx;
+            const int base = ((unsigned)ry < (unsigned)rows && (unsigned)cx < (unsigned)H2)
+                                 ? ry * RS + cx * Fp + coff : zoff + krow;   // halo -> zero block
 #pragma unroll
-            for (int i = 0; i < TPW; ++i) {
-                const bool rowok = (unsigned)(py[i] + g.ky) < (unsigned)rows;
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const bool ok = rowok && (unsigned)(px[i] + kxu[u]) < (unsigned)H2;
-                    av[u][i] = img[ok ? pbase[i] + off[u] : zoff + krow];   // halo / padding -> zero block
-                }
-            }
-        };
-        auto compute = [&](const Grp& g, const float (&av)[4][4], const float (&bw)[4][NT]) {
-            // the group's taps: kx0 .. kxl (the tap of its last quad inside the run)
-            int kxl = g.kx0;
-            {
-                int kx = g.kx0, c = g.c0;
-#pragma unroll
-                for (int u = 1; u < 4; ++u) {
-                    if (++c == q) { c = 0; ++kx; }
-                    if (g.j + u < L) kxl = kx;
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < TPW; ++i) {
-                const bool live = g.ky >= kylo[i] && g.ky < kyhi[i] && kxl >= kxlo[i] && g.kx0 < kxhi[i];
-                if (!live) continue;
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-#pragma unroll
-                    for (int jn = 0; jn < NT; ++jn)
-                        acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][i], bw[u][jn], acc[i][jn], 0, 0, 0);
-            }
-        };
-        float b0[4][NT], b1[4][NT], a0[4][4], a1[4][4];
-        Grp cur{uy0, 0, ux0, 0}, nxt = cur;   // groups g and g + 1
-        if (ngroups) {
-            load_group(cur, b0);
-            readA(cur, a0);
-            advance(nxt);
-        }
-        // the prefetch of group g + 1 is unconditional (past the end it reads clamped
-        // weights and halo zeros, never used): every path into a group's MFMAs then has
-        // the same loads in flight, and the compiler's vmcnt waits stay one group ahead
-        for (int g = 0; g < ngroups; g += 2) {
-            load_group(nxt, b1);
-            readA(nxt, a1);
-            __builtin_amdgcn_sched_barrier(0);
-            compute(cur, a0, b0);
-            __builtin_amdgcn_sched_barrier(0);
-            if (g + 1 >= ngroups) break;
-            cur = nxt;
-            advance(nxt);
-            load_group(nxt, b0);
-            readA(nxt, a0);
-            __builtin_amdgcn_sched_barrier(0);
-            compute(cur, a1, b1);
-            __builtin_amdgcn_sched_barrier(0);
-            cur = nxt;
-            advance(nxt);
+            for (int u = 0; u < 4; ++u) av[u][i] = img[base + u * 4];
         }
     };
-    // this wave's tile count: tiles [wave * per, min(T, wave * per + per))
-    const int mine = __builtin_amdgcn_readfirstlane(max(0, min(per, T - wave * per)));
-    if (mine >= 4) run(std::integral_constant<int, 4>{});
-    else if (mine == 3) run(std::integral_constant<int, 3>{});
-    else if (mine == 2) run(std::integral_constant<int, 2>{});
-    else if (mine == 1) run(std::integral_constant<int, 1>{});
+    auto compute = [&](int ky, int kx, int cb, const float (&av)[4][4], const float (&bw)[4][NT]) {
+        bool live[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            live[i] = has[i] && ky >= kylo[i] && ky < kyhi[i] && kx >= kxlo[i] && kx < kxhi[i];
+        const int nu = min(4, (F4 - cb * 16) >> 2);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (u >= nu) break;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (!live[i]) continue;
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][i], bw[u][j], acc[i][j], 0, 0, 0);
+            }
+        }
+    };
+    float b0[4][NT], b1[4][NT], a0[4][4], a1[4][4];
+    int cky = uy0, ckx = ux0, ccb = 0;   // group g
+    int nky = uy0, nkx = ux0, ncb = 0;   // group g + 1
+    if (ngroups) {
+        load_group(cky, ckx, ccb, b0);
+        readA(cky, ckx, ccb, a0);
+        advance(nky, nkx, ncb);
+    }
+    for (int g = 0; g < ngroups; g += 2) {
+        if (g + 1 < ngroups) {
+            load_group(nky, nkx, ncb, b1);
+            readA(nky, nkx, ncb, a1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        compute(cky, ckx, ccb, a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (g + 1 >= ngroups) break;
+        cky = nky; ckx = nkx; ccb = ncb;
+        advance(nky, nkx, ncb);
+        if (g + 2 < ngroups) {
+            load_group(nky, nkx, ncb, b0);
+            readA(nky, nkx, ncb, a0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        compute(cky, ckx, ccb, a1, b1);
+        __builtin_amdgcn_sched_barrier(0);
+        cky = nky; ckx = nkx; ccb = ncb;
+        advance(nky, nkx, ncb);
+    }
 
     // ---- epilogue: accumulator row p = krow*4 + r is tile pixel (p>>2, p&3)
 #pragma unroll

@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--trials", type=int, default=64)
     ap.add_argument("--folds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--shard", default=None,
+                    help="K/N: only rank K's LPT-by-FLOPs share of the (trial, fold) units over N ranks "
+                         "(what one GPU trains of the population in the distributed search)")
     args = ap.parse_args()
     trials = sample_trials(args.trials)
     members = []
@@ -32,6 +35,14 @@ def main():
         for f in range(args.folds):
             members.append(TrialSpec(t.nb_filters, t.kernel_size, t.pool_size, t.dense, t.lr, t.dropout, seed=len(members)))
             folds.append(f)
+    if args.shard:
+        from mpi_opt_amd.blocks import lpt_assign
+
+        k, n = (int(v) for v in args.shard.split("/"))
+        owner = lpt_assign([m.flops_per_sample_train() for m in members], n)
+        mine = [i for i, o in enumerate(owner) if o == k]
+        members = [members[i] for i in mine]
+        folds = [folds[i] for i in mine]
     t0 = time.time()
     eng = PopulationEngine(members, batch=100)
     x, y = synthetic_mnist(60000, seed=0)
