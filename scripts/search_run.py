@@ -37,10 +37,22 @@ def main():
         with open(out_path + ".partial", "w") as fh:
             json.dump(partial, fh, indent=1, default=float)
 
+    import threading
+
+    from mpi_opt_amd import optimizer as O
+
+    stop = threading.Event()
+
+    def heartbeat():   # a line a minute, whatever phase the search is in
+        while not stop.wait(60.0):
+            log(f"heartbeat: {O.STATS['refits']} refits so far")
+
+    threading.Thread(target=heartbeat, daemon=True).start()
     with tempfile.TemporaryDirectory() as tmp:
         if args.checkpoint == "coordinator.pkl":
             args.checkpoint = os.path.join(tmp, "coordinator.pkl")
         rep = search.run_search(args, log=log, progress=log, on_population=population_done)
+    stop.set()
     if rep is None:
         return 0
     rep["argv"] = argv
