@@ -39,21 +39,25 @@ def make_parser():
                    default="binary_crossentropy")
     p.add_argument("--sync-every", default=1, type=int, dest="sync_every",
                    help="how often to sync weights with master (no effect: synchronous single-GPU trials)")
-    p.add_argument("--preload-data", default=0, type=int, dest="data_preload")
-    p.add_argument("--cache-data", default="", dest="caching_dir")
+    p.add_argument("--preload-data", default=0, type=int, dest="data_preload",
+                   help="mpi_learn data preloading (no effect here: the data is resident on the GPU)")
+    p.add_argument("--cache-data", default="", dest="caching_dir",
+                   help="mpi_learn data cache dir (no effect here: the data is resident on the GPU)")
     p.add_argument("--early-stopping", default=None, dest="early_stopping",
                    help="patience for early stopping: N (val_loss) or METRIC,~<,N / METRIC,~>,N")
     p.add_argument("--target-metric", default=None, dest="target_metric",
                    help="stop a fold once METRIC,OP,VALUE holds (e.g. val_acc,>,0.97)")
-    p.add_argument("--easgd", action="store_true")
-    p.add_argument("--worker-optimizer", dest="worker_optimizer", default="sgd")
-    p.add_argument("--elastic-force", type=float, default=0.9)
-    p.add_argument("--elastic-lr", type=float, default=1.0, dest="elastic_lr")
-    p.add_argument("--elastic-momentum", type=float, default=0, dest="elastic_momentum")
+    p.add_argument("--easgd", action="store_true", help="mpi_learn EASGD exchange (no effect here: trials train synchronously on one GPU)")
+    p.add_argument("--worker-optimizer", dest="worker_optimizer", default="sgd",
+                   help="mpi_learn worker optimizer (no effect here: trials train synchronously on one GPU)")
+    p.add_argument("--elastic-force", type=float, default=0.9, help="EASGD (no effect here: trials train synchronously on one GPU)")
+    p.add_argument("--elastic-lr", type=float, default=1.0, dest="elastic_lr", help="EASGD (no effect here: trials train synchronously on one GPU)")
+    p.add_argument("--elastic-momentum", type=float, default=0, dest="elastic_momentum", help="EASGD (no effect here: trials train synchronously on one GPU)")
     p.add_argument("--block-size", type=int, default=2, help="number of ranks per block (reference MPI layout)")
     p.add_argument("--n-fold", type=int, default=1, dest="n_fold")
-    p.add_argument("--n-master", type=int, default=1, dest="n_master")
-    p.add_argument("--n-process", type=int, default=1, dest="n_process")
+    p.add_argument("--n-master", type=int, default=1, dest="n_master", help="mpi_learn masters per block (no effect here: trials train synchronously on one GPU)")
+    p.add_argument("--n-process", type=int, default=1, dest="n_process",
+                   help="mpi_learn processes per worker (no effect here: trials train synchronously on one GPU)")
     p.add_argument("--num-iterations", type=int, default=10)
     p.add_argument("--previous-result", default=None, dest="previous_state")
     p.add_argument("--target-objective", type=float, default=None, dest="target_objective")
@@ -101,6 +105,20 @@ def check_training_flags(args):
     return StopRule.from_args(args.early_stopping, args.target_metric)
 
 
+#: flags of mpi_learn's asynchronous multi-process training that have no counterpart
+#: here (a trial trains synchronously on one GPU): (dest, default)
+NO_EFFECT_FLAGS = (("sync_every", 1), ("data_preload", 0), ("caching_dir", ""), ("easgd", False),
+                   ("worker_optimizer", "sgd"), ("elastic_force", 0.9), ("elastic_lr", 1.0),
+                   ("elastic_momentum", 0), ("n_master", 1), ("n_process", 1))
+
+
+def no_effect_notes(args):
+    """One note per no-effect flag set away from its default (printed, not silent)."""
+    return [f"note: --{dest.replace('_', '-')}={getattr(args, dest)!r} has no effect here "
+            f"(mpi_learn's multi-process exchange is not reproduced; trials train synchronously on one GPU)"
+            for dest, dflt in NO_EFFECT_FLAGS if getattr(args, dest, dflt) != dflt]
+
+
 def block_layout(world_size, block_size):
     """option3:174-181: (num_blocks, left_over)."""
     return divmod(world_size - 1, block_size)
@@ -125,6 +143,8 @@ def run_search(args, x=None, y=None, log=print, progress=None, on_population=Non
 
     num_blocks, left_over = block_layout(args.world_size, args.block_size)
     stopping = check_training_flags(args)
+    for note in no_effect_notes(args):
+        log(note)
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None

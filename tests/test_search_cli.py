@@ -65,3 +65,17 @@ def test_sanity_and_leftover_exit():
         check_sanity(make_parser().parse_args(["--block-size", "1"]))
     assert main(["--block-size", "5", "--world-size", "20"]) == 1
     assert main(["--example", "gan"]) == 2
+
+
+def test_no_effect_flags_are_reported_not_silent():
+    """mpi_learn's asynchronous-exchange flags have no counterpart here: set away
+    from their defaults they produce a note (and their --help says so)."""
+    from mpi_opt_amd import search
+
+    p = search.make_parser()
+    assert search.no_effect_notes(p.parse_args([])) == []
+    notes = search.no_effect_notes(p.parse_args(["--easgd", "--sync-every", "4", "--elastic-lr", "0.5"]))
+    assert len(notes) == 3 and all("no effect" in n for n in notes)
+    helps = {a.dest: a.help or "" for a in p._actions}
+    for dest, _ in search.NO_EFFECT_FLAGS:
+        assert "no effect" in helps[dest], dest
