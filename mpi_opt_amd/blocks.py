@@ -313,9 +313,10 @@ class PopulationComm:
 
     def Barrier(self):
         if self.train_tail and self.exited and self.pending:
-            launched = {b: resolve(p) for b, p in self.pending.items()}
+            # the points stay lazy here too: evaluate_pending resolves them (by chunk)
+            launched = dict(self.pending)
             self.evaluate_pending()
-            self.tail = [(launched[b], self.results[b]) for b in sorted(launched)]
+            self.tail = [(resolve(launched[b]), self.results[b]) for b in sorted(launched)]
 
     @property
     def trials_trained(self):
