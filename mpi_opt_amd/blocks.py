@@ -226,6 +226,11 @@ class _Request:
         return True, c.results.pop(self.block)
 
 
+def _batch_seq(p):
+    """Submission number of a lazy point's ask batch (-1: already a plain point)."""
+    return p.batch.seq if isinstance(p, LazyPoint) and p.batch.seq is not None else -1
+
+
 class PopulationComm:
     """MPI-communicator stand-in for :class:`Coordinator` (size = 1 + blocks x block_size)."""
 
@@ -291,15 +296,20 @@ class PopulationComm:
         blocks = sorted(self.pending)
         points = [self.pending.pop(b) for b in blocks]
         k = min(self.chunks, len(points))
+        # parts in the order their ask batches were submitted (the executors run them
+        # first-in first-out; the scheduler polls blocks in a shuffled order, so block
+        # order is not submission order); results go back to their blocks
+        order = sorted(range(len(points)), key=lambda i: (_batch_seq(points[i]), i)) if k > 1 else \
+            list(range(len(points)))
         cuts = [len(points) * i // k for i in range(k + 1)]
-        params, foms, wait = [], [], 0.0
+        params, foms, wait = [None] * len(points), [None] * len(points), 0.0
         for c0, c1 in zip(cuts[:-1], cuts[1:]):
-            # block order is the order the ask batches were submitted in
+            idx = order[c0:c1]
             tw = time.perf_counter()
-            part = resolve_all(points[c0:c1])
+            part = resolve_all([points[i] for i in idx])
             wait += time.perf_counter() - tw
-            params.extend(part)
-            foms.extend(self.evaluator.evaluate(part))
+            for i, p_, f_ in zip(idx, part, self.evaluator.evaluate(part)):
+                params[i], foms[i] = p_, f_
         t2 = time.perf_counter()
         t1 = t0 + wait
         self.timeline.append((t0 - self._t_last, wait, t2 - t1, len(params)))

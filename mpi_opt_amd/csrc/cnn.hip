@@ -1388,8 +1388,8 @@ int env_int(const char* name, int dflt) {
 }
 
 // Planner overrides for tuning sweeps, one variable: MPO_POP_PLAN="key=value,..."
-// (keys: dg_tiles, dg_kb, conv_mt, conv_kb1, conv_kb2, wg_spg1, wg_spg2).  Every
-// value only changes how work is cut into items, never the arithmetic.
+// (keys: dg_tiles, dg_kb, conv_mt, conv_kb1, conv_kb2, wg_spg1, wg_spg2, streams).  Every
+// value only changes how work is cut into items or ordered over streams, never the arithmetic.
 int plan_knob(const char* key, int dflt) {
     const char* v = getenv("MPO_POP_PLAN");
     if (!v) return dflt;
@@ -1430,6 +1430,52 @@ struct Plan {
     size_t lds_conv_max = 0, lds_wg_max = 0;
     int conv_mt = 4;        // forward conv m-tiles per wave at most: items of up to 256 pixels (MPO_POP_PLAN conv_mt=2: 128)
     int dg_tiles = 12;      // 4x4 tiles per conv2 input-gradient work item at most (MPO_POP_PLAN dg_tiles)
+    // Second stream for independent launches (MPO_POP_PLAN streams=1 keeps one): the
+    // forward conv2 buckets alternate between the two, and the conv2 weight gradient
+    // runs beside the input gradient + conv1 weight gradient, so one launch's tail
+    // overlaps the other's work.  No two concurrent kernels write the same buffer.
+    int streams = 2;
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    int side_device = -1;
+    ~Plan() {
+        if (side) (void)hipStreamDestroy(side);
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+        if (ev_join) (void)hipEventDestroy(ev_join);
+    }
+    // the side stream on s's device (created on first use); nullptr = run serially on s
+    hipStream_t side_for(hipStream_t s) {
+        if (streams < 2) return nullptr;
+        int dev = 0;
+        if (hipStreamGetDevice(s, &dev) != hipSuccess) return nullptr;
+        if (side && dev == side_device) return side;
+        if (side) {   // the caller moved to another device: new stream and events there
+            (void)hipStreamDestroy(side);
+            (void)hipEventDestroy(ev_fork);
+            (void)hipEventDestroy(ev_join);
+            side = nullptr; ev_fork = ev_join = nullptr;
+        }
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(dev);
+        const bool ok = hipStreamCreateWithFlags(&side, hipStreamNonBlocking) == hipSuccess &&
+                        hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) == hipSuccess &&
+                        hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) == hipSuccess;
+        (void)hipSetDevice(cur);
+        if (!ok) { streams = 1; return nullptr; }
+        side_device = dev;
+        return side;
+    }
+    // s2 starts after everything enqueued on s so far
+    hipError_t fork(hipStream_t s, hipStream_t s2) {
+        if (hipError_t e = hipEventRecord(ev_fork, s)) return e;
+        return hipStreamWaitEvent(s2, ev_fork, 0);
+    }
+    // s continues after everything enqueued on s2 so far
+    hipError_t join(hipStream_t s, hipStream_t s2) {
+        if (hipError_t e = hipEventRecord(ev_join, s2)) return e;
+        return hipStreamWaitEvent(s, ev_join, 0);
+    }
 };
 
 size_t conv_lds_bytes(int rows, int Wp, int Cin, int Ho, int K, int nt) {
@@ -1568,6 +1614,7 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         const Member& m = P.mem[i];
         const int k = m.k, F = m.F, nt = m.nt;
         if (i == 0) P.conv_mt = plan_knob("conv_mt", 4) == 2 ? 2 : 4;
+        if (i == 0) P.streams = plan_knob("streams", 2) >= 2 ? 2 : 1;
         const int mcap = P.conv_mt * 64;   // 4 waves x conv_mt m-tiles of 16 pixels
         const int R1 = choose_rows(m.H1, [&](int R) { return conv_lds_bytes(R + k - 1, kImg, 1, m.H1, k * k, nt); }, kc1, kc2, mcap);
         const int R2 = choose_rows(m.H2, [&](int R) { return conv_lds_bytes(R + k - 1, m.H1, F, m.H2, k * k * F, nt); }, kc1, kc2, mcap);
@@ -1712,10 +1759,13 @@ hipError_t launch_wg1_wave_nt(const StepArgs& a, const WgItem* items, int count,
     return hipGetLastError();
 }
 
+// s2 (optional): segments alternate between s and s2 (independent launches)
 template <class Fn>
-hipError_t launch_segs(Plan& P, const Bucketed& bk, const char* name, hipStream_t s, Fn launch_nt) {
+hipError_t launch_segs(Plan& P, const Bucketed& bk, const char* name, hipStream_t s, Fn launch_nt,
+                       hipStream_t s2 = nullptr) {
+    int i = 0;
     for (const Seg& sg : bk.segs) {
-        if (hipError_t e = launch_nt(sg)) return e;
+        if (hipError_t e = launch_nt(sg, (s2 && (i++ & 1)) ? s2 : s)) return e;
         P.timer.mark(std::string(name) + "/nt" + std::to_string(sg.nt) + (sg.sub ? "/mt" + std::to_string(sg.sub) : "") +
                          (P.timer_detail ? "/occ" + std::to_string(lds_class(sg.lds)) + "/n" + std::to_string(sg.end - sg.begin) : ""),
                      s);
@@ -1737,17 +1787,18 @@ struct ConvLaunch {
 };
 
 template <int OP>
-hipError_t launch_conv(Plan& P, const StepArgs& a, size_t table_off, const Bucketed& bk, hipStream_t s) {
+hipError_t launch_conv(Plan& P, const StepArgs& a, size_t table_off, const Bucketed& bk, hipStream_t s,
+                       hipStream_t s2 = nullptr) {
     const ConvItem* base = dev_table<ConvItem>(P, table_off);
-    return launch_segs(P, bk, OP == CONV1_FWD ? "conv1_fwd" : "conv2_fwd", s, [&](const Seg& sg) {
-        return MPO_NT_SWITCH(ConvLaunch<OP>::template go, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, s);
-    });
+    return launch_segs(P, bk, OP == CONV1_FWD ? "conv1_fwd" : "conv2_fwd", s, [&](const Seg& sg, hipStream_t st) {
+        return MPO_NT_SWITCH(ConvLaunch<OP>::template go, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, st);
+    }, s2);
 }
 
 hipError_t launch_dgrad(Plan& P, const StepArgs& a, hipStream_t s) {
     const ConvItem* base = dev_table<ConvItem>(P, P.off_dgrad);
-    return launch_segs(P, P.bdg, "conv2_dgrad", s, [&](const Seg& sg) {
-        return MPO_NT_SWITCH(launch_dgrad_nt, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, s);
+    return launch_segs(P, P.bdg, "conv2_dgrad", s, [&](const Seg& sg, hipStream_t st) {
+        return MPO_NT_SWITCH(launch_dgrad_nt, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, st);
     });
 }
 
@@ -1762,11 +1813,11 @@ struct WgLaunch {
 template <int OP>
 hipError_t launch_wg(Plan& P, const StepArgs& a, size_t table_off, const Bucketed& bk, hipStream_t s) {
     const WgItem* base = dev_table<WgItem>(P, table_off);
-    return launch_segs(P, bk, OP == WG_CONV1 ? "conv1_wgrad" : "conv2_wgrad", s, [&](const Seg& sg) {
+    return launch_segs(P, bk, OP == WG_CONV1 ? "conv1_wgrad" : "conv2_wgrad", s, [&](const Seg& sg, hipStream_t st) {
         if constexpr (OP == WG_CONV1)
-            return MPO_NT_SWITCH(launch_wg1_wave_nt, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, sg.sub, s);
+            return MPO_NT_SWITCH(launch_wg1_wave_nt, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, sg.sub, st);
         else
-            return MPO_NT_SWITCH(WgLaunch<OP>::template go, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, sg.sub, s);
+            return MPO_NT_SWITCH(WgLaunch<OP>::template go, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, sg.sub, st);
     });
 }
 
@@ -1808,7 +1859,13 @@ int forward(Plan& P, const StepArgs& a, hipStream_t s) {
     MPO_LAUNCH_CHECK();
     P.timer.mark("flip_w2", s);
     MPO_HIP(launch_conv<CONV1_FWD>(P, a, P.off_conv1, P.bc1, s));
-    MPO_HIP(launch_conv<CONV2_FWD>(P, a, P.off_conv2, P.bc2, s));
+    if (hipStream_t s2 = P.timer.on ? nullptr : P.side_for(s)) {   // profiled steps stay serial
+        MPO_HIP(P.fork(s, s2));
+        MPO_HIP(launch_conv<CONV2_FWD>(P, a, P.off_conv2, P.bc2, s, s2));
+        MPO_HIP(P.join(s, s2));
+    } else {
+        MPO_HIP(launch_conv<CONV2_FWD>(P, a, P.off_conv2, P.bc2, s));
+    }
     hipLaunchKernelGGL(pool_fwd_kernel, dim3((unsigned)P.per_sample.size()), dim3(256), 0, s, a,
                        dev_table<MItem>(P, P.off_ps));
     MPO_LAUNCH_CHECK();
@@ -1919,9 +1976,19 @@ int mpo_pop_train_step(void* handle, const float* x, const int32_t* labels, cons
                        dev_table<MItem>(P, P.off_ps));
     MPO_LAUNCH_CHECK();
     P.timer.mark("pool_bwd", s);
-    MPO_HIP(launch_dgrad(P, a, s));
-    MPO_HIP(launch_wg<WG_CONV2>(P, a, P.off_wg2, P.bw2, s));
-    MPO_HIP(launch_wg<WG_CONV1>(P, a, P.off_wg1, P.bw1, s));
+    if (hipStream_t s2 = P.timer.on ? nullptr : P.side_for(s)) {
+        // conv2 weight gradient (a1, dz2 -> slabs) beside the input gradient and the
+        // conv1 weight gradient (dz2 -> dz1 -> slabs): disjoint outputs
+        MPO_HIP(P.fork(s, s2));
+        MPO_HIP(launch_wg<WG_CONV2>(P, a, P.off_wg2, P.bw2, s2));
+        MPO_HIP(launch_dgrad(P, a, s));
+        MPO_HIP(launch_wg<WG_CONV1>(P, a, P.off_wg1, P.bw1, s));
+        MPO_HIP(P.join(s, s2));
+    } else {
+        MPO_HIP(launch_dgrad(P, a, s));
+        MPO_HIP(launch_wg<WG_CONV2>(P, a, P.off_wg2, P.bw2, s));
+        MPO_HIP(launch_wg<WG_CONV1>(P, a, P.off_wg1, P.bw1, s));
+    }
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)P.wred_blocks, (unsigned)P.wred.size()), dim3(256), 0, s, a,
                        dev_table<MItem>(P, P.off_wr), P.wred_per_block);
     MPO_LAUNCH_CHECK();
