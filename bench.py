@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import argparse
 import collections
+import math
 import json
 import os
 import shutil
@@ -416,6 +417,35 @@ def cpu_baseline_train(trials, n_sample=32, concurrent=4):
                       f"extrapolated to 24000 train steps + 6000 validation batches per trial ({wall:.1f} s)"}
 
 
+def shard_step_ratio(eng, members, folds, x, yl, otr, torch, dev, gpus=8, steps=10):
+    """ms per train step of one GPU's LPT share (by FLOPs, as DistributedEvaluator
+    deals (trial, fold) units) of this population over ``gpus`` GPUs, against the
+    whole population's, same process: how much of a population's training one of
+    ``gpus`` GPUs still pays (small populations run at a higher per-member cost)."""
+    from mpi_opt_amd.blocks import lpt_assign
+    from mpi_opt_amd.population import PopulationEngine
+
+    owner = lpt_assign([m.flops_per_sample_train() for m in members], gpus)
+    mine = [i for i, o in enumerate(owner) if o == 0]
+    sub = PopulationEngine([members[i] for i in mine], batch=eng.batch, device=dev)
+    osub = otr[mine].contiguous()
+
+    def timed(e, order):
+        for s_ in range(2):
+            e.train_step(x, yl, order, s_ * e.batch)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for s_ in range(steps):
+            e.train_step(x, yl, order, (s_ + 2) * e.batch)
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / steps * 1e3
+
+    full_ms, shard_ms = timed(eng, otr), timed(sub, osub)
+    del sub
+    return {"gpus": gpus, "members": len(mine), "shard_ms_per_step": shard_ms, "full_ms_per_step": full_ms,
+            "factor": shard_ms / full_ms}
+
+
 def bench_train(args, torch, dist, ws, rank, dev):
     from mpi_opt_amd.population import PopulationEngine, TrialSpec, kfold_split, synthetic_mnist
 
@@ -484,6 +514,7 @@ def bench_train(args, torch, dist, ws, rank, dev):
             by_kernel[k] += v
     algo_bytes = sum(by_kernel.values())
     pmc = (args.pmc or {}).get("train") if n_trials == 64 else None
+    shard = shard_step_ratio(eng, members, folds, x, yl, otr, torch, dev) if (n_trials == 64 and ws == 1) else None
     if pmc and pmc.get("per_family_hbm_bytes"):
         fam = pmc["per_family_hbm_bytes"]
         pmc["per_family_vs_model"] = {k: {"measured": fam.get(k, 0.0), "model": v,
@@ -510,6 +541,7 @@ def bench_train(args, torch, dist, ws, rank, dev):
                      "every_tensor_once_hbm_bytes_per_train_batch": floor_bytes,
                      "algorithmic_flops_per_step": flops,
                      "pmc": pmc},
+        "shard_8gpu": shard,
         "_trials": trials,
     }
 
@@ -846,39 +878,59 @@ def _price(curve, ns):
     return float(sum(np.sum(c * ns ** p) for p, c in curve))
 
 
-def project_configs3(proj, gpus=8, cpu=None):
+def project_configs3(proj, gpus=8, cpu=None, shard=None):
     """BASELINE configs[3] in full (``-n 129 --block-size 2 --n-fold 5
     --num-iterations 256 --epochs 10``, 256 trials over ``gpus`` GPUs), from this
-    run's measured parts -- a projection, labelled as such:
+    run's measured parts -- a projection, labelled as such (the 1-GPU full run
+    itself is measured once per round: scripts/search_run.py, profiles/r04/):
 
-    * the protocol's exact refit schedule (protocol_refits), split into the tells'
-      refits (rank 0, one after another) and the cl_min chains' (dealt over the
-      GPUs, ``chain_workers`` concurrent chains each, mpi_opt_amd.chains);
-    * a tell refit costs its sequential latency t(n) (fitted on the standalone
-      ask(256)'s refits + this run's small-n ones); a chain refit costs its
-      share of this run's optimizer window: c(n) = t(n) * optimizer_s / sum_run t(n)
-      (the measured concurrency on one GPU), divided by ``gpus``;
-    * training: trials x GPU-seconds per 10-epoch 5-fold trial / ``gpus``.
+    * the protocol's exact refit schedule (protocol_refits): the tells' refits on
+      rank 0 one after another, each followed by an ask(256) chain of refits at
+      n = told .. told + 255;
+    * t(n): the sequential refit + proposal latency fitted on the standalone
+      ask(256)'s refits and this run's small-n ones; ``scale`` = this run's
+      optimizer window / sum of t over its refits (the measured concurrency of
+      ``chain_workers`` chains on one GPU);
+    * per population boundary, the chains over ``gpus`` GPUs: their work
+      (sum t x scale) / gpus, but never below ceil(chains / (gpus x workers))
+      rounds of one chain's latency under that concurrency (scale x workers x
+      sum t over its refits);
+    * training: trials x GPU-seconds per 10-epoch 5-fold trial x ``shard.factor``
+      (one GPU's LPT share of a population vs the whole, measured in the train
+      leg; 1 / gpus when absent).
     The optimizer and the populations do not overlap (a population's batches
     resolve before it trains)."""
     refits, pops, tells = protocol_refits(129, 2, 256, with_tells=True)
     coef = fit_refit_cost(proj["latency_samples"])
     ns = np.array(refits, dtype=float)
-    ts = np.array(tells, dtype=float)
     run_ns = np.array(proj["run_refit_ns"], dtype=float)
+    workers = max(1, int(proj.get("chain_workers") or 1))
     scale = proj["optimizer_s"] / max(1e-12, _price(coef, run_ns))
-    t_tell = _price(coef, ts)
-    t_chain = (_price(coef, ns) - t_tell) * scale / gpus
+    t_tell = _price(coef, np.array(tells, dtype=float))
+    t_chain, bounds, told = 0.0, [], 0
+    for b, npop in enumerate(pops[:-1]):
+        told += npop
+        starts = np.arange(told - npop + 1, told + 1, dtype=float)      # told count at each ask of the boundary
+        chain_seq = np.array([_price(coef, n0 + np.arange(256)) for n0 in starts])
+        work = float(chain_seq.sum()) * scale / gpus
+        floor = math.ceil(len(starts) / (gpus * workers)) * float(chain_seq.mean()) * scale * workers
+        bounds.append({"chains": len(starts), "work_s": work, "latency_floor_s": floor, "seconds": max(work, floor)})
+        t_chain += max(work, floor)
     trials = sum(pops)
-    t_train = trials * proj["trial_s_gpu"] / gpus
+    factor = shard["factor"] if shard else 1.0 / gpus
+    t_train = trials * proj["trial_s_gpu"] * factor
     t_gp = t_tell + t_chain
     out = {"workload": "configs[3] in full: -n 129 --block-size 2 --n-fold 5 --num-iterations 256 --epochs 10, "
                        f"{gpus} GPUs (projection from this run's measured parts)",
            "refits": len(refits), "tell_refits": len(tells), "refit_n_mean": float(ns.mean()),
            "refit_n_max": int(ns.max()), "populations": pops, "trials_trained": trials,
-           "refit_latency_fit_s": coef, "chain_concurrency_scale": scale,
+           "trials_told": trials - pops[-1],
+           "refit_latency_fit_s": coef, "chain_concurrency_scale": scale, "chain_workers": workers,
+           "boundaries": bounds, "train_shard_factor": factor,
            "optimizer_s": t_gp, "optimizer_tells_s": t_tell, "optimizer_chains_s": t_chain, "training_s": t_train,
-           "trials_per_hour": trials * 3600.0 / (t_gp + t_train), "optimizer_share": t_gp / (t_gp + t_train)}
+           "trials_per_hour": trials * 3600.0 / (t_gp + t_train),
+           "told_trials_per_hour": (trials - pops[-1]) * 3600.0 / (t_gp + t_train),
+           "optimizer_share": t_gp / (t_gp + t_train)}
     if cpu:
         ccoef = fit_refit_cost(cpu["samples"], powers=(2, 3))
         t_gp_cpu = _price(ccoef, ns)
@@ -1048,8 +1100,8 @@ def main():
                 srch3.pop("_told_state")
                 srch3.pop("_samples")
                 srch3["cpu_baseline"] = None
-            srch3["projection_configs3_8gpu"] = project_configs3(srch3.pop("_proj"),
-                                                                 cpu=cpu_parts)
+            srch3["projection_configs3_8gpu"] = project_configs3(srch3.pop("_proj"), cpu=cpu_parts,
+                                                                 shard=(train or {}).get("shard_8gpu"))
         if dn is not None:
             dn["cpu_baseline"] = cpu_baseline_densenet() if cpu else None
         if res is not None:

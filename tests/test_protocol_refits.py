@@ -52,7 +52,16 @@ def test_configs3_projection_splits_tells_and_chains():
             "latency_samples": [(n, 0.01) for n in range(10, 500, 10)]}            # flat 10 ms latency
     p8, p1 = bench.project_configs3(proj, gpus=8), bench.project_configs3(proj, gpus=1)
     assert abs(p8["optimizer_tells_s"] - 182 * 0.01) < 1e-9 and p1["optimizer_tells_s"] == p8["optimizer_tells_s"]
-    # chains: (49471 - 182) refits x 10 ms/refit measured as 10 s per 1000 refits -> 1 x latency, / gpus
-    assert abs(p1["optimizer_chains_s"] - (49471 - 182) * 0.01) < 1e-6
+    # chains: 3 boundaries x 64 ask(256) chains x 256 refits x 10 ms (measured as 10 s per 1000
+    # refits at 4 workers: scale 1), / gpus; the latency floor (ceil(64 / (gpus x 4)) rounds of
+    # a 256-refit chain running 4x slower under 4-way sharing) meets the work bound exactly here
+    assert abs(p1["optimizer_chains_s"] - 3 * 64 * 256 * 0.01) < 1e-6
     assert abs(p8["optimizer_chains_s"] * 8 - p1["optimizer_chains_s"]) < 1e-6
+    assert all(abs(b["work_s"] - b["latency_floor_s"]) < 1e-9 for b in p8["boundaries"])
     assert abs(p8["training_s"] - 256 * 3.0 / 8) < 1e-9
+    # one GPU's share of a population measured at 0.2 of the whole (not 1/8)
+    ps = bench.project_configs3(proj, gpus=8, shard={"factor": 0.2})
+    assert abs(ps["training_s"] - 256 * 3.0 * 0.2) < 1e-9
+    # 32 GPUs x 4 workers = 128 slots for 64 chains: one chain's latency bounds each boundary
+    p32 = bench.project_configs3(proj, gpus=32)
+    assert all(b["seconds"] == b["latency_floor_s"] > b["work_s"] for b in p32["boundaries"])
