@@ -1434,48 +1434,7 @@ struct Plan {
     // forward conv2 buckets alternate between the two, and the conv2 weight gradient
     // runs beside the input gradient + conv1 weight gradient, so one launch's tail
     // overlaps the other's work.  No two concurrent kernels write the same buffer.
-    int streams = 2;
-    hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    int side_device = -1;
-    ~Plan() {
-        if (side) (void)hipStreamDestroy(side);
-        if (ev_fork) (void)hipEventDestroy(ev_fork);
-        if (ev_join) (void)hipEventDestroy(ev_join);
-    }
-    // the side stream on s's device (created on first use); nullptr = run serially on s
-    hipStream_t side_for(hipStream_t s) {
-        if (streams < 2) return nullptr;
-        int dev = 0;
-        if (hipStreamGetDevice(s, &dev) != hipSuccess) return nullptr;
-        if (side && dev == side_device) return side;
-        if (side) {   // the caller moved to another device: new stream and events there
-            (void)hipStreamDestroy(side);
-            (void)hipEventDestroy(ev_fork);
-            (void)hipEventDestroy(ev_join);
-            side = nullptr; ev_fork = ev_join = nullptr;
-        }
-        int cur = 0;
-        (void)hipGetDevice(&cur);
-        (void)hipSetDevice(dev);
-        const bool ok = hipStreamCreateWithFlags(&side, hipStreamNonBlocking) == hipSuccess &&
-                        hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) == hipSuccess &&
-                        hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) == hipSuccess;
-        (void)hipSetDevice(cur);
-        if (!ok) { streams = 1; return nullptr; }
-        side_device = dev;
-        return side;
-    }
-    // s2 starts after everything enqueued on s so far
-    hipError_t fork(hipStream_t s, hipStream_t s2) {
-        if (hipError_t e = hipEventRecord(ev_fork, s)) return e;
-        return hipStreamWaitEvent(s2, ev_fork, 0);
-    }
-    // s continues after everything enqueued on s2 so far
-    hipError_t join(hipStream_t s, hipStream_t s2) {
-        if (hipError_t e = hipEventRecord(ev_join, s2)) return e;
-        return hipStreamWaitEvent(s, ev_join, 0);
-    }
+    mpo::SideStream side;
 };
 
 size_t conv_lds_bytes(int rows, int Wp, int Cin, int Ho, int K, int nt) {
@@ -1614,7 +1573,7 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         const Member& m = P.mem[i];
         const int k = m.k, F = m.F, nt = m.nt;
         if (i == 0) P.conv_mt = plan_knob("conv_mt", 4) == 2 ? 2 : 4;
-        if (i == 0) P.streams = plan_knob("streams", 2) >= 2 ? 2 : 1;
+        if (i == 0) P.side.enabled = plan_knob("streams", 2) >= 2;
         const int mcap = P.conv_mt * 64;   // 4 waves x conv_mt m-tiles of 16 pixels
         const int R1 = choose_rows(m.H1, [&](int R) { return conv_lds_bytes(R + k - 1, kImg, 1, m.H1, k * k, nt); }, kc1, kc2, mcap);
         const int R2 = choose_rows(m.H2, [&](int R) { return conv_lds_bytes(R + k - 1, m.H1, F, m.H2, k * k * F, nt); }, kc1, kc2, mcap);
@@ -1859,10 +1818,10 @@ int forward(Plan& P, const StepArgs& a, hipStream_t s) {
     MPO_LAUNCH_CHECK();
     P.timer.mark("flip_w2", s);
     MPO_HIP(launch_conv<CONV1_FWD>(P, a, P.off_conv1, P.bc1, s));
-    if (hipStream_t s2 = P.timer.on ? nullptr : P.side_for(s)) {   // profiled steps stay serial
-        MPO_HIP(P.fork(s, s2));
+    if (hipStream_t s2 = P.timer.on ? nullptr : P.side.get(s)) {   // profiled steps stay serial
+        MPO_HIP(P.side.fork(s, s2));
         MPO_HIP(launch_conv<CONV2_FWD>(P, a, P.off_conv2, P.bc2, s, s2));
-        MPO_HIP(P.join(s, s2));
+        MPO_HIP(P.side.join(s, s2));
     } else {
         MPO_HIP(launch_conv<CONV2_FWD>(P, a, P.off_conv2, P.bc2, s));
     }
@@ -1976,14 +1935,14 @@ int mpo_pop_train_step(void* handle, const float* x, const int32_t* labels, cons
                        dev_table<MItem>(P, P.off_ps));
     MPO_LAUNCH_CHECK();
     P.timer.mark("pool_bwd", s);
-    if (hipStream_t s2 = P.timer.on ? nullptr : P.side_for(s)) {
+    if (hipStream_t s2 = P.timer.on ? nullptr : P.side.get(s)) {
         // conv2 weight gradient (a1, dz2 -> slabs) beside the input gradient and the
         // conv1 weight gradient (dz2 -> dz1 -> slabs): disjoint outputs
-        MPO_HIP(P.fork(s, s2));
+        MPO_HIP(P.side.fork(s, s2));
         MPO_HIP(launch_wg<WG_CONV2>(P, a, P.off_wg2, P.bw2, s2));
         MPO_HIP(launch_dgrad(P, a, s));
         MPO_HIP(launch_wg<WG_CONV1>(P, a, P.off_wg1, P.bw1, s));
-        MPO_HIP(P.join(s, s2));
+        MPO_HIP(P.side.join(s, s2));
     } else {
         MPO_HIP(launch_dgrad(P, a, s));
         MPO_HIP(launch_wg<WG_CONV2>(P, a, P.off_wg2, P.bw2, s));

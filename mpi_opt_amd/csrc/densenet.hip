@@ -37,6 +37,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <memory>
 #include <vector>
 
@@ -1084,6 +1085,10 @@ struct DnPlan {
     std::vector<int> bn_S, bn_bs;   // per layer: batch slices and samples per slice
     float *params = nullptr, *grads = nullptr, *m = nullptr, *v = nullptr, *state = nullptr, *act = nullptr;
     bool bound = false;
+    // the weight gradients (+ their slab reduction) of the backward run on a second
+    // stream beside the input-gradient convs and BN backward (MPO_DN_PLAN=streams=1:
+    // one stream); see enqueue_backward for what they read and write
+    mpo::SideStream side;
 };
 
 // (member stride, offset) allocator over the member-major activation arena
@@ -1468,6 +1473,14 @@ void enqueue_bn_bwd(DnPlan& p, const BnArgs& bn, int li, hipStream_t s) {
 
 int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_ms, long long row0, hipStream_t s) {
     const int B = p.B, n = p.n;
+    // Weight gradients on a side stream s2, each forked after its dOut is final on s.
+    // Disjoint from what s writes meanwhile: a dense layer's dOut is its growth slice
+    // [coff, coff + g) of dcat, and the BN backward of it and of every earlier layer
+    // writes dcat[0, cin) with cin <= coff; the input x is cat (not written in the
+    // backward); the slabs and the gradient slots are s2's alone.  The transition dOut
+    // buffer dt is shared by the transitions, so s waits for s2 before each pool
+    // backward refills it; s waits for everything at the end (Adam reads the gradients).
+    hipStream_t s2 = p.side.get(s);
     for (int i = (int)p.layers.size() - 1; i >= 0; --i) {
         Layer& ly = p.layers[i];
         const int st = ly.stage;
@@ -1487,6 +1500,7 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
         long long dout_ms;
         int dout_ps;
         if (ly.kind == K_TRANS) {
+            if (s2) MPO_HIP(p.side.join(s, s2));     // an earlier-issued transition wgrad may still read dt
             const bool v4 = pool_vec4(ly.cout, p.sC[st + 1], p.dt_ms, p.cat_ms[st + 1], p.act + p.dt_off,
                                       p.act + p.dcat_off[st + 1]);
             hipLaunchKernelGGL(v4 ? dn_pool_bwd_kernel<4> : dn_pool_bwd_kernel<1>, dim3((B * ly.H + 1) / 2, n),
@@ -1505,9 +1519,14 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
             w.in = bx.x; w.in_ms = bx.x_ms; w.in_ps = bx.x_ps;   // cat: the staging forms ELU(BN(x))
             w.bnc = bx.coef; w.bnc_ms = bx.coef_ms;
         }
-        DN_TRY(launch_wgrad(w, ly.ks, n, ly.G, s));
+        hipStream_t sw = s;
+        if (s2) {
+            MPO_HIP(p.side.fork(s, s2));
+            sw = s2;
+        }
+        DN_TRY(launch_wgrad(w, ly.ks, n, ly.G, sw));
         const long long cnt = (long long)ly.ks * ly.ks * ly.cin * ly.cout;
-        hipLaunchKernelGGL(dn_wgrad_reduce_kernel, flat_grid(cnt, n), dim3(256), 0, s, (const float*)(p.act + p.part_off),
+        hipLaunchKernelGGL(dn_wgrad_reduce_kernel, flat_grid(cnt, n), dim3(256), 0, sw, (const float*)(p.act + p.part_off),
                            p.part_ms, ly.G, cnt, p.grads, p.n_params, ly.w_off);
         if (ly.kind == K_CONV0) continue;
         // input gradient: 'same' conv of dOut with the rotated, transposed kernel -> dz
@@ -1524,6 +1543,7 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
         bn.accumulate = ly.kind == K_DENSE ? 1 : 0;
         enqueue_bn_bwd(p, bn, i, s);
     }
+    if (s2) MPO_HIP(p.side.join(s, s2));
     MPO_LAUNCH_CHECK();
     return MPO_OK;
 }
@@ -1546,6 +1566,8 @@ int mpo_dn_create(const MpoDnArch* arch, int n_members, int batch, void** handle
     p->arch = *arch;
     p->n = n_members;
     p->B = batch;
+    // A/B switch (one variable, as MPO_POP_PLAN for the MNIST population): streams=1
+    if (const char* e = getenv("MPO_DN_PLAN")) p->side.enabled = strstr(e, "streams=1") == nullptr;
     const int rc = build_plan(*p);
     if (rc != MPO_OK) {
         mpo::set_error("mpo_dn_create: architecture outside the kernels' range (W <= %d, C <= 1024)", kMaxPix);

@@ -56,6 +56,57 @@ struct StreamDeviceScope {
     StreamDeviceScope& operator=(const StreamDeviceScope&) = delete;
 };
 
+// A second stream for independent launches of one step, on the caller's stream's
+// device, forked from / joined into that stream with events (created on first use,
+// re-created if the caller moves to another device).  get() returns nullptr when
+// disabled or when the stream / events cannot be created (the step then runs
+// serially on the caller's stream).
+struct SideStream {
+    bool enabled = true;
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    int device = -1;
+    SideStream() = default;
+    SideStream(const SideStream&) = delete;
+    SideStream& operator=(const SideStream&) = delete;
+    ~SideStream() { release(); }
+    void release() {
+        if (side) (void)hipStreamDestroy(side);
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+        if (ev_join) (void)hipEventDestroy(ev_join);
+        side = nullptr;
+        ev_fork = ev_join = nullptr;
+        device = -1;
+    }
+    hipStream_t get(hipStream_t s) {
+        if (!enabled) return nullptr;
+        int dev = 0;
+        if (hipStreamGetDevice(s, &dev) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+        if (side && dev == device) return side;
+        release();
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(dev);
+        const bool ok = hipStreamCreateWithFlags(&side, hipStreamNonBlocking) == hipSuccess &&
+                        hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) == hipSuccess &&
+                        hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) == hipSuccess;
+        (void)hipSetDevice(cur);
+        if (!ok) { (void)hipGetLastError(); release(); enabled = false; return nullptr; }
+        device = dev;
+        return side;
+    }
+    // s2 starts after everything enqueued on s so far
+    hipError_t fork(hipStream_t s, hipStream_t s2) {
+        if (hipError_t e = hipEventRecord(ev_fork, s)) return e;
+        return hipStreamWaitEvent(s2, ev_fork, 0);
+    }
+    // s continues after everything enqueued on s2 so far
+    hipError_t join(hipStream_t s, hipStream_t s2) {
+        if (hipError_t e = hipEventRecord(ev_join, s2)) return e;
+        return hipStreamWaitEvent(s, ev_join, 0);
+    }
+};
+
 // Static (compile-time) LDS bytes of a kernel, from its code object.
 inline size_t static_lds_bytes(const void* kern) {
     hipFuncAttributes at{};

@@ -156,3 +156,29 @@ def test_trial_evaluator_routes_densenet_specs():
     # every trial trains with the evaluator's lr; the trials differ by their init seeds
     assert all(ev.model_provider.builder(*p).spec(lr=ev.lr).lr == ev.lr for p in ([-3.0], [-2.0]))
     assert len(set(round(f, 6) for f in foms)) == 3
+
+
+def test_side_stream_weight_gradients_bit_identical(monkeypatch):
+    """The weight gradients on a second stream (default) vs one stream
+    (MPO_DN_PLAN=streams=1): the same parameters and BN state, bit for bit,
+    after 3 train steps (reference-grid architecture, 3 members)."""
+    from mpi_opt_amd.densenet import DenseNetArch, DenseNetPopulation, he_uniform_init
+
+    arch = DenseNetArch(img_dim=(32, 32, 3), nb_classes=10, depth=10, nb_dense_block=3, growth_rate=12, nb_filter=16)
+    layers = od.arch_layers(img_dim=(32, 32, 3), nb_classes=10, depth=10, nb_dense_block=3, growth_rate=12,
+                            nb_filter=16)
+    init = [he_uniform_init(layers, 11 + i) for i in range(3)]
+    rng = np.random.RandomState(6)
+    x = torch.from_numpy(rng.rand(64, 32, 32, 3).astype(np.float32)).cuda()
+    y = torch.from_numpy(rng.randint(0, 10, 64).astype(np.int32)).cuda()
+    order = torch.from_numpy(np.stack([rng.permutation(64).astype(np.int32) for _ in range(3)])).cuda()
+    out = []
+    for plan in ("streams=1", "streams=2"):
+        monkeypatch.setenv("MPO_DN_PLAN", plan)
+        pop = DenseNetPopulation(arch, [1e-3, 2e-3, 4e-3], batch=16, init=init)
+        for s in range(3):
+            pop.train_step(x, y, order, s * 16)
+        torch.cuda.synchronize()
+        out.append((pop.params.clone(), pop.state.clone()))
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
