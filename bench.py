@@ -354,10 +354,10 @@ def bench_gp_fit(args, torch, dev, cpu):
            "value": s200["fits_per_s"], "unit": "fits/s", "ms_per_fit": s200["ms_per_fit"],
            "launches_per_fit": s200["launches_per_fit"], "lml": s200["lml"], "dtype": "f64",
            "by_n": {str(k): v for k, v in sizes.items()},
-           "kernel": {"name": "split block sweep (sw_pivot_kernel + sw_update_kernel per 32-wide block, "
-                              "sw_build/alpha/pairs/final)", "ms_per_launch": s200["kernel_ms_per_launch"],
+           "kernel": {"name": "split block sweep (sw_xs_build, one sw_step per 32-wide pivot block, sw_alpha, "
+                              "sw_pairs_final)", "ms_per_launch": s200["kernel_ms_per_launch"],
                       "thetas_per_launch": 3,
-                      "note": "one LML evaluation of 3 thetas = 2 launches per 32-wide pivot block + 5; latency-"
+                      "note": "one LML evaluation of 3 thetas = one launch per 32-wide pivot block + 3; latency-"
                               "bound (the sequential pivot sweeps), not a roofline kernel"}}
     if cpu:
         from oracle import gp_ei as O
