@@ -11,7 +11,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mpi_opt_amd.population import PopulationEngine, TrialSpec, kfold_split, synthetic_mnist  # noqa: E402
 from scripts.train_probe import sample_trials  # noqa: E402
 
-VARIANTS = [v for v in (sys.argv[1:] or ["base"])]
+ARGS = sys.argv[1:]
+SHARD = None
+if ARGS and ARGS[0].startswith("--shard="):     # --shard=K/N: one GPU's LPT share of the population
+    SHARD = tuple(int(v) for v in ARGS.pop(0).split("=", 1)[1].split("/"))
+VARIANTS = [v for v in (ARGS or ["base"])]
 
 
 def members_of(trials, folds=5):
@@ -53,6 +57,11 @@ def run(variant, x, y, order, members, steps=3):
 
 def main():
     members = members_of(sample_trials(64))
+    if SHARD:
+        from mpi_opt_amd.blocks import lpt_assign
+
+        owner = lpt_assign([m.flops_per_sample_train() for m in members], SHARD[1])
+        members = [m for m, o in zip(members, owner) if o == SHARD[0]]
     x, y = synthetic_mnist(60000, seed=0)
     tr = np.stack([kfold_split(60000, 5, i % 5)[0] for i in range(len(members))])
     order = torch.from_numpy(tr).cuda()
