@@ -1535,12 +1535,13 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         m.w3 = palloc((long long)m.K1 * D); m.b3 = palloc(D);
         m.w4 = palloc((long long)D * kClasses); m.b4 = palloc(kClasses);
         m.pend = po;
-        // wgrad sample groups (partial slabs reduced in a fixed order): 4 samples per
-        // conv2 slab, 2 when the population is small (<= 160 members: the conv2 weight
-        // gradient's workgroups would not fill the GPU; r04, 40-member LPT shard 6.75 ->
-        // 6.12 ms per step, 320 members unchanged, profiles/r04/train_probe_spg_i.log);
-        // 4 per conv1 slab (its GEMM is tiny)
-        const int spg2 = std::max(1, plan_knob("wg_spg2", n <= 160 ? 2 : 4));
+        // wgrad sample groups (partial slabs reduced in a fixed order): 2 samples per
+        // conv2 slab (r04: a 40-member population's conv2 weight gradient has too few
+        // workgroups at 4: 6.75 -> 6.12 ms per step, 320 members unchanged 37.48 -> 37.39,
+        // profiles/r04/train_probe_spg_i.log), 4 per conv1 slab (its GEMM is tiny).  A
+        // function of the member only, never of the population: a member's trajectory
+        // must not depend on who trains beside it (isolation tests, chunked populations)
+        const int spg2 = std::max(1, plan_knob("wg_spg2", 2));
         const int spg1 = std::max(1, plan_knob("wg_spg1", 4));
         m.g2 = std::max(1, std::min(B, (B + spg2 - 1) / spg2));
         m.g1 = std::max(1, std::min(B, (B + spg1 - 1) / spg1));

@@ -94,7 +94,7 @@ class TrialSpec:
         return 4 * (batch * per_sample + 8 * n_params)
 
 
-    def hbm_bytes_train_by_kernel(self, batch, spg=(4, 4)):
+    def hbm_bytes_train_by_kernel(self, batch, spg=(4, 2)):
         """Each csrc/cnn.hip kernel family's own minimal HBM bytes for one train step
         of this member (f32; every operand read once and every result written once
         per launch, as ``mpo_pop_train_step`` launches them).  Beyond
