@@ -148,7 +148,10 @@ struct Walk3 {
 // it must be cheap (expm1f here cost the conv and wgrad staging 10-35%).
 __device__ __forceinline__ float bn_elu(float x, float s, float t) {
     const float y = x * s + t;
-    return y > 0.f ? y : __expf(y) - 1.f;
+    // exp of min(y, 0) on every lane and a select (not a branch around the exp for
+    // lanes with y <= 0): the same values, NaN included, and no exec-masked blocks
+    const float e = __expf(y > 0.f ? 0.f : y) - 1.f;
+    return y > 0.f ? y : e;
 }
 
 __device__ __forceinline__ double block_sum(double v, double* red) {
@@ -496,20 +499,33 @@ __global__ __launch_bounds__(kWgWaves * 64) void dn_wgrad3_kernel(WgArgs a) {
 // contiguous in both operands.  Split-K inside the workgroup: every wave holds all
 // MT x NT tiles and streams every 8th k-step straight from global memory (no LDS
 // staging); the 8 partial accumulators are summed through LDS in fixed order.
+// r04: the raw operands of kWg1Depth k-steps are in flight per wave (r03 had one:
+// each k-step waited a full memory latency, 1.8 ms per 32-member launch at 5% of
+// the MFMA rate), the image row of a pixel is tracked by adds instead of a
+// division per k-step, and the BN (scale, shift) per row sits in the LDS; BN + ELU
+// are applied when a k-step is consumed.  Same MFMA sequence per accumulator.
 // ============================================================================
+constexpr int kWg1Depth = 4;
+constexpr int kWg1MaxH = 1024;   // image rows whose BN coefficients dn_wgrad1 keeps in LDS
+
 template <int MT, int NT>
 __global__ __launch_bounds__(kWgWaves * 64) void dn_wgrad1_kernel(WgArgs a) {
     __shared__ __attribute__((aligned(16))) float red[kWgWaves - 1][MT * NT * 4 * 64];
+    __shared__ float bnl[2 * kWg1MaxH];
     const int m = blockIdx.z, grp = blockIdx.y;
     const int Cin = a.Cin, N = a.N;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int krow = lane >> 4, kcol = lane & 15;
-    const int HW = a.H * a.W;
+    const int H = a.H, W = a.W, HW = H * W;
     const int b0 = grp * a.spg, b1 = min(a.B, b0 + a.spg);
     const long long p0 = (long long)b0 * HW, p1 = (long long)b1 * HW;
     const float* z = a.in + m * a.in_ms;
     const float* d = a.dout + m * a.dout_ms;
+    const float* bnc = a.bnc ? a.bnc + m * a.bnc_ms : nullptr;
+    if (bnc)
+        for (int e = tid; e < 2 * H; e += kWgWaves * 64) bnl[e] = bnc[2 * H + e];   // scale rows, then shift rows
+    __syncthreads();
     bool am[MT], bm[NT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) am[i] = i * 16 + kcol < Cin;
@@ -520,41 +536,70 @@ __global__ __launch_bounds__(kWgWaves * 64) void dn_wgrad1_kernel(WgArgs a) {
     for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // k-step s covers pixels [p0 + 4s, p0 + 4s + 4); wave w takes s = w, w + 8, ...
+    // k-step s covers pixels [p0 + 4s, p0 + 4s + 4); wave w takes s = w, w + 8, ...:
+    // this lane's pixel advances by 32 per k-step of the wave; its image row
+    // h = (pixel / W) mod H is carried as (h, column) and advanced by adds
     const long long nsteps = (p1 - p0 + 3) >> 2;
-    float av[2][MT], bv[2][NT];
-    const float* bnc = a.bnc ? a.bnc + m * a.bnc_ms : nullptr;
-    auto ld = [&](long long s, float (&A)[MT], float (&Bv)[NT]) {
+    const long long pl0 = 4LL * wave + krow;                 // lane's pixel offset in the group
+    int col = (int)(pl0 % W), hrow = (int)((pl0 / W) % H);   // once per kernel (b0 * HW is a multiple of W and H * W)
+    const int dstep = 4 * kWgWaves;                          // pixels per wave k-step
+    const int dcol = dstep % W, drow = dstep / W;
+    float zr[kWg1Depth][MT], dr[kWg1Depth][NT];
+    int hr[kWg1Depth];
+    bool okr[kWg1Depth];
+    // loads are unconditional (clamped to the last pixel / channel, the value zeroed
+    // afterwards by a select), so every path has the same loads in flight and the
+    // compiler's vmcnt waits stay kWg1Depth - 1 k-steps behind
+    auto ld = [&](long long s, int slot) {
         const long long p = p0 + 4 * s + krow;
         const bool ok = p < p1;
-        const float* zp = z + p * a.in_ps + kcol;
-        const float* dp = d + p * a.dout_ps + kcol;
-        float sc = 1.f, sh = 0.f;
-        if (bnc && ok) {
-            const int h = (int)(((unsigned)p / (unsigned)a.W) % (unsigned)a.H);   // p < 2^31
-            sc = bnc[2 * a.H + h];
-            sh = bnc[3 * a.H + h];
-        }
+        const long long pc = ok ? p : p1 - 1;
+        okr[slot] = ok;
+        hr[slot] = hrow;
+        const float* zp = z + pc * a.in_ps;
+        const float* dp = d + pc * a.dout_ps;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) zr[slot][i] = zp[min(i * 16 + kcol, Cin - 1)];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) dr[slot][j] = dp[min(j * 16 + kcol, N - 1)];   // raw: zeroed when used
+        // the next k-step of this wave: pixel + 32 (selects, not branches)
+        col += dcol;
+        const bool wrap = col >= W;
+        col = wrap ? col - W : col;
+        hrow += drow + (wrap ? 1 : 0);
+        hrow = hrow >= H ? hrow - H : hrow;
+        if (drow + 1 >= H) hrow %= H;        // images of fewer than 32 pixels (uniform, rare)
+    };
+    auto use = [&](int slot) {
+        float av[MT];
+        // (scale, shift) = (1, 0) and no ELU without BN; a padding lane's value is zero
+        const float sc = bnc ? bnl[hr[slot]] : 1.f, sh = bnc ? bnl[H + hr[slot]] : 0.f;
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
-            const float v = (ok && am[i]) ? zp[i * 16] : 0.f;
-            A[i] = (bnc && ok && am[i]) ? bn_elu(v, sc, sh) : v;
+            const float v = bn_elu(zr[slot][i], sc, sh);
+            av[i] = (okr[slot] && am[i]) ? (bnc ? v : zr[slot][i]) : 0.f;
         }
+        float bv[NT];
 #pragma unroll
-        for (int j = 0; j < NT; ++j) Bv[j] = (ok && bm[j]) ? dp[j * 16] : 0.f;
-    };
-    // A operand: lane (row = lane & 15 = channel c, k = krow = pixel); B: (k = pixel, col = n)
-    long long s = wave;
-    if (s < nsteps) ld(s, av[0], bv[0]);
-    int cur = 0;
-    for (; s < nsteps; s += kWgWaves) {
-        if (s + kWgWaves < nsteps) ld(s + kWgWaves, av[cur ^ 1], bv[cur ^ 1]);
+        for (int j = 0; j < NT; ++j) bv[j] = (okr[slot] && bm[j]) ? dr[slot][j] : 0.f;
 #pragma unroll
         for (int i = 0; i < MT; ++i)
 #pragma unroll
             for (int j = 0; j < NT; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[cur][i], bv[cur][j], acc[i][j], 0, 0, 0);
-        cur ^= 1;
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    };
+    // this wave's k-steps t = 0 .. nw-1 (s = wave + 8 t), kWg1Depth in flight; the loop
+    // runs whole groups of kWg1Depth: steps past nw are all padding lanes (zero A and
+    // B), exact no-ops on the accumulators
+    const long long nw = nsteps > wave ? (nsteps - wave + kWgWaves - 1) / kWgWaves : 0;
+#pragma unroll
+    for (int u = 0; u < kWg1Depth; ++u) ld(wave + (long long)kWgWaves * u, u);
+    for (long long t = 0; t < nw; t += kWg1Depth) {
+#pragma unroll
+        for (int u = 0; u < kWg1Depth; ++u) {
+            use(u);
+            ld(wave + (long long)kWgWaves * (t + u + kWg1Depth), u);
+        }
     }
     if (wave > 0) {
         float* r = red[wave - 1];
@@ -1297,6 +1342,7 @@ int launch_wgrad(const WgArgs& a, int ks, int n_members, int G, hipStream_t s) {
     if (ks == 1) {
         const int mt = (a.Cin + 15) / 16;
         if (mt > 4 || nt > 4) { mpo::set_error("dn_wgrad1: cin %d / cout %d > 64 unsupported", a.Cin, a.N); return MPO_ENOTSUP; }
+        if (a.H > kWg1MaxH) { mpo::set_error("dn_wgrad1: %d image rows > %d unsupported", a.H, kWg1MaxH); return MPO_ENOTSUP; }
         const dim3 grid(1, G, n_members);
         switch (mt) {
             case 1: launch_wg1_mt<1>(a, grid, nt, s); break;
