@@ -175,8 +175,10 @@ class _LbfgsbRun:
                    self.iwa, task, self.lsave, self.isave, self.dsave, self.maxls, self.ln_task)
             t0 = task[0]
             if t0 == 3:
-                # ScalarFunction's cache: the same x (np.array_equal of same-shape float arrays)
-                if self.sf_x is not None and bool((self.x == self.sf_x).all()):
+                # ScalarFunction's cache: the same x (np.array_equal of same-shape float
+                # arrays: elementwise ==, so -0.0 == 0.0 and NaN != NaN -- as Python float
+                # equality on fresh float objects, ~10x cheaper than the ufunc reduction)
+                if self.sf_x is not None and self.x.tolist() == self.sf_x.tolist():
                     self.f, self.g = self.sf_f, self.sf_g
                     continue
                 return self.x.copy()
@@ -202,10 +204,14 @@ def lbfgsb_batched(evaluate, starts, bounds, ftol=MINIMIZE_FTOL, gtol=1e-5, maxi
     setulb = _setulb()
     runs = [_LbfgsbRun(x0, bounds, ftol, gtol, maxiter, maxfun) for x0 in starts]
     want = {i: r.request() for i, r in enumerate(runs)}
+    buf = np.empty((len(runs), runs[0].x.size), dtype=np.float64)   # the round's points (no np.stack)
     rounds = 0
     while want:
         ids = sorted(want)
-        f, g = evaluate(np.stack([want[i] for i in ids]), ids)
+        X = buf[:len(ids)]
+        for k, i in enumerate(ids):
+            X[k] = want[i]
+        f, g = evaluate(X, ids)
         rounds += 1
         g = np.asarray(g, dtype=np.float64)
         for k, i in enumerate(ids):
