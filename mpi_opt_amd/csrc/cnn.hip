@@ -1630,8 +1630,7 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         tiles(P.d1d, B, m.K1);
         P.per_member.push_back({i, 0});
         for (int c = 2; c < 4; ++c) P.colsum.push_back({i, c});
-        P.wred.push_back({i, 0});
-        P.wred.push_back({i, 1});
+        P.wred.push_back({i, 1});   // conv2 slabs: items [0, n) (reduced on the side stream)
         const long long np_ = m.pend - m.w1;
         for (long long c = 0; c * P.adam_chunk < np_; ++c) P.adam.push_back({i, (int)c});
     }
@@ -1639,6 +1638,7 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         mpo::set_error("mpo_pop_create: LDS plan exceeds 160 KiB (conv %zu, wgrad %zu)", P.lds_conv_max, P.lds_wg_max);
         return MPO_ENOTSUP;
     }
+    for (int i = 0; i < n; ++i) P.wred.push_back({i, 0});   // conv1 slabs: items [n, 2n)
     long long wmax = 0;
     for (auto& m : P.mem) wmax = std::max(wmax, (long long)m.k * m.k * m.F * m.F + m.F);
     P.wred_blocks = (int)((wmax + P.wred_per_block - 1) / P.wred_per_block);
@@ -1930,32 +1930,53 @@ int mpo_pop_train_step(void* handle, const float* x, const int32_t* labels, cons
     a.loss_out = loss_out;
     int rc = forward(P, a, s);
     if (rc) return rc;
-    // backward
-    MPO_HIP(launch_dense<D2_WGRAD>(P, a, P.off_d2w, P.d2w.size(), s));
-    MPO_HIP(launch_dense<D2_DGRAD>(P, a, P.off_d2d, P.d2d.size(), s));
-    MPO_HIP(launch_dense<D1_WGRAD>(P, a, P.off_d1w, P.d1w.size(), s));
-    MPO_HIP(launch_dense<D1_DGRAD>(P, a, P.off_d1d, P.d1d.size(), s));
+    // backward.  With the side stream s2: each weight gradient runs on s2 beside the
+    // input gradient that follows it on s (disjoint outputs; s2 stays one stream, so
+    // its work keeps its own order), the conv2 slab reduction right after the conv2
+    // weight gradient, and s joins s2 before Adam.
+    hipStream_t s2 = P.timer.on ? nullptr : P.side.get(s);
+    const MItem* wred = dev_table<MItem>(P, P.off_wr);
+    const unsigned nm = (unsigned)P.n;
+    if (s2) {
+        MPO_HIP(P.side.fork(s, s2));                                        // dz3 ready
+        MPO_HIP(launch_dense<D2_WGRAD>(P, a, P.off_d2w, P.d2w.size(), s2));
+        MPO_HIP(launch_dense<D2_DGRAD>(P, a, P.off_d2d, P.d2d.size(), s));
+        MPO_HIP(P.side.fork(s, s2));                                        // dh ready
+        MPO_HIP(launch_dense<D1_WGRAD>(P, a, P.off_d1w, P.d1w.size(), s2));
+        MPO_HIP(launch_dense<D1_DGRAD>(P, a, P.off_d1d, P.d1d.size(), s));
+    } else {
+        MPO_HIP(launch_dense<D2_WGRAD>(P, a, P.off_d2w, P.d2w.size(), s));
+        MPO_HIP(launch_dense<D2_DGRAD>(P, a, P.off_d2d, P.d2d.size(), s));
+        MPO_HIP(launch_dense<D1_WGRAD>(P, a, P.off_d1w, P.d1w.size(), s));
+        MPO_HIP(launch_dense<D1_DGRAD>(P, a, P.off_d1d, P.d1d.size(), s));
+    }
     P.timer.mark("dense_bwd", s);
     hipLaunchKernelGGL(pool_bwd_kernel, dim3((unsigned)P.per_sample.size()), dim3(256), 0, s, a,
                        dev_table<MItem>(P, P.off_ps));
     MPO_LAUNCH_CHECK();
     P.timer.mark("pool_bwd", s);
-    if (hipStream_t s2 = P.timer.on ? nullptr : P.side.get(s)) {
-        // conv2 weight gradient (a1, dz2 -> slabs) beside the input gradient and the
-        // conv1 weight gradient (dz2 -> dz1 -> slabs): disjoint outputs
-        MPO_HIP(P.side.fork(s, s2));
+    if (s2) {
+        // conv2 weight gradient (a1, dz2 -> slabs -> dw2) beside the input gradient and
+        // the conv1 weight gradient (dz2 -> dz1 -> slabs -> dw1): disjoint outputs
+        MPO_HIP(P.side.fork(s, s2));                                        // dz2 ready
         MPO_HIP(launch_wg<WG_CONV2>(P, a, P.off_wg2, P.bw2, s2));
+        hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)P.wred_blocks, nm), dim3(256), 0, s2, a, wred,
+                           P.wred_per_block);
+        MPO_LAUNCH_CHECK();
         MPO_HIP(launch_dgrad(P, a, s));
         MPO_HIP(launch_wg<WG_CONV1>(P, a, P.off_wg1, P.bw1, s));
+        hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)P.wred_blocks, nm), dim3(256), 0, s, a, wred + nm,
+                           P.wred_per_block);
+        MPO_LAUNCH_CHECK();
         MPO_HIP(P.side.join(s, s2));
     } else {
         MPO_HIP(launch_dgrad(P, a, s));
         MPO_HIP(launch_wg<WG_CONV2>(P, a, P.off_wg2, P.bw2, s));
         MPO_HIP(launch_wg<WG_CONV1>(P, a, P.off_wg1, P.bw1, s));
+        hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)P.wred_blocks, 2 * nm), dim3(256), 0, s, a, wred,
+                           P.wred_per_block);
+        MPO_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)P.wred_blocks, (unsigned)P.wred.size()), dim3(256), 0, s, a,
-                       dev_table<MItem>(P, P.off_wr), P.wred_per_block);
-    MPO_LAUNCH_CHECK();
     hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)P.colsum.size()), dim3(256), 0, s, a, dev_table<MItem>(P, P.off_cs));
     MPO_LAUNCH_CHECK();
     P.timer.mark("wgrad_reduce", s);
