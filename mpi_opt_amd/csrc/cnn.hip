@@ -1388,7 +1388,7 @@ int env_int(const char* name, int dflt) {
 }
 
 // Planner overrides for tuning sweeps, one variable: MPO_POP_PLAN="key=value,..."
-// (keys: dg_tiles, dg_kb, conv_mt, conv_kb1, conv_kb2, wg_spg1, wg_spg2, streams).  Every
+// (keys: dg_tiles, dg_kb, conv_mt, conv_kb1, conv_kb2, wg_spg1, wg_spg2, streams = 1 | 2 | 3).  Every
 // value only changes how work is cut into items or ordered over streams, never the arithmetic.
 int plan_knob(const char* key, int dflt) {
     const char* v = getenv("MPO_POP_PLAN");
@@ -1435,6 +1435,7 @@ struct Plan {
     // runs beside the input gradient + conv1 weight gradient, so one launch's tail
     // overlaps the other's work.  No two concurrent kernels write the same buffer.
     mpo::SideStream side;
+    mpo::SideStream side2;   // a third stream: the input-gradient buckets alternate over s and it
 };
 
 size_t conv_lds_bytes(int rows, int Wp, int Cin, int Ho, int K, int nt) {
@@ -1578,7 +1579,8 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         const Member& m = P.mem[i];
         const int k = m.k, F = m.F, nt = m.nt;
         if (i == 0) P.conv_mt = plan_knob("conv_mt", 4) == 2 ? 2 : 4;
-        if (i == 0) P.side.enabled = plan_knob("streams", 2) >= 2;
+        if (i == 0) P.side.enabled = plan_knob("streams", 3) >= 2;
+        if (i == 0) P.side2.enabled = plan_knob("streams", 3) >= 3;
         const int mcap = P.conv_mt * 64;   // 4 waves x conv_mt m-tiles of 16 pixels
         const int R1 = choose_rows(m.H1, [&](int R) { return conv_lds_bytes(R + k - 1, kImg, 1, m.H1, k * k, nt); }, kc1, kc2, mcap);
         const int R2 = choose_rows(m.H2, [&](int R) { return conv_lds_bytes(R + k - 1, m.H1, F, m.H2, k * k * F, nt); }, kc1, kc2, mcap);
@@ -1759,11 +1761,11 @@ hipError_t launch_conv(Plan& P, const StepArgs& a, size_t table_off, const Bucke
     }, s2);
 }
 
-hipError_t launch_dgrad(Plan& P, const StepArgs& a, hipStream_t s) {
+hipError_t launch_dgrad(Plan& P, const StepArgs& a, hipStream_t s, hipStream_t s2 = nullptr) {
     const ConvItem* base = dev_table<ConvItem>(P, P.off_dgrad);
     return launch_segs(P, P.bdg, "conv2_dgrad", s, [&](const Seg& sg, hipStream_t st) {
         return MPO_NT_SWITCH(launch_dgrad_nt, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, st);
-    });
+    }, s2);
 }
 
 template <int OP>
@@ -1963,7 +1965,13 @@ int mpo_pop_train_step(void* handle, const float* x, const int32_t* labels, cons
         hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)P.wred_blocks, nm), dim3(256), 0, s2, a, wred,
                            P.wred_per_block);
         MPO_LAUNCH_CHECK();
-        MPO_HIP(launch_dgrad(P, a, s));
+        if (hipStream_t s3 = P.side2.get(s)) {   // input-gradient buckets over s and s3 (disjoint rows of dz1)
+            MPO_HIP(P.side2.fork(s, s3));
+            MPO_HIP(launch_dgrad(P, a, s, s3));
+            MPO_HIP(P.side2.join(s, s3));
+        } else {
+            MPO_HIP(launch_dgrad(P, a, s));
+        }
         MPO_HIP(launch_wg<WG_CONV1>(P, a, P.off_wg1, P.bw1, s));
         hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)P.wred_blocks, nm), dim3(256), 0, s, a, wred + nm,
                            P.wred_per_block);

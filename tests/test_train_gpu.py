@@ -230,19 +230,21 @@ def test_unsupported_options_are_refused():
 
 
 def test_side_stream_schedule_is_bit_identical(monkeypatch):
-    """MPO_POP_PLAN streams=2 (default: conv2 forward buckets over two streams, the
-    conv2 weight gradient beside the input gradient) vs streams=1 (one stream):
-    the same parameters, bit for bit, after 3 train steps of the mixed population."""
+    """MPO_POP_PLAN streams=3 (default: conv2 forward buckets over two streams, the
+    weight gradients beside the input gradients, the input-gradient buckets over a
+    third), streams=2 and streams=1 (one stream): the same parameters, bit for bit,
+    after 3 train steps of the mixed population."""
     x, y = dataset(5)
     xd, yd = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
     tr, _ = orders(MEMBERS, x)
     otr = torch.from_numpy(tr).cuda()
     out = []
-    for streams in ("1", "2"):
+    for streams in ("1", "2", "3"):
         monkeypatch.setenv("MPO_POP_PLAN", f"streams={streams}")
         eng, _, _ = make_engine()
         losses = [eng.train_step(xd, yd, otr, st * BATCH).cpu().numpy().copy() for st in range(3)]
         torch.cuda.synchronize()
         out.append((np.stack(losses), eng.params.cpu().numpy().copy()))
-    np.testing.assert_array_equal(out[0][0], out[1][0])
-    np.testing.assert_array_equal(out[0][1], out[1][1])
+    for k in (1, 2):
+        np.testing.assert_array_equal(out[0][0], out[k][0])
+        np.testing.assert_array_equal(out[0][1], out[k][1])
