@@ -35,6 +35,7 @@
 #include "mpo_internal.h"
 
 #include <algorithm>
+#include <cstring>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -167,13 +168,14 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 
 // ============================================================================
 // Implicit-GEMM 'same' convolution, stride 1 (forward and input gradient).
-// One workgroup = (member, sample b, output rows [y0, y0 + R)); M = R*W <= 128
-// pixels in up to 8 m-tiles of 16 (2 per wave), N = NT tiles of 16.
+// One workgroup = (member, sample b, output rows [y0, y0 + R)); M = R*W <= 128 or
+// 256 pixels in up to 8 or 16 m-tiles of 16 (MTX = 2 or 4 per wave), N = NT tiles
+// of 16.  The wave's live m-tiles MT <= MTX are a template parameter of the loop.
 // ============================================================================
-template <int MT, int NT>
+template <int MT, int NT, int MTX>
 __device__ __forceinline__ void dn_conv_loop(const float* __restrict__ img, const int* __restrict__ koff,
-                                             const float* __restrict__ Wt, int N16, int ngroups, const int (&pb)[2],
-                                             f32x4 (&acc)[2][NT], int krow, int kcol) {
+                                             const float* __restrict__ Wt, int N16, int ngroups, const int (&pb)[MTX],
+                                             f32x4 (&acc)[MTX][NT], int krow, int kcol) {
     const float* wsrc = Wt + krow * N16 + kcol;
     const int* kp = koff + krow * 4;
     float b0[4][NT], b1[4][NT], a0[4][MT], a1[4][MT];
@@ -222,7 +224,9 @@ __device__ __forceinline__ void dn_conv_loop(const float* __restrict__ img, cons
     }
 }
 
-template <int KS, int NT>
+// MTX: m-tiles per wave at most (2: <= 128 pixels per workgroup; 4: <= 256, so every
+// weight fragment feeds up to 4 NT MFMAs -- the growth convs have NT = 1)
+template <int KS, int NT, int MTX>
 __global__ __launch_bounds__(256) void dn_conv_kernel(ConvArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int P = (KS - 1) / 2;
@@ -269,29 +273,38 @@ __global__ __launch_bounds__(256) void dn_conv_kernel(ConvArgs a) {
     }
     const int Mc = rows_out * W;
     const int mtiles = (Mc + 15) >> 4;
-    const int mine = __builtin_amdgcn_readfirstlane(mtiles > wave + 4 ? 2 : (mtiles > wave ? 1 : 0));
-    int pb[2];
+    // m-tile t is wave t % 4's slot t / 4
+    const int mine = __builtin_amdgcn_readfirstlane(mtiles > wave ? min(MTX, (mtiles - wave + 3) >> 2) : 0);
+    int pb[MTX];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < MTX; ++i) {
         const int mm = (wave + 4 * i) * 16 + (lane & 15);
         pb[i] = mm < Mc ? ((mm / W) * Wp + (mm % W)) * Cp : 0;
     }
-    f32x4 acc[2][NT];
+    f32x4 acc[MTX][NT];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MTX; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     __syncthreads();
     const int ngroups = K16 >> 4;
     const float* Wt = a.w + m * a.w_ms;
     const int N16 = NT * 16;
-    if (mine == 2) dn_conv_loop<2, NT>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
-    else if (mine == 1) dn_conv_loop<1, NT>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
-    else return;
+    if constexpr (MTX == 4) {
+        if (mine == 4) dn_conv_loop<4, NT, MTX>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
+        else if (mine == 3) dn_conv_loop<3, NT, MTX>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
+        else if (mine == 2) dn_conv_loop<2, NT, MTX>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
+        else if (mine == 1) dn_conv_loop<1, NT, MTX>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
+        else return;
+    } else {
+        if (mine == 2) dn_conv_loop<2, NT, MTX>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
+        else if (mine == 1) dn_conv_loop<1, NT, MTX>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
+        else return;
+    }
 
     float* dst = a.out + m * a.out_ms + ((long long)b * H + y0) * W * a.out_ps;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < MTX; ++i) {
         if (i >= mine) break;
         const int mt = wave + 4 * i;
 #pragma unroll
@@ -1109,7 +1122,7 @@ struct Layer {
     long long wf_off = -1, wd_off_act = -1;    // padded fwd / dgrad weights (act arena)
     int wf_rows = 0, wf_n16 = 0, wd_rows = 0, wd_n16 = 0;
     long long z_off = -1, t_off = -1, coef_off = -1;
-    int G = 1, spg = 1, R = 1, Rw = 1;
+    int G = 1, spg = 1, R = 1, Rd = 1, Rw = 1;   // row chunks: forward conv, input-gradient conv, wgrad
 };
 
 struct DnPlan {
@@ -1157,6 +1170,23 @@ int rows_per_chunk(int H, int W) { return std::max(1, std::min(H, kMaxPix / std:
 size_t conv_lds(int R, int W, int ks, int cin) {
     const int img = (R + ks - 1) * (W + ks - 1) * conv_cp(cin);
     return (size_t)(r4(img) + r16(ks * ks * r4(cin)) + kKoffSlack) * sizeof(float);
+}
+
+// Conv row chunk: up to 2 kMaxPix pixels (4 m-tiles per wave: every weight fragment
+// feeds up to 4 NT MFMAs) while the staged rows fit kConvPixBudget of LDS (two
+// workgroups per CU), else up to kMaxPix.  MPO_DN_PLAN="conv_px=128" keeps kMaxPix.
+constexpr size_t kConvPixBudget = 64 << 10;
+// (Only for N <= 48 output channels: with 4 m-tiles x NT > 3 tiles the accumulators
+// alone cap the occupancy at 1-2 waves per SIMD.)
+int conv_rows(int H, int W, int ks, int cin, int N) {
+    const int R1 = rows_per_chunk(H, W);
+    int px = 2 * kMaxPix;
+    if (const char* e = getenv("MPO_DN_PLAN")) {
+        if (const char* q = strstr(e, "conv_px=")) px = atoi(q + 8);
+    }
+    if (px <= kMaxPix || N > 48) return R1;
+    const int R2 = std::max(1, std::min(H, px / std::max(1, W)));
+    return R2 > R1 && conv_lds(R2, W, ks, cin) <= kConvPixBudget ? R2 : R1;
 }
 
 size_t wg_lds(int R, int W, int ks, int cin, int nt) {
@@ -1251,8 +1281,10 @@ int build_plan(DnPlan& p) {
                 ly.wd_rows = r16(taps * r4(ly.cout)) + kWRowsSlack;
                 ly.wd_off_act = ar.take((long long)ly.wd_rows * ly.wd_n16, &ms);
             }
-            ly.R = rows_per_chunk(ly.H, ly.W);
-            ly.Rw = ly.R;
+            ly.Rw = rows_per_chunk(ly.H, ly.W);
+            // forward conv (N = cout over cin channels) and input-gradient conv (N = cin over cout)
+            ly.R = conv_rows(ly.H, ly.W, ly.ks, ly.cin, ly.cout);
+            ly.Rd = conv_rows(ly.H, ly.W, ly.ks, ly.cout, ly.cin);
             const long long Kw = (long long)taps * ly.cin;
             const int mgroups = ly.ks == 1 ? 1 : (int)((Kw + kWgRows - 1) / kWgRows);
             const int gt = std::max(1, (target + mgroups * p.n - 1) / (mgroups * p.n));
@@ -1294,10 +1326,19 @@ int build_plan(DnPlan& p) {
 }
 
 template <int KS, int NT>
-void launch_conv_t(const ConvArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-    auto kern = dn_conv_kernel<KS, NT>;
+int launch_conv_t(const ConvArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+    auto kern = dn_conv_kernel<KS, NT, 2>;
+    if (a.R * a.W > kMaxPix) {   // 256-pixel items (conv_rows: only for N <= 48)
+        if constexpr (NT <= 3) {
+            kern = dn_conv_kernel<KS, NT, 4>;
+        } else {
+            mpo::set_error("dn_conv: %d-pixel chunks need N <= 48 (got %d)", a.R * a.W, a.N);
+            return MPO_ENOTSUP;
+        }
+    }
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a);
+    return MPO_OK;
 }
 
 template <int NT>
@@ -1314,15 +1355,14 @@ int launch_conv(const ConvArgs& a, int n_members, int B, hipStream_t s) {
     size_t lds = conv_lds(a.R, a.W, KS, a.Cin);
     if (lds > ((size_t)160 << 10)) { mpo::set_error("dn_conv: LDS %zu B exceeds 160 KiB", lds); return MPO_ENOTSUP; }
     switch (nt) {
-        case 1: launch_conv_t<KS, 1>(a, grid, lds, s); break;
-        case 2: launch_conv_t<KS, 2>(a, grid, lds, s); break;
-        case 3: launch_conv_t<KS, 3>(a, grid, lds, s); break;
-        case 4: launch_conv_t<KS, 4>(a, grid, lds, s); break;
-        case 5: launch_conv_t<KS, 5>(a, grid, lds, s); break;
-        case 6: launch_conv_t<KS, 6>(a, grid, lds, s); break;
+        case 1: return launch_conv_t<KS, 1>(a, grid, lds, s);
+        case 2: return launch_conv_t<KS, 2>(a, grid, lds, s);
+        case 3: return launch_conv_t<KS, 3>(a, grid, lds, s);
+        case 4: return launch_conv_t<KS, 4>(a, grid, lds, s);
+        case 5: return launch_conv_t<KS, 5>(a, grid, lds, s);
+        case 6: return launch_conv_t<KS, 6>(a, grid, lds, s);
         default: mpo::set_error("dn_conv: %d output channels unsupported (max 96)", a.N); return MPO_ENOTSUP;
     }
-    return MPO_OK;
 }
 
 // 1x1 weight gradient: MT x NT tiles per wave (<= 6 x 6, i.e. cin, cout <= 96)
@@ -1581,7 +1621,7 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
         c.in = dout; c.in_ms = dout_ms; c.in_ps = dout_ps;
         c.w = p.act + ly.wd_off_act; c.w_ms = ((long long)ly.wd_rows * ly.wd_n16 + 63) & ~63LL;
         c.out = p.act + p.dz_off; c.out_ms = p.dz_ms; c.out_ps = ly.cin;
-        c.H = ly.H; c.W = ly.W; c.Cin = ly.cout; c.N = ly.cin; c.R = ly.R;
+        c.H = ly.H; c.W = ly.W; c.Cin = ly.cout; c.N = ly.cin; c.R = ly.Rd;
         if (ly.ks == 3) DN_TRY(launch_conv<3>(c, n, B, s));
         else DN_TRY(launch_conv<1>(c, n, B, s));
         bn.dz = p.act + p.dz_off; bn.dz_ms = p.dz_ms;
@@ -1622,7 +1662,7 @@ int mpo_dn_create(const MpoDnArch* arch, int n_members, int batch, void** handle
     for (auto& ly : p->layers) {
         if (ly.kind == K_HEAD) continue;
         if (conv_lds(ly.R, ly.W, ly.ks, ly.cin) > ((size_t)160 << 10) ||
-            conv_lds(ly.R, ly.W, ly.ks, ly.cout) > ((size_t)160 << 10) ||
+            conv_lds(ly.Rd, ly.W, ly.ks, ly.cout) > ((size_t)160 << 10) ||
             wg_lds(ly.Rw, ly.W, ly.ks, ly.cin, (ly.cout + 15) / 16) > ((size_t)160 << 10) || ly.cout > 64 ||
             (ly.kind != K_CONV0 && ly.cin > 96) || (ly.ks == 1 && ly.cin > 64)) {
             mpo::set_error("mpo_dn_create: layer (cin %d, cout %d, %dx%d) exceeds the kernels' LDS / channel range",
