@@ -35,7 +35,6 @@
 #include "mpo_internal.h"
 
 #include <algorithm>
-#include <cstring>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -166,16 +165,19 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
     return s;
 }
 
+// elements per thread in flight in the conv / wgrad LDS staging loops
+constexpr int kStageU = 4;
+constexpr int kWgStageU = 2;   // dn_wgrad3: 4 would cost it an occupancy step (129 VGPRs)
+
 // ============================================================================
 // Implicit-GEMM 'same' convolution, stride 1 (forward and input gradient).
-// One workgroup = (member, sample b, output rows [y0, y0 + R)); M = R*W <= 128 or
-// 256 pixels in up to 8 or 16 m-tiles of 16 (MTX = 2 or 4 per wave), N = NT tiles
-// of 16.  The wave's live m-tiles MT <= MTX are a template parameter of the loop.
+// One workgroup = (member, sample b, output rows [y0, y0 + R)); M = R*W <= 128
+// pixels in up to 8 m-tiles of 16 (2 per wave), N = NT tiles of 16.
 // ============================================================================
-template <int MT, int NT, int MTX>
+template <int MT, int NT>
 __device__ __forceinline__ void dn_conv_loop(const float* __restrict__ img, const int* __restrict__ koff,
-                                             const float* __restrict__ Wt, int N16, int ngroups, const int (&pb)[MTX],
-                                             f32x4 (&acc)[MTX][NT], int krow, int kcol) {
+                                             const float* __restrict__ Wt, int N16, int ngroups, const int (&pb)[2],
+                                             f32x4 (&acc)[2][NT], int krow, int kcol) {
     const float* wsrc = Wt + krow * N16 + kcol;
     const int* kp = koff + krow * 4;
     float b0[4][NT], b1[4][NT], a0[4][MT], a1[4][MT];
@@ -224,9 +226,7 @@ __device__ __forceinline__ void dn_conv_loop(const float* __restrict__ img, cons
     }
 }
 
-// MTX: m-tiles per wave at most (2: <= 128 pixels per workgroup; 4: <= 256, so every
-// weight fragment feeds up to 4 NT MFMAs -- the growth convs have NT = 1)
-template <int KS, int NT, int MTX>
+template <int KS, int NT>
 __global__ __launch_bounds__(256) void dn_conv_kernel(ConvArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int P = (KS - 1) / 2;
@@ -248,16 +248,71 @@ __global__ __launch_bounds__(256) void dn_conv_kernel(ConvArgs a) {
     const int krow = lane >> 4, kcol = lane & 15;
 
     const float* bnc = a.bnc ? a.bnc + m * a.bnc_ms : nullptr;
-    Walk3 wk(tid, Wp, Cp, 256);
-    for (int e = tid; e < img_elems; e += 256, wk.next()) {
-        const int r = wk.r, col = wk.x, c = wk.c;
-        const int gy = y0 + r - P, gx = col - P;
-        float v = 0.f;
-        if (gy >= 0 && gy < H && gx >= 0 && gx < W && c < Cin) {
-            v = src[((long long)gy * W + gx) * a.in_ps + c];
-            if (bnc) v = bn_elu(v, bnc[2 * H + gy], bnc[3 * H + gy]);   // zero padding stays zero
+    // Staging: kStageU elements per thread in flight -- the loads are unconditional
+    // (out-of-image taps read a clamped in-bounds address) and the zero padding is
+    // selected when the value is used, so a thread issues kStageU loads before its
+    // first wait instead of one load per dependent round trip.
+    const bool vin = ((Cin & 3) == 0) && ((a.in_ps & 3) == 0) && ((reinterpret_cast<uintptr_t>(src) & 15) == 0);
+    if (vin) {
+        // float4 channel groups; the padding channels [Cin, Cp) are never read by
+        // the k loop (koff covers c < Cin4 == Cin), so only the halo is zeroed
+        const int C4 = Cin >> 2, tot = rows * Wp * C4;
+        Walk3 wk(tid, Wp, C4, 256);
+        for (int e0 = tid; e0 < tot; e0 += kStageU * 256) {
+            float4 v[kStageU];
+            float sc[kStageU], sh[kStageU];
+            int dst[kStageU];
+            bool ok[kStageU];
+#pragma unroll
+            for (int u = 0; u < kStageU; ++u) {
+                const int gy = y0 + wk.r - P, gx = wk.x - P;
+                ok[u] = e0 + u * 256 < tot && gy >= 0 && gy < H && gx >= 0 && gx < W;
+                const int cy = ok[u] ? gy : 0, cx = ok[u] ? gx : 0, c4 = ok[u] ? wk.c : 0;
+                v[u] = *reinterpret_cast<const float4*>(src + ((long long)cy * W + cx) * a.in_ps + 4 * c4);
+                if (bnc) {
+                    sc[u] = bnc[2 * H + cy];
+                    sh[u] = bnc[3 * H + cy];
+                }
+                dst[u] = e0 + u * 256 < tot ? (wk.r * Wp + wk.x) * Cp + 4 * wk.c : -1;
+                wk.next();
+            }
+#pragma unroll
+            for (int u = 0; u < kStageU; ++u) {
+                float4 x = v[u];
+                if (bnc)
+                    x = make_float4(bn_elu(x.x, sc[u], sh[u]), bn_elu(x.y, sc[u], sh[u]), bn_elu(x.z, sc[u], sh[u]),
+                                    bn_elu(x.w, sc[u], sh[u]));
+                if (!ok[u]) x = make_float4(0.f, 0.f, 0.f, 0.f);   // zero padding stays zero
+                if (dst[u] >= 0) {   // Cp even: 8-byte aligned pairs
+                    *reinterpret_cast<float2*>(img + dst[u]) = make_float2(x.x, x.y);
+                    *reinterpret_cast<float2*>(img + dst[u] + 2) = make_float2(x.z, x.w);
+                }
+            }
         }
-        img[e] = v;
+    } else {
+        Walk3 wk(tid, Wp, Cp, 256);
+        for (int e0 = tid; e0 < img_elems; e0 += kStageU * 256) {
+            float v[kStageU], sc[kStageU], sh[kStageU];
+            bool ok[kStageU];
+#pragma unroll
+            for (int u = 0; u < kStageU; ++u) {
+                const int gy = y0 + wk.r - P, gx = wk.x - P;
+                ok[u] = e0 + u * 256 < img_elems && gy >= 0 && gy < H && gx >= 0 && gx < W && wk.c < Cin;
+                const int cy = ok[u] ? gy : 0, cx = ok[u] ? gx : 0, c = ok[u] ? wk.c : 0;
+                v[u] = src[((long long)cy * W + cx) * a.in_ps + c];
+                if (bnc) {
+                    sc[u] = bnc[2 * H + cy];
+                    sh[u] = bnc[3 * H + cy];
+                }
+                wk.next();
+            }
+#pragma unroll
+            for (int u = 0; u < kStageU; ++u) {
+                float x = v[u];
+                if (bnc) x = bn_elu(x, sc[u], sh[u]);
+                if (e0 + u * 256 < img_elems) img[e0 + u * 256] = ok[u] ? x : 0.f;
+            }
+        }
     }
     // tap offsets, each 16-k group stored as [krow][u] so a lane reads its four
     // k-steps (k = g*16 + u*4 + krow) as one b128
@@ -273,38 +328,29 @@ __global__ __launch_bounds__(256) void dn_conv_kernel(ConvArgs a) {
     }
     const int Mc = rows_out * W;
     const int mtiles = (Mc + 15) >> 4;
-    // m-tile t is wave t % 4's slot t / 4
-    const int mine = __builtin_amdgcn_readfirstlane(mtiles > wave ? min(MTX, (mtiles - wave + 3) >> 2) : 0);
-    int pb[MTX];
+    const int mine = __builtin_amdgcn_readfirstlane(mtiles > wave + 4 ? 2 : (mtiles > wave ? 1 : 0));
+    int pb[2];
 #pragma unroll
-    for (int i = 0; i < MTX; ++i) {
+    for (int i = 0; i < 2; ++i) {
         const int mm = (wave + 4 * i) * 16 + (lane & 15);
         pb[i] = mm < Mc ? ((mm / W) * Wp + (mm % W)) * Cp : 0;
     }
-    f32x4 acc[MTX][NT];
+    f32x4 acc[2][NT];
 #pragma unroll
-    for (int i = 0; i < MTX; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     __syncthreads();
     const int ngroups = K16 >> 4;
     const float* Wt = a.w + m * a.w_ms;
     const int N16 = NT * 16;
-    if constexpr (MTX == 4) {
-        if (mine == 4) dn_conv_loop<4, NT, MTX>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
-        else if (mine == 3) dn_conv_loop<3, NT, MTX>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
-        else if (mine == 2) dn_conv_loop<2, NT, MTX>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
-        else if (mine == 1) dn_conv_loop<1, NT, MTX>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
-        else return;
-    } else {
-        if (mine == 2) dn_conv_loop<2, NT, MTX>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
-        else if (mine == 1) dn_conv_loop<1, NT, MTX>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
-        else return;
-    }
+    if (mine == 2) dn_conv_loop<2, NT>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
+    else if (mine == 1) dn_conv_loop<1, NT>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
+    else return;
 
     float* dst = a.out + m * a.out_ms + ((long long)b * H + y0) * W * a.out_ps;
 #pragma unroll
-    for (int i = 0; i < MTX; ++i) {
+    for (int i = 0; i < 2; ++i) {
         if (i >= mine) break;
         const int mt = wave + 4 * i;
 #pragma unroll
@@ -430,21 +476,36 @@ __global__ __launch_bounds__(kWgWaves * 64) void dn_wgrad3_kernel(WgArgs a) {
             const int Mc = min(R, H - y0) * W;
             __syncthreads();   // the previous chunk's MFMAs are done with the LDS (and the zero fill)
             if (vin) {
+                // kWgStageU float4 loads in flight per thread (clamped, zeroed when used)
                 const int tot = rows * W * C4;
                 Walk3 wk(tid, W, C4, NTH);
-                for (int e = tid; e < tot; e += NTH, wk.next()) {
-                    const int r = wk.r, x = wk.x, c4 = wk.c;
-                    const int gy = y0 + r - P;
-                    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (gy >= 0 && gy < H) {
-                        v = *reinterpret_cast<const float4*>(src + ((long long)gy * W + x) * a.in_ps + 4 * c4);
+                for (int e0 = tid; e0 < tot; e0 += kWgStageU * NTH) {
+                    float4 v[kWgStageU];
+                    float sc[kWgStageU], sh[kWgStageU];
+                    int dst[kWgStageU];
+                    bool ok[kWgStageU];
+#pragma unroll
+                    for (int u = 0; u < kWgStageU; ++u) {
+                        const int gy = y0 + wk.r - P;
+                        ok[u] = e0 + u * NTH < tot && gy >= 0 && gy < H;
+                        const int cy = ok[u] ? gy : 0, x = ok[u] ? wk.x : 0, c4 = ok[u] ? wk.c : 0;
+                        v[u] = *reinterpret_cast<const float4*>(src + ((long long)cy * W + x) * a.in_ps + 4 * c4);
                         if (bnc) {
-                            const float sc = bnc[2 * H + gy], sh = bnc[3 * H + gy];
-                            v = make_float4(bn_elu(v.x, sc, sh), bn_elu(v.y, sc, sh), bn_elu(v.z, sc, sh),
-                                            bn_elu(v.w, sc, sh));
+                            sc[u] = bnc[2 * H + cy];
+                            sh[u] = bnc[3 * H + cy];
                         }
+                        dst[u] = e0 + u * NTH < tot ? (wk.r * Wp + wk.x + P) * Cp + 4 * wk.c : -1;
+                        wk.next();
                     }
-                    *reinterpret_cast<float4*>(img + (r * Wp + x + P) * Cp + 4 * c4) = v;
+#pragma unroll
+                    for (int u = 0; u < kWgStageU; ++u) {
+                        float4 x = v[u];
+                        if (bnc)
+                            x = make_float4(bn_elu(x.x, sc[u], sh[u]), bn_elu(x.y, sc[u], sh[u]),
+                                            bn_elu(x.z, sc[u], sh[u]), bn_elu(x.w, sc[u], sh[u]));
+                        if (!ok[u]) x = make_float4(0.f, 0.f, 0.f, 0.f);
+                        if (dst[u] >= 0) *reinterpret_cast<float4*>(img + dst[u]) = x;
+                    }
                 }
             } else {
                 const int tot = rows * W * Cin;
@@ -1122,7 +1183,7 @@ struct Layer {
     long long wf_off = -1, wd_off_act = -1;    // padded fwd / dgrad weights (act arena)
     int wf_rows = 0, wf_n16 = 0, wd_rows = 0, wd_n16 = 0;
     long long z_off = -1, t_off = -1, coef_off = -1;
-    int G = 1, spg = 1, R = 1, Rd = 1, Rw = 1;   // row chunks: forward conv, input-gradient conv, wgrad
+    int G = 1, spg = 1, R = 1, Rw = 1;
 };
 
 struct DnPlan {
@@ -1170,23 +1231,6 @@ int rows_per_chunk(int H, int W) { return std::max(1, std::min(H, kMaxPix / std:
 size_t conv_lds(int R, int W, int ks, int cin) {
     const int img = (R + ks - 1) * (W + ks - 1) * conv_cp(cin);
     return (size_t)(r4(img) + r16(ks * ks * r4(cin)) + kKoffSlack) * sizeof(float);
-}
-
-// Conv row chunk: up to 2 kMaxPix pixels (4 m-tiles per wave: every weight fragment
-// feeds up to 4 NT MFMAs) while the staged rows fit kConvPixBudget of LDS (two
-// workgroups per CU), else up to kMaxPix.  MPO_DN_PLAN="conv_px=128" keeps kMaxPix.
-constexpr size_t kConvPixBudget = 64 << 10;
-// (Only for N <= 48 output channels: with 4 m-tiles x NT > 3 tiles the accumulators
-// alone cap the occupancy at 1-2 waves per SIMD.)
-int conv_rows(int H, int W, int ks, int cin, int N) {
-    const int R1 = rows_per_chunk(H, W);
-    int px = 2 * kMaxPix;
-    if (const char* e = getenv("MPO_DN_PLAN")) {
-        if (const char* q = strstr(e, "conv_px=")) px = atoi(q + 8);
-    }
-    if (px <= kMaxPix || N > 48) return R1;
-    const int R2 = std::max(1, std::min(H, px / std::max(1, W)));
-    return R2 > R1 && conv_lds(R2, W, ks, cin) <= kConvPixBudget ? R2 : R1;
 }
 
 size_t wg_lds(int R, int W, int ks, int cin, int nt) {
@@ -1281,10 +1325,8 @@ int build_plan(DnPlan& p) {
                 ly.wd_rows = r16(taps * r4(ly.cout)) + kWRowsSlack;
                 ly.wd_off_act = ar.take((long long)ly.wd_rows * ly.wd_n16, &ms);
             }
-            ly.Rw = rows_per_chunk(ly.H, ly.W);
-            // forward conv (N = cout over cin channels) and input-gradient conv (N = cin over cout)
-            ly.R = conv_rows(ly.H, ly.W, ly.ks, ly.cin, ly.cout);
-            ly.Rd = conv_rows(ly.H, ly.W, ly.ks, ly.cout, ly.cin);
+            ly.R = rows_per_chunk(ly.H, ly.W);
+            ly.Rw = ly.R;
             const long long Kw = (long long)taps * ly.cin;
             const int mgroups = ly.ks == 1 ? 1 : (int)((Kw + kWgRows - 1) / kWgRows);
             const int gt = std::max(1, (target + mgroups * p.n - 1) / (mgroups * p.n));
@@ -1326,19 +1368,10 @@ int build_plan(DnPlan& p) {
 }
 
 template <int KS, int NT>
-int launch_conv_t(const ConvArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-    auto kern = dn_conv_kernel<KS, NT, 2>;
-    if (a.R * a.W > kMaxPix) {   // 256-pixel items (conv_rows: only for N <= 48)
-        if constexpr (NT <= 3) {
-            kern = dn_conv_kernel<KS, NT, 4>;
-        } else {
-            mpo::set_error("dn_conv: %d-pixel chunks need N <= 48 (got %d)", a.R * a.W, a.N);
-            return MPO_ENOTSUP;
-        }
-    }
+void launch_conv_t(const ConvArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+    auto kern = dn_conv_kernel<KS, NT>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a);
-    return MPO_OK;
 }
 
 template <int NT>
@@ -1355,14 +1388,15 @@ int launch_conv(const ConvArgs& a, int n_members, int B, hipStream_t s) {
     size_t lds = conv_lds(a.R, a.W, KS, a.Cin);
     if (lds > ((size_t)160 << 10)) { mpo::set_error("dn_conv: LDS %zu B exceeds 160 KiB", lds); return MPO_ENOTSUP; }
     switch (nt) {
-        case 1: return launch_conv_t<KS, 1>(a, grid, lds, s);
-        case 2: return launch_conv_t<KS, 2>(a, grid, lds, s);
-        case 3: return launch_conv_t<KS, 3>(a, grid, lds, s);
-        case 4: return launch_conv_t<KS, 4>(a, grid, lds, s);
-        case 5: return launch_conv_t<KS, 5>(a, grid, lds, s);
-        case 6: return launch_conv_t<KS, 6>(a, grid, lds, s);
+        case 1: launch_conv_t<KS, 1>(a, grid, lds, s); break;
+        case 2: launch_conv_t<KS, 2>(a, grid, lds, s); break;
+        case 3: launch_conv_t<KS, 3>(a, grid, lds, s); break;
+        case 4: launch_conv_t<KS, 4>(a, grid, lds, s); break;
+        case 5: launch_conv_t<KS, 5>(a, grid, lds, s); break;
+        case 6: launch_conv_t<KS, 6>(a, grid, lds, s); break;
         default: mpo::set_error("dn_conv: %d output channels unsupported (max 96)", a.N); return MPO_ENOTSUP;
     }
+    return MPO_OK;
 }
 
 // 1x1 weight gradient: MT x NT tiles per wave (<= 6 x 6, i.e. cin, cout <= 96)
@@ -1621,7 +1655,7 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
         c.in = dout; c.in_ms = dout_ms; c.in_ps = dout_ps;
         c.w = p.act + ly.wd_off_act; c.w_ms = ((long long)ly.wd_rows * ly.wd_n16 + 63) & ~63LL;
         c.out = p.act + p.dz_off; c.out_ms = p.dz_ms; c.out_ps = ly.cin;
-        c.H = ly.H; c.W = ly.W; c.Cin = ly.cout; c.N = ly.cin; c.R = ly.Rd;
+        c.H = ly.H; c.W = ly.W; c.Cin = ly.cout; c.N = ly.cin; c.R = ly.R;
         if (ly.ks == 3) DN_TRY(launch_conv<3>(c, n, B, s));
         else DN_TRY(launch_conv<1>(c, n, B, s));
         bn.dz = p.act + p.dz_off; bn.dz_ms = p.dz_ms;
@@ -1662,7 +1696,7 @@ int mpo_dn_create(const MpoDnArch* arch, int n_members, int batch, void** handle
     for (auto& ly : p->layers) {
         if (ly.kind == K_HEAD) continue;
         if (conv_lds(ly.R, ly.W, ly.ks, ly.cin) > ((size_t)160 << 10) ||
-            conv_lds(ly.Rd, ly.W, ly.ks, ly.cout) > ((size_t)160 << 10) ||
+            conv_lds(ly.R, ly.W, ly.ks, ly.cout) > ((size_t)160 << 10) ||
             wg_lds(ly.Rw, ly.W, ly.ks, ly.cin, (ly.cout + 15) / 16) > ((size_t)160 << 10) || ly.cout > 64 ||
             (ly.kind != K_CONV0 && ly.cin > 96) || (ly.ks == 1 && ly.cin > 64)) {
             mpo::set_error("mpo_dn_create: layer (cin %d, cout %d, %dx%d) exceeds the kernels' LDS / channel range",
