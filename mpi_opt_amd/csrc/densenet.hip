@@ -74,6 +74,7 @@ struct ConvArgs {
     const float* w; long long w_ms;                       // padded weights [K16 + slack][N16]
     float* out; long long out_ms; int out_ps;
     int H, W, Cin, N, R;
+    int pool;      // 1: out is AvgPool2D((2,2)) of the conv output, [B][H/2][W/2] (R, y0 even)
 };
 
 struct WgArgs {
@@ -84,6 +85,7 @@ struct WgArgs {
     const float* dout; long long dout_ms; int dout_ps;
     float* part; long long part_ms;                       // [G][Kw][N]
     int H, W, Cin, N, R, spg, B;
+    int kw;        // dn_wgrad3: k-step interleave inside the workgroup (wg3_kw), 1 for dn_wgrad1
 };
 
 struct BnArgs {
@@ -167,7 +169,7 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 
 // elements per thread in flight in the conv / wgrad LDS staging loops
 constexpr int kStageU = 4;
-constexpr int kWgStageU = 2;   // dn_wgrad3: 4 would cost it an occupancy step (129 VGPRs)
+constexpr int kWgStageU = 1;   // dn_wgrad3: more would cost it an occupancy step (> 128 VGPRs)
 
 // ============================================================================
 // Implicit-GEMM 'same' convolution, stride 1 (forward and input gradient).
@@ -346,7 +348,36 @@ __global__ __launch_bounds__(256) void dn_conv_kernel(ConvArgs a) {
     const int N16 = NT * 16;
     if (mine == 2) dn_conv_loop<2, NT>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
     else if (mine == 1) dn_conv_loop<1, NT>(img, koff, Wt, N16, ngroups, pb, acc, krow, kcol);
-    else return;
+    else if (!a.pool) return;
+
+    if (a.pool) {
+        // the transition's AvgPool2 in the epilogue (the pre-pool output never goes to
+        // HBM): the chunk's outputs through the LDS, then each pooled element as
+        // dn_pool_fwd forms it, 0.25 (x00 + x01 + x10 + x11)
+        constexpr int S = NT * 16 + 4;
+        float* ot = smem;
+        __syncthreads();   // every wave is done with img / koff
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            if (i >= mine) break;
+            const int mt = wave + 4 * i;
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) ot[(mt * 16 + krow * 4 + r) * S + j * 16 + kcol] = acc[i][j][r];
+        }
+        __syncthreads();
+        const int H2 = H / 2, W2 = W / 2, pr0 = y0 / 2;
+        const int npr = min(rows_out / 2, H2 - pr0);
+        float* dst = a.out + m * a.out_ms + ((long long)b * H2 + pr0) * W2 * a.out_ps;
+        for (int e = tid; e < npr * W2 * a.N; e += 256) {
+            const int q = e / a.N, n = e - q * a.N;
+            const int pr = q / W2, px = q - pr * W2;
+            const float* s0 = ot + (2 * pr * W + 2 * px) * S + n;
+            dst[((long long)pr * W2 + px) * a.out_ps + n] = 0.25f * (s0[0] + s0[S] + s0[W * S] + s0[W * S + S]);
+        }
+        return;
+    }
 
     float* dst = a.out + m * a.out_ms + ((long long)b * H + y0) * W * a.out_ps;
 #pragma unroll
@@ -376,6 +407,11 @@ __global__ __launch_bounds__(256) void dn_conv_kernel(ConvArgs a) {
 // the dOut rows are staged in LDS; the zero halo columns / padding channels are
 // written once per workgroup, the data with float4 loads when the channel
 // counts allow (runtime-uniform branch).  One partial slab per sample group.
+// Layers with few m-tiles (M = 9 cin <= 6 mw tiles) split the row chunk's k-steps
+// over kw = 8 / mw wave groups instead (wave = kq * mw + wm: m-tiles wm, wm + mw,
+// ..., k-steps kq, kq + kw, ...), so each wave keeps up to 6 independent MFMA chains
+// over the LDS latency of its operand reads; at the end the k groups' accumulators
+// are summed through the LDS in fixed order (kq = 0, 1, ...) into the one slab.
 // ============================================================================
 constexpr int kWgWaves = 8;
 constexpr int kWgMT = 6;
@@ -384,7 +420,7 @@ constexpr int kWgRows = kWgWaves * kWgMT * 16;   // 768
 template <int MT, int NT>
 __device__ __forceinline__ void dn_wgrad_chunk(const float* __restrict__ img, const float* __restrict__ dl,
                                                const int* __restrict__ ptab, const int (&aoff)[kWgMT], int ns, int nk4,
-                                               int krow, int kcol, f32x4 (&acc)[kWgMT][NT]) {
+                                               int s0, int ds, int krow, int kcol, f32x4 (&acc)[kWgMT][NT]) {
     float a0[MT], a1[MT], b0[NT], b1[NT];
     auto rd = [&](int s, float (&av)[MT], float (&bv)[NT]) {
         const int p = 4 * s + krow;
@@ -400,14 +436,16 @@ __device__ __forceinline__ void dn_wgrad_chunk(const float* __restrict__ img, co
 #pragma unroll
             for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
     };
-    rd(0, a0, b0);
-    for (int s = 0; s < nk4; s += 2) {
-        rd(s + 1, a1, b1);   // s + 1 <= nk4: the tables hold one zero k-step of slack
+    // k-steps s0, s0 + ds, ... < nk4; s + ds < nk4 + kWgWaves: the tables hold
+    // kWgWaves zero k-steps of slack
+    rd(s0, a0, b0);
+    for (int s = s0; s < nk4; s += 2 * ds) {
+        rd(s + ds, a1, b1);
         __builtin_amdgcn_sched_barrier(0);
         mma(a0, b0);
         __builtin_amdgcn_sched_barrier(0);
-        if (s + 1 >= nk4) break;
-        rd(s + 2, a0, b0);
+        if (s + ds >= nk4) break;
+        rd(s + 2 * ds, a0, b0);
         __builtin_amdgcn_sched_barrier(0);
         mma(a1, b1);
         __builtin_amdgcn_sched_barrier(0);
@@ -428,7 +466,7 @@ __global__ __launch_bounds__(kWgWaves * 64) void dn_wgrad3_kernel(WgArgs a) {
     const int R = a.R;
     const int rows = R + KS - 1;
     const int img_elems = rows * Wp * Cp;
-    const int np = 4 * (((R * W + 3) >> 2) + 1);   // pixel slots incl. one zero k-step of slack
+    const int np = 4 * (((R * W + 3) >> 2) + kWgWaves);   // pixel slots incl. kWgWaves zero k-steps of slack
     float* img = smem;
     float* dl = smem + r4(img_elems);
     int* ptab = reinterpret_cast<int*>(dl + np * ns);
@@ -436,13 +474,15 @@ __global__ __launch_bounds__(kWgWaves * 64) void dn_wgrad3_kernel(WgArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int krow = lane >> 4, kcol = lane & 15;
     const int mtiles = (Kw + 15) >> 4;
-    const int t0 = mg * (kWgRows / 16);
-    const int mine = __builtin_amdgcn_readfirstlane(min(kWgMT, max(0, (mtiles - t0 - wave + kWgWaves - 1) / kWgWaves)));
+    const int t0 = mg * (kWgRows / 16);   // kw > 1 only when every tile fits one m-group
+    const int kw = a.kw, mw = kWgWaves / kw;
+    const int wm = wave % mw, kq = wave / mw;
+    const int mine = __builtin_amdgcn_readfirstlane(min(kWgMT, max(0, (mtiles - t0 - wm + mw - 1) / mw)));
 
     int aoff[kWgMT];
 #pragma unroll
     for (int i = 0; i < kWgMT; ++i) {
-        const int r = (t0 + wave + kWgWaves * i) * 16 + (lane & 15);
+        const int r = (t0 + wm + mw * i) * 16 + (lane & 15);
         int off = 0;   // rows past Kw read finite LDS; their partials are never stored
         if (r < Kw) {
             const int tap = r / Cin, c = r - tap * Cin;
@@ -539,13 +579,41 @@ __global__ __launch_bounds__(kWgWaves * 64) void dn_wgrad3_kernel(WgArgs a) {
             __syncthreads();
             const int nk4 = (Mc + 3) >> 2;
             switch (mine) {
-                case 6: dn_wgrad_chunk<6, NT>(img, dl, ptab, aoff, ns, nk4, krow, kcol, acc); break;
-                case 5: dn_wgrad_chunk<5, NT>(img, dl, ptab, aoff, ns, nk4, krow, kcol, acc); break;
-                case 4: dn_wgrad_chunk<4, NT>(img, dl, ptab, aoff, ns, nk4, krow, kcol, acc); break;
-                case 3: dn_wgrad_chunk<3, NT>(img, dl, ptab, aoff, ns, nk4, krow, kcol, acc); break;
-                case 2: dn_wgrad_chunk<2, NT>(img, dl, ptab, aoff, ns, nk4, krow, kcol, acc); break;
-                case 1: dn_wgrad_chunk<1, NT>(img, dl, ptab, aoff, ns, nk4, krow, kcol, acc); break;
+                case 6: dn_wgrad_chunk<6, NT>(img, dl, ptab, aoff, ns, nk4, kq, kw, krow, kcol, acc); break;
+                case 5: dn_wgrad_chunk<5, NT>(img, dl, ptab, aoff, ns, nk4, kq, kw, krow, kcol, acc); break;
+                case 4: dn_wgrad_chunk<4, NT>(img, dl, ptab, aoff, ns, nk4, kq, kw, krow, kcol, acc); break;
+                case 3: dn_wgrad_chunk<3, NT>(img, dl, ptab, aoff, ns, nk4, kq, kw, krow, kcol, acc); break;
+                case 2: dn_wgrad_chunk<2, NT>(img, dl, ptab, aoff, ns, nk4, kq, kw, krow, kcol, acc); break;
+                case 1: dn_wgrad_chunk<1, NT>(img, dl, ptab, aoff, ns, nk4, kq, kw, krow, kcol, acc); break;
                 default: break;
+            }
+        }
+    }
+    if (kw > 1) {
+        constexpr int TS = kWgMT * NT * 256;   // one wave's accumulators
+        __syncthreads();                       // the last chunk's MFMAs are done with the LDS
+        if (kq > 0) {
+            float* dst = smem + ((kq - 1) * mw + wm) * TS;
+#pragma unroll
+            for (int i = 0; i < kWgMT; ++i) {
+                if (i >= mine) break;
+#pragma unroll
+                for (int j = 0; j < NT; ++j) *reinterpret_cast<f32x4*>(dst + (i * NT + j) * 256 + lane * 4) = acc[i][j];
+            }
+        }
+        __syncthreads();
+        if (kq > 0) return;
+        for (int g = 1; g < kw; ++g) {
+            const float* src = smem + ((g - 1) * mw + wm) * TS;
+#pragma unroll
+            for (int i = 0; i < kWgMT; ++i) {
+                if (i >= mine) break;
+#pragma unroll
+                for (int j = 0; j < NT; ++j) {
+                    const f32x4 v = *reinterpret_cast<const f32x4*>(src + (i * NT + j) * 256 + lane * 4);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[i][j][r] += v[r];
+                }
             }
         }
     }
@@ -553,7 +621,7 @@ __global__ __launch_bounds__(kWgWaves * 64) void dn_wgrad3_kernel(WgArgs a) {
 #pragma unroll
     for (int i = 0; i < kWgMT; ++i) {
         if (i >= mine) break;
-        const int mt = t0 + wave + kWgWaves * i;
+        const int mt = t0 + wm + mw * i;
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
             const int n = j * 16 + kcol;
@@ -1184,6 +1252,7 @@ struct Layer {
     int wf_rows = 0, wf_n16 = 0, wd_rows = 0, wd_n16 = 0;
     long long z_off = -1, t_off = -1, coef_off = -1;
     int G = 1, spg = 1, R = 1, Rw = 1;
+    int kw = 1;    // dn_wgrad3 k groups per workgroup (wg3_kw)
 };
 
 struct DnPlan {
@@ -1228,16 +1297,29 @@ struct Arena {
 // Choose rows per chunk so that R * W <= kMaxPix pixels.
 int rows_per_chunk(int H, int W) { return std::max(1, std::min(H, kMaxPix / std::max(1, W))); }
 
+// dn_conv's pooled epilogue: the chunk's m-tiles of outputs, NT 16 + 4 floats apart
+size_t pool_tile_lds(int R, int W, int nt) { return (size_t)r16(R * W) * (nt * 16 + 4) * sizeof(float); }
+
 size_t conv_lds(int R, int W, int ks, int cin) {
     const int img = (R + ks - 1) * (W + ks - 1) * conv_cp(cin);
     return (size_t)(r4(img) + r16(ks * ks * r4(cin)) + kKoffSlack) * sizeof(float);
 }
 
-size_t wg_lds(int R, int W, int ks, int cin, int nt) {
+// dn_wgrad3's k groups: the fewest m-waves mw (8 / kw) that keep every wave's
+// m-tiles <= kWgMT; layers past one m-group keep mw = 8
+int wg3_kw(int Kw) {
+    const int mt = std::min(kWgRows / 16, (Kw + 15) / 16);
+    int mw = 1;
+    while (mw < kWgWaves && (mt + mw - 1) / mw > kWgMT) mw *= 2;
+    return kWgWaves / mw;
+}
+
+size_t wg_lds(int R, int W, int ks, int cin, int nt, int kw) {
     if (ks == 1) return 0;   // dn_wgrad1: static LDS only
     const int img = (R + ks - 1) * (W + ks - 1) * wg_cp(cin);
-    const int np = 4 * (((R * W + 3) >> 2) + 1);
-    return (size_t)(r4(img) + np * wg_ns(nt) + np) * sizeof(float);
+    const int np = 4 * (((R * W + 3) >> 2) + kWgWaves);
+    const size_t red = kw > 1 ? (size_t)(kWgWaves - kWgWaves / kw) * kWgMT * nt * 256 : 0;   // k-group sums
+    return std::max((size_t)(r4(img) + np * wg_ns(nt) + np), red) * sizeof(float);
 }
 
 int build_plan(DnPlan& p) {
@@ -1333,6 +1415,7 @@ int build_plan(DnPlan& p) {
             const int G0 = std::min(B, gt);
             ly.spg = (B + G0 - 1) / G0;
             ly.G = (B + ly.spg - 1) / ly.spg;
+            ly.kw = ly.ks == 3 ? wg3_kw((int)Kw) : 1;
             part_max = std::max(part_max, (long long)ly.G * Kw * ly.cout);
         }
     }
@@ -1386,6 +1469,7 @@ int launch_conv(const ConvArgs& a, int n_members, int B, hipStream_t s) {
     const int nt = (a.N + 15) / 16;
     const dim3 grid((a.H + a.R - 1) / a.R, B, n_members);
     size_t lds = conv_lds(a.R, a.W, KS, a.Cin);
+    if (a.pool) lds = std::max(lds, pool_tile_lds(a.R, a.W, nt));
     if (lds > ((size_t)160 << 10)) { mpo::set_error("dn_conv: LDS %zu B exceeds 160 KiB", lds); return MPO_ENOTSUP; }
     switch (nt) {
         case 1: launch_conv_t<KS, 1>(a, grid, lds, s); break;
@@ -1429,7 +1513,7 @@ int launch_wgrad(const WgArgs& a, int ks, int n_members, int G, hipStream_t s) {
     }
     const int Kw = 9 * a.Cin;
     const dim3 grid((Kw + kWgRows - 1) / kWgRows, G, n_members);
-    const size_t lds = wg_lds(a.R, a.W, 3, a.Cin, nt);
+    const size_t lds = wg_lds(a.R, a.W, 3, a.Cin, nt, a.kw);
     if (lds > ((size_t)160 << 10)) { mpo::set_error("dn_wgrad: LDS %zu B exceeds 160 KiB", lds); return MPO_ENOTSUP; }
     switch (nt) {
         case 1: launch_wg3_t<1>(a, grid, lds, s); break;
@@ -1566,6 +1650,13 @@ int enqueue_forward(DnPlan& p, const float* x, const int* labels, const int* ord
             c.out = p.act + p.cat_off[st] + ly.coff; c.out_ms = p.cat_ms[st]; c.out_ps = p.sC[st];
             DN_TRY(launch_conv<3>(c, n, B, s));
         } else {
+            if (ly.R % 2 == 0) {
+                // AvgPool2 in the conv's epilogue: straight into the next stage's concat
+                c.out = p.act + p.cat_off[st + 1]; c.out_ms = p.cat_ms[st + 1]; c.out_ps = p.sC[st + 1];
+                c.pool = 1;
+                DN_TRY(launch_conv<1>(c, n, B, s));
+                continue;
+            }
             const long long tms = ((long long)B * ly.H * ly.W * ly.cout + 63) & ~63LL;
             c.out = p.act + ly.t_off; c.out_ms = tms; c.out_ps = ly.cout;
             DN_TRY(launch_conv<1>(c, n, B, s));
@@ -1614,7 +1705,7 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
         }
         // dOut of this layer's conv and the input it saw
         WgArgs w{};
-        w.H = ly.H; w.W = ly.W; w.Cin = ly.cin; w.N = ly.cout; w.R = ly.Rw; w.spg = ly.spg; w.B = B;
+        w.H = ly.H; w.W = ly.W; w.Cin = ly.cin; w.N = ly.cout; w.R = ly.Rw; w.spg = ly.spg; w.B = B; w.kw = ly.kw;
         w.part = p.act + p.part_off; w.part_ms = p.part_ms;
         const float* dout;
         long long dout_ms;
@@ -1697,7 +1788,7 @@ int mpo_dn_create(const MpoDnArch* arch, int n_members, int batch, void** handle
         if (ly.kind == K_HEAD) continue;
         if (conv_lds(ly.R, ly.W, ly.ks, ly.cin) > ((size_t)160 << 10) ||
             conv_lds(ly.R, ly.W, ly.ks, ly.cout) > ((size_t)160 << 10) ||
-            wg_lds(ly.Rw, ly.W, ly.ks, ly.cin, (ly.cout + 15) / 16) > ((size_t)160 << 10) || ly.cout > 64 ||
+            wg_lds(ly.Rw, ly.W, ly.ks, ly.cin, (ly.cout + 15) / 16, ly.kw) > ((size_t)160 << 10) || ly.cout > 64 ||
             (ly.kind != K_CONV0 && ly.cin > 96) || (ly.ks == 1 && ly.cin > 64)) {
             mpo::set_error("mpo_dn_create: layer (cin %d, cout %d, %dx%d) exceeds the kernels' LDS / channel range",
                            ly.cin, ly.cout, ly.H, ly.W);

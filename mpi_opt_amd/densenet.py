@@ -137,12 +137,19 @@ def flops_per_sample_train(layers):
     return 3 * flops_per_sample_fwd(layers) - 2 * 9 * c0["cin"] * c0["cout"] * c0["H"] * c0["W"]
 
 
+def _pool_fused(H, W):
+    """csrc/densenet.hip enqueue_forward: a transition's AvgPool2 runs in the 1x1
+    conv's epilogue when the conv's row chunk (rows_per_chunk) is even."""
+    return max(1, min(H, 128 // max(1, W))) % 2 == 0
+
+
 def hbm_bytes_train(layers, batch, n_params):
     """Algorithmic HBM bytes of one train step of one member over ``batch``
     samples (f32), every tensor written once and read once per consuming kernel:
     forward -- each layer reads its input channels (BN + ELU folded into the
     consumer) and writes its output channels, the transition's AvgPool reads the
-    conv output and writes the pooled stage; backward -- each layer reads its
+    conv output and writes the pooled stage (the conv writes the pooled stage itself
+    when the pool is fused into its epilogue); backward -- each layer reads its
     output gradient and its input (for the weight gradient and the BN / ELU
     derivative), writes its input gradient (not for the initial conv), the pool
     reads / writes the gradient once; per member the parameters are read twice
@@ -154,13 +161,17 @@ def hbm_bytes_train(layers, batch, n_params):
         if ly["kind"] == "head":
             per_sample += hw * ly["cin"] * 2 + hw * ly["cin"] * 2      # GAP read fwd; dGAP fold + input read bwd
             continue
-        per_sample += hw * (ly["cin"] + ly["cout"])                    # forward
+        q = (ly["H"] // 2) * (ly["W"] // 2) * ly["cout"]
+        if ly["kind"] == "trans" and _pool_fused(ly["H"], ly["W"]):
+            per_sample += hw * ly["cin"] + q                           # forward: conv + AvgPool2
+            per_sample += hw * ly["cout"] + q                          # AvgPool2 backward
+        else:
+            per_sample += hw * (ly["cin"] + ly["cout"])                # forward
+            if ly["kind"] == "trans":
+                per_sample += 2 * (hw * ly["cout"] + q)                # AvgPool2 forward + backward
         per_sample += hw * (ly["cout"] + ly["cin"])                    # backward: dOut, input for wgrad / BN
         if ly["kind"] != "conv0":
             per_sample += hw * ly["cin"]                               # input gradient
-        if ly["kind"] == "trans":
-            q = (ly["H"] // 2) * (ly["W"] // 2) * ly["cout"]
-            per_sample += 2 * (hw * ly["cout"] + q)                    # AvgPool2 forward + backward
     return 4 * (batch * per_sample + 8 * n_params)
 
 
@@ -204,8 +215,11 @@ def hbm_bytes_train_by_kernel(layers, batch, n_params):
             by["dn_bn_bwd_apply_kernel"] += 4 * hw * cin              # dz, x, dcat in; dcat out
         else:                                                         # transition
             q = (ly["H"] // 2) * (ly["W"] // 2) * cout
-            by["dn_conv_kernel"] += hw * (cin + cout)
-            by["dn_pool_fwd_kernel"] += hw * cout + q
+            if _pool_fused(ly["H"], ly["W"]):
+                by["dn_conv_kernel"] += hw * cin + q                  # AvgPool2 in the epilogue
+            else:
+                by["dn_conv_kernel"] += hw * (cin + cout)
+                by["dn_pool_fwd_kernel"] += hw * cout + q
             by["dn_pool_bwd_kernel"] += q + hw * cout
             by["dn_wgrad1_kernel"] += hw * (cin + cout)
             by["dn_conv_kernel"] += hw * (cout + cin)
