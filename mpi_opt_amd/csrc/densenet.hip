@@ -207,6 +207,41 @@ __device__ __forceinline__ void dn_conv_loop(const float* __restrict__ img, cons
                 for (int j = 0; j < NT; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][i], bw[u][j], acc[i][j], 0, 0, 0);
     };
+    if constexpr (NT <= 2) {
+        // narrow N (the growth convs): each group's MFMAs are few, so the weights
+        // stream two groups ahead of their MFMAs (L2 latency) from a 3-buffer ring;
+        // loads reach group ngroups + 1 (kWRowsSlack / kKoffSlack cover it)
+        float b2[4][NT], a2[4][MT];
+        loadB(0, b0);
+        loadB(1, b1);
+        int4 ko = kof(0);
+        readA(ko, a0);
+        ko = kof(1);
+        for (int g = 0;; g += 3) {
+            loadB(g + 2, b2);
+            readA(ko, a1);
+            ko = kof(g + 2);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(a0, b0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (g + 1 >= ngroups) break;
+            loadB(g + 3, b0);
+            readA(ko, a2);
+            ko = kof(g + 3);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(a1, b1);
+            __builtin_amdgcn_sched_barrier(0);
+            if (g + 2 >= ngroups) break;
+            loadB(g + 4, b1);
+            readA(ko, a0);
+            ko = kof(g + 4);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(a2, b2);
+            __builtin_amdgcn_sched_barrier(0);
+            if (g + 3 >= ngroups) break;
+        }
+        return;
+    }
     loadB(0, b0);
     int4 ko = kof(0);
     readA(ko, a0);
