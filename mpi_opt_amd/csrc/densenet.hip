@@ -1333,6 +1333,11 @@ struct Arena {
 int rows_per_chunk(int H, int W) { return std::max(1, std::min(H, kMaxPix / std::max(1, W))); }
 
 // dn_conv's pooled epilogue: the chunk's m-tiles of outputs, NT 16 + 4 floats apart
+// the population the work splits are sized for (build_plan): the reference search's
+// 32 DenseNet trials per GPU
+constexpr int kNominalMembers = 32;
+constexpr int kWgTarget = 2048;   // weight-gradient workgroups per launch at kNominalMembers
+
 size_t pool_tile_lds(int R, int W, int nt) { return (size_t)r16(R * W) * (nt * 16 + 4) * sizeof(float); }
 
 size_t conv_lds(int R, int W, int ks, int cin) {
@@ -1418,7 +1423,11 @@ int build_plan(DnPlan& p) {
         p.cat_ms[s] = ms;
     }
     long long dz_max = 0, dt_max = 0, part_max = 0;
-    const int target = 2048;
+    // The work splits (weight-gradient sample groups, BN batch slices) are sized for
+    // a nominal population, never the actual one: they fix the order of the
+    // partial sums, so a member's arithmetic must not depend on how many members
+    // train beside it (tests/test_densenet_gpu.py::test_member_isolation_*).
+    const int target = kWgTarget;
     for (auto& ly : ls) {
         long long ms;
         if (ly.kind != K_CONV0) {
@@ -1446,7 +1455,7 @@ int build_plan(DnPlan& p) {
             ly.Rw = ly.R;
             const long long Kw = (long long)taps * ly.cin;
             const int mgroups = ly.ks == 1 ? 1 : (int)((Kw + kWgRows - 1) / kWgRows);
-            const int gt = std::max(1, (target + mgroups * p.n - 1) / (mgroups * p.n));
+            const int gt = std::max(1, (target + mgroups * kNominalMembers - 1) / (mgroups * kNominalMembers));
             const int G0 = std::min(B, gt);
             ly.spg = (B + G0 - 1) / G0;
             ly.G = (B + ly.spg - 1) / ly.spg;
@@ -1461,7 +1470,7 @@ int build_plan(DnPlan& p) {
     for (size_t i = 0; i < ls.size(); ++i) {
         const Layer& ly = ls[i];
         if (ly.kind == K_CONV0) continue;
-        const int want = std::max(1, (2048 + ly.H * p.n - 1) / (ly.H * p.n));
+        const int want = std::max(1, (2048 + ly.H * kNominalMembers - 1) / (ly.H * kNominalMembers));
         const int bs = (B + std::min(B, want) - 1) / std::min(B, want);
         p.bn_bs[i] = bs;
         p.bn_S[i] = (B + bs - 1) / bs;

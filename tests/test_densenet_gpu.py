@@ -127,6 +127,34 @@ def test_member_isolation_bit_identical():
     assert torch.equal(full.state[1], solo.state[0])
 
 
+def test_member_isolation_at_the_reference_batch():
+    """At batch 100 the work splits (weight-gradient sample groups, BN batch
+    slices) are sized for a nominal population: a member of a 24-member population
+    and the same member alone take the same partial-sum orders, so the same bits
+    (split by the actual population size, 24 members would use 2-sample groups and
+    6 BN slices, one member 1-sample groups and 100 slices)."""
+    from mpi_opt_amd.densenet import DenseNetArch, DenseNetPopulation, he_uniform_init
+
+    arch = DenseNetArch(img_dim=(16, 16, 3), nb_classes=10, depth=7, nb_dense_block=3, growth_rate=12, nb_filter=16)
+    layers = od.arch_layers(img_dim=(16, 16, 3), nb_classes=10, depth=7, nb_dense_block=3, growth_rate=12,
+                            nb_filter=16)
+    n, k, B = 24, 5, 100
+    init = [he_uniform_init(layers, 11 + i) for i in range(n)]
+    rng = np.random.RandomState(9)
+    x = torch.from_numpy(rng.rand(2 * B, 16, 16, 3).astype(np.float32)).cuda()
+    y = torch.from_numpy(rng.randint(0, 10, 2 * B).astype(np.int32)).cuda()
+    order = torch.from_numpy(np.stack([rng.permutation(2 * B).astype(np.int32) for _ in range(n)])).cuda()
+    lrs = [1e-3 * (1 + i % 4) for i in range(n)]
+    full = DenseNetPopulation(arch, lrs, batch=B, init=init)
+    solo = DenseNetPopulation(arch, [lrs[k]], batch=B, init=[init[k]])
+    for s in range(2):
+        full.train_step(x, y, order, s * B)
+        solo.train_step(x, y, order[k:k + 1].contiguous(), s * B)
+    torch.cuda.synchronize()
+    assert torch.equal(full.params[k], solo.params[0])
+    assert torch.equal(full.state[k], solo.state[0])
+
+
 def test_fit_folds_reference_config_runs():
     from mpi_opt_amd.densenet import DenseNetArch, DenseNetPopulation, synthetic_cifar
 
