@@ -62,6 +62,17 @@ def main():
     flops = sum(m.flops_per_sample_train() for m in members) * 100
     print("train step %.2f ms  %.1f TFLOP/s  (%.1f%% of 157.3)" % (dt * 1e3, flops / dt / 1e12, flops / dt / 157.3e12 * 100))
     print("loss", eng.loss[:5].cpu().numpy())
+    va = np.stack([kfold_split(60000, args.folds, f)[1] for f in folds])
+    vorder = torch.from_numpy(va).cuda()
+    eng.eval_step(x, y, vorder, 0)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    for s in range(args.steps):
+        eng.eval_step(x, y, vorder, (s + 1) * 100)
+    torch.cuda.synchronize()
+    de = (time.time() - t0) / args.steps
+    fe = sum(m.flops_per_sample_fwd() for m in members) * 100
+    print("eval step %.2f ms  %.1f TFLOP/s  (%.1f%% of 157.3)" % (de * 1e3, fe / de / 1e12, fe / de / 157.3e12 * 100))
 
 
 if __name__ == "__main__":
