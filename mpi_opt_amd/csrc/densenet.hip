@@ -451,6 +451,11 @@ __global__ __launch_bounds__(256) void dn_conv_kernel(ConvArgs a) {
 constexpr int kWgWaves = 8;
 constexpr int kWgMT = 6;
 constexpr int kWgRows = kWgWaves * kWgMT * 16;   // 768
+// m-tiles per wave of the first m-group when mw waves share its tiles
+__host__ __device__ inline int wg3_tpw(int Kw, int mw) {
+    const int mt = min(kWgRows / 16, (Kw + 15) >> 4);
+    return (mt + mw - 1) / mw;
+}
 
 template <int MT, int NT>
 __device__ __forceinline__ void dn_wgrad_chunk(const float* __restrict__ img, const float* __restrict__ dl,
@@ -625,7 +630,8 @@ __global__ __launch_bounds__(kWgWaves * 64) void dn_wgrad3_kernel(WgArgs a) {
         }
     }
     if (kw > 1) {
-        constexpr int TS = kWgMT * NT * 256;   // one wave's accumulators
+        // one wave's accumulators: its m-tiles (kw > 1: one m-group, so wg3_tpw) x NT
+        const int TS = wg3_tpw(Kw, mw) * NT * 256;
         __syncthreads();                       // the last chunk's MFMAs are done with the LDS
         if (kq > 0) {
             float* dst = smem + ((kq - 1) * mw + wm) * TS;
@@ -1358,7 +1364,8 @@ size_t wg_lds(int R, int W, int ks, int cin, int nt, int kw) {
     if (ks == 1) return 0;   // dn_wgrad1: static LDS only
     const int img = (R + ks - 1) * (W + ks - 1) * wg_cp(cin);
     const int np = 4 * (((R * W + 3) >> 2) + kWgWaves);
-    const size_t red = kw > 1 ? (size_t)(kWgWaves - kWgWaves / kw) * kWgMT * nt * 256 : 0;   // k-group sums
+    // k-group sums: the accumulators of the kq > 0 waves
+    const size_t red = kw > 1 ? (size_t)(kWgWaves - kWgWaves / kw) * wg3_tpw(9 * cin, kWgWaves / kw) * nt * 256 : 0;
     return std::max((size_t)(r4(img) + np * wg_ns(nt) + np), red) * sizeof(float);
 }
 

@@ -50,10 +50,13 @@ CASES = [
     dict(img=(32, 32, 3), classes=10, depth=10, blocks=3, growth=12, nbf=16, B=6),
     # odd spatial sizes (floor-mode AvgPool), 2 blocks, ragged channel counts
     dict(img=(9, 11, 2), classes=5, depth=7, blocks=2, growth=5, nbf=7, B=5),
+    # wide dense layers: the second has 9 x 90 = 810 weight-gradient rows (two 768-row
+    # m-groups), growth 30 (two 16-column tiles)
+    dict(img=(8, 8, 3), classes=4, depth=10, blocks=1, growth=30, nbf=60, B=4),
 ]
 
 
-@pytest.mark.parametrize("case", CASES, ids=["cifar-d10", "odd-d7"])
+@pytest.mark.parametrize("case", CASES, ids=["cifar-d10", "odd-d7", "wide-d10"])
 def test_forward_loss_and_gradients(case):
     lrs = [1e-3, 3e-4, 1e-2]
     pop, layers, init, x, y, order, xd, yd, od_ = _setup(case["img"], case["classes"], case["depth"], case["blocks"],
