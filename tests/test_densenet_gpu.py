@@ -53,10 +53,12 @@ CASES = [
     # wide dense layers: the second has 9 x 90 = 810 weight-gradient rows (two 768-row
     # m-groups), growth 30 (two 16-column tiles)
     dict(img=(8, 8, 3), classes=4, depth=10, blocks=1, growth=30, nbf=60, B=4),
+    # a pooled transition epilogue (10-row chunk) over an odd width: AvgPool2 drops column 8
+    dict(img=(10, 9, 3), classes=3, depth=7, blocks=2, growth=8, nbf=12, B=4),
 ]
 
 
-@pytest.mark.parametrize("case", CASES, ids=["cifar-d10", "odd-d7", "wide-d10"])
+@pytest.mark.parametrize("case", CASES, ids=["cifar-d10", "odd-d7", "wide-d10", "pooled-odd-w"])
 def test_forward_loss_and_gradients(case):
     lrs = [1e-3, 3e-4, 1e-2]
     pop, layers, init, x, y, order, xd, yd, od_ = _setup(case["img"], case["classes"], case["depth"], case["blocks"],
