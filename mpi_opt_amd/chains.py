@@ -39,7 +39,15 @@ import time
 
 
 class LazyBatch:
-    """The future result of one ``ask(n)`` batch."""
+    """The future result of one ``ask(n)`` batch.
+
+    It behaves as the list skopt's ``ask(n)`` returns, as far as the reference's
+    ``Coordinator`` uses one (coordinator.py:46-50): truthiness and ``len`` count
+    the entries not yet popped, and ``pop(-1)`` removes the last one and returns
+    it as a :class:`LazyPoint` without waiting for the batch.  skopt hands out its
+    cached list itself, so the Coordinator's pops consume the optimizer's ask
+    cache; popping this batch (the optimizer's cache entry) does the same.
+    Iteration and indexing resolve the batch and see the remaining entries."""
 
     def __init__(self, executor, job):
         self.executor, self.job = executor, job
@@ -47,11 +55,19 @@ class LazyBatch:
         self._trace = None
         self._error = None
         self._done = threading.Event()
+        self._left = list(range(job.n_points))   # entries not popped yet, in order
         self.seq = None             # submission number (executor bookkeeping)
         self.run_s = None           # seconds the batch ran on its worker
 
     def __len__(self):
-        return self.job.n_points
+        return len(self._left)
+
+    def __bool__(self):
+        return bool(self._left)
+
+    def pop(self, index=-1):
+        """Remove entry ``index`` of the remaining ones; a :class:`LazyPoint` (no wait)."""
+        return LazyPoint(self, self._left.pop(index))
 
     def done(self):
         return self._done.is_set()
@@ -69,14 +85,15 @@ class LazyBatch:
 
     def points(self):
         """One :class:`LazyPoint` per batch entry (what the scheduler pops from)."""
-        return [LazyPoint(self, i) for i in range(len(self))]
+        return [LazyPoint(self, i) for i in range(self.job.n_points)]
 
     # list-like access resolves the batch
     def __iter__(self):
-        return iter(self.result())
+        X = self.result()
+        return iter([X[i] for i in self._left])
 
     def __getitem__(self, i):
-        return self.result()[i]
+        return self.result()[self._left[i]]
 
 
 class LazyPoint:
