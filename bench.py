@@ -56,6 +56,24 @@ def dist_env():
 PMC_FAMILIES = (("conv_img_kernel<0", "conv1_fwd"), ("conv_img_kernel<1", "conv2_fwd"), ("conv_dgrad", "conv2_dgrad"),
                 ("conv_wgrad_kernel<1", "conv2_wgrad"), ("conv_wgrad_kernel<0", "conv1_wgrad"),
                 ("dense_kernel", "dense_kernel"))
+# DenseNet kernels that issue MFMAs (csrc/densenet.hip): the convs (3x3 growth / initial,
+# 1x1 transitions, their input gradients) and the two weight-gradient kernels
+DN_PMC_FAMILIES = (("dn_conv_kernel<3", "conv3x3"), ("dn_conv_kernel<1", "conv1x1"), ("dn_wgrad3_kernel", "wgrad3"),
+                   ("dn_wgrad1_kernel", "wgrad1"))
+
+
+def mfma_busy(rows, families):
+    """SQ_VALU_MFMA_BUSY_CYCLES over the SIMD cycles of the matching dispatches
+    (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs), per family and pooled."""
+    per, num, den = {}, 0.0, 0.0
+    for needle, fam in families:
+        busy = sum(_per_dispatch(rows, "SQ_VALU_MFMA_BUSY_CYCLES", lambda k: needle in k).values())
+        gui = sum(_per_dispatch(rows, "GRBM_GUI_ACTIVE", lambda k: needle in k).values())
+        if gui:
+            per[fam] = busy / (gui / 8 * 1024)
+            num += busy
+            den += gui / 8 * 1024
+    return (num / den if den else None), per
 
 
 def pmc_pass(counters, prog, timeout=150):
@@ -136,8 +154,11 @@ def live_pmc(train_trials):
                      "write_size_bytes": write, "launches": passes, "dispatches": len(f)}
     except Exception as e:  # noqa: BLE001 -- reported, the bench line carries traffic null
         out["errors"].append(f"ei: {e}")
+    # 2 warmup + 1 timed train steps and no evaluation (r04 counted the probe's eval
+    # kernels too, which inflated the forward families 5/3x)
     steps = 3
-    tr_prog = [os.path.join(ROOT, "scripts", "train_probe.py"), "--steps", "1", "--trials", str(train_trials)]
+    tr_prog = [os.path.join(ROOT, "scripts", "train_probe.py"), "--steps", "1", "--trials", str(train_trials),
+               "--no-eval"]
     try:
         ours = lambda k: "anonymous namespace" in k     # noqa: E731 -- libmpo's kernels, not torch's setup
         rf, rw = pmc_pass(["FETCH_SIZE"], tr_prog), pmc_pass(["WRITE_SIZE"], tr_prog)
@@ -147,17 +168,9 @@ def live_pmc(train_trials):
         per_family = _per_kernel_bytes(rf, rw, ours, steps, family=True)
         fetch = 1024.0 * sum(f.values()) / steps
         write = 1024.0 * sum(w.values()) / steps
-        rows = pmc_pass(["SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"], tr_prog)
-        per, num, den = {}, 0.0, 0.0
-        for needle, fam in PMC_FAMILIES:
-            busy = sum(_per_dispatch(rows, "SQ_VALU_MFMA_BUSY_CYCLES", lambda k: needle in k).values())
-            gui = sum(_per_dispatch(rows, "GRBM_GUI_ACTIVE", lambda k: needle in k).values())
-            if gui:
-                per[fam] = busy / (gui / 8 * 1024)
-                num += busy
-                den += gui / 8 * 1024
+        busy, per = mfma_busy(pmc_pass(["SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"], tr_prog), PMC_FAMILIES)
         out["train"] = {"hbm_bytes_per_train_batch": 2.0 * fetch + write, "fetch_size_bytes_raw": fetch,
-                        "write_size_bytes": write, "mfma_busy": num / den if den else None,
+                        "write_size_bytes": write, "mfma_busy": busy, "steps_counted": steps,
                         "per_kernel_mfma_busy": per, "per_kernel_hbm_bytes": per_kernel,
                         "per_family_hbm_bytes": per_family}
     except Exception as e:  # noqa: BLE001
@@ -171,8 +184,9 @@ def live_pmc(train_trials):
         w = _per_dispatch(rw, "WRITE_SIZE", ours)
         fetch = 1024.0 * sum(f.values()) / 5
         write = 1024.0 * sum(w.values()) / 5
+        busy, per = mfma_busy(pmc_pass(["SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"], dn_prog), DN_PMC_FAMILIES)
         out["densenet"] = {"hbm_bytes_per_train_step": 2.0 * fetch + write, "fetch_size_bytes_raw": fetch,
-                           "write_size_bytes": write, "steps": 5,
+                           "write_size_bytes": write, "steps": 5, "mfma_busy": busy, "per_kernel_mfma_busy": per,
                            "per_kernel_hbm_bytes": _per_kernel_bytes(rf, rw, ours, 5),
                            "per_family_hbm_bytes": _per_kernel_bytes(rf, rw, ours, 5, family=True)}
     except Exception as e:  # noqa: BLE001
@@ -671,7 +685,7 @@ def bench_densenet(args, torch, dist, ws, rank, dev):
 
 
 SEARCH_ARGV = ["--world-size", "21", "--block-size", "5", "--epochs", "10", "--num-iterations", "10",
-               "--n-fold", "5", "--n-samples", "60000"]
+               "--n-fold", "5", "--n-samples", "60000", "--synthetic-labels", "learnable"]
 
 
 def bench_search(args, torch, dist, ws, rank, dev):
@@ -715,8 +729,10 @@ def bench_search(args, torch, dist, ws, rank, dev):
     return out
 
 
+# learnable synthetic labels (population.synthetic_mnist): with uniform labels every
+# told FOM is the uniform-softmax BCE and the GP of the search fits a flat function
 SEARCH3_ARGV = ["--world-size", "129", "--block-size", "2", "--n-fold", "5", "--num-iterations", "128",
-                "--epochs", "1", "--n-samples", "60000"]
+                "--epochs", "1", "--n-samples", "60000", "--synthetic-labels", "learnable"]
 
 
 def bench_search_gp(args, torch, dist, ws, rank, dev):

@@ -11,9 +11,6 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmpo.so")
-if os.environ.get("MPO_LIB_AB"):
-    # A/B experiments only (scripts/ab_libs.sh builds other revisions' libraries)
-    LIB_PATH = os.path.abspath(os.environ["MPO_LIB_AB"])
 
 MPO_OK = 0
 MPO_ACQ_EI = 1

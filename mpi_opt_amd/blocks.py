@@ -88,45 +88,47 @@ class TrialEvaluator:
                 out.append((t, f, spec, cost))
         return out
 
-    def train_units(self, units, seed_base=0):
+    def train_units(self, units, seed_base=0, trial_ids=None):
         """Train the given (trial, fold, spec) units as populations -- one for the
         test_mnist units, one per DenseNet architecture; returns
-        {(trial, fold): history dict}."""
+        {(trial, fold): history dict}.  Trial ``t`` is seeded by its identity
+        ``trial_ids[t]`` (default ``seed_base + t``)."""
         import time
 
         t0 = time.perf_counter()
+        tid = (lambda t: seed_base + t) if trial_ids is None else (lambda t: int(trial_ids[t]))
         try:
-            return self._train_units(units, seed_base)
+            return self._train_units(units, tid)
         finally:
             self.train_s += time.perf_counter() - t0
 
-    def _train_units(self, units, seed_base):
+    def _train_units(self, units, tid):
         from .models import DenseNetSpec
 
         out = {}
         mnist = [u for u in units if not isinstance(u[2], DenseNetSpec)]
-        out.update(self._train_mnist(mnist, seed_base))
+        out.update(self._train_mnist(mnist, tid))
         groups = {}
         for u in units:
             if isinstance(u[2], DenseNetSpec):
                 groups.setdefault(u[2].arch.key(), []).append(u)
         for us in groups.values():
-            out.update(self._train_densenet(us, seed_base))
+            out.update(self._train_densenet(us, tid))
         return out
 
-    def _uid(self, seed_base, t, f):
+    def _uid(self, trial_id, f):
         # seeds depend on the unit's identity only, never on how units are
-        # sharded or batched: results are independent of the world size
-        return (self.init_seed + 1000003 * (seed_base + t) + f) & 0x7FFFFFFF
+        # sharded, batched or chunked: results are independent of the world size
+        return (self.init_seed + 1000003 * trial_id + f) & 0x7FFFFFFF
 
-    def _train_mnist(self, units, seed_base):
+    def _train_mnist(self, units, tid):
         from .population import PopulationEngine, TrialSpec, glorot_uniform_init
 
         if not units:
             return {}
         specs, folds, init = [], [], []
         for (t, f, spec, _) in units:
-            uid = self._uid(seed_base, t, f)
+            uid = self._uid(tid(t), f)
             s = TrialSpec(spec.nb_filters, spec.kernel_size, spec.pool_size, spec.dense, spec.lr, spec.dropout,
                           seed=uid, loss=self.loss, optimizer=self.optimizer)
             specs.append(s)
@@ -146,14 +148,14 @@ class TrialEvaluator:
         return lambda ep, eps: self.progress(f"population of {members} members: epoch {ep}/{eps} "
                                              f"({time.perf_counter() - t0:.1f} s)")
 
-    def _train_densenet(self, units, seed_base):
+    def _train_densenet(self, units, tid):
         from .densenet import DenseNetPopulation, he_uniform_init
 
         arch = units[0][2].arch
         layers = arch.layers()
         lrs = [u[2].lr for u in units]
         folds = [u[1] for u in units]
-        init = [he_uniform_init(layers, self._uid(seed_base, t, f)) for (t, f, _, _) in units]
+        init = [he_uniform_init(layers, self._uid(tid(t), f)) for (t, f, _, _) in units]
         pop = DenseNetPopulation(arch, lrs, batch=self.batch, device=self.device, init=init)
         return self._histories(units, pop.fit_folds(self.x, self.y, folds, self.n_fold, self.epochs,
                                                       holdout=self.holdout, progress=self._epoch_cb(len(units)),
@@ -183,9 +185,16 @@ class TrialEvaluator:
             self._record(params, [results[(t, f)] for f in range(folds)])
         return foms
 
-    def evaluate(self, params_list):
+    accepts_trial_ids = True
+
+    def evaluate(self, params_list, trial_ids=None):
+        """FOMs of ``params_list``; trial ``t`` is seeded by ``trial_ids[t]``
+        (default: its position in the sequence of evaluated trials)."""
         units = self.units(params_list)
-        results = self.train_units(units, seed_base=self.n_evaluated)
+        if trial_ids is None:
+            results = self.train_units(units, seed_base=self.n_evaluated)
+        else:
+            results = self.train_units(units, seed_base=self.n_evaluated, trial_ids=trial_ids)
         self.n_evaluated += len(params_list)
         return self.foms(params_list, results)
 
@@ -296,6 +305,9 @@ class PopulationComm:
         blocks = sorted(self.pending)
         points = [self.pending.pop(b) for b in blocks]
         k = min(self.chunks, len(points))
+        # a trial's seed identity is its population's base plus its block-order
+        # position, whatever part it trains in (evaluators that seed trials)
+        base = self.trials_trained
         # parts in the order their ask batches were submitted (the executors run them
         # first-in first-out; the scheduler polls blocks in a shuffled order, so block
         # order is not submission order); results go back to their blocks
@@ -308,7 +320,11 @@ class PopulationComm:
             tw = time.perf_counter()
             part = resolve_all([points[i] for i in idx])
             wait += time.perf_counter() - tw
-            for i, p_, f_ in zip(idx, part, self.evaluator.evaluate(part)):
+            if getattr(self.evaluator, "accepts_trial_ids", False):
+                got = self.evaluator.evaluate(part, trial_ids=[base + i for i in idx])
+            else:
+                got = self.evaluator.evaluate(part)
+            for i, p_, f_ in zip(idx, part, got):
                 params[i], foms[i] = p_, f_
         t2 = time.perf_counter()
         t1 = t0 + wait
@@ -403,11 +419,14 @@ class DistributedEvaluator:
         self.dist.all_gather_object(out, obj, group=self.group)
         return out
 
-    def _train(self, params_list):
+    def _train(self, params_list, trial_ids=None):
         units = self.local.units(params_list)
         owner = lpt_assign([u[3] for u in units], self.world)
         mine = [u for u, o in zip(units, owner) if o == self.rank]
-        res = self.local.train_units(mine, seed_base=self.n_evaluated)
+        if trial_ids is None:
+            res = self.local.train_units(mine, seed_base=self.n_evaluated)
+        else:
+            res = self.local.train_units(mine, seed_base=self.n_evaluated, trial_ids=trial_ids)
         self.n_evaluated += len(params_list)
         merged = {}
         for g in self._gather({k: v for k, v in res.items()}):
@@ -431,14 +450,24 @@ class DistributedEvaluator:
             raise RuntimeError("DistributedEvaluator: no chain runner on this rank")
         if self.rank != 0:
             O.reset_stats()
-        res = self.chain_runner.run_now([jobs[i] for i in mine]) if mine else []
+        # a failure on one rank is gathered like a result and raised on every rank,
+        # so no rank is left blocked in the all-gather
+        try:
+            res, err = (self.chain_runner.run_now([jobs[i] for i in mine]) if mine else []), None
+        except Exception as e:  # noqa: BLE001 -- re-raised below on every rank
+            res, err = [], f"rank {self.rank}: {type(e).__name__}: {e}"
         stats = dict(O.STATS) if self.rank != 0 else None
         merged = [None] * len(jobs)
-        for part, st in self._gather(({i: r for i, r in zip(mine, res)}, stats)):
+        errors = []
+        for part, st, e in self._gather(({i: r for i, r in zip(mine, res)}, stats, err)):
+            if e is not None:
+                errors.append(e)
             for i, r in part.items():
                 merged[i] = r
             if st is not None and self.rank == 0:
                 O.merge_stats(st)
+        if errors:
+            raise RuntimeError("ask batches failed: " + "; ".join(errors))
         return merged
 
     def _serve_one(self):
@@ -447,7 +476,7 @@ class DistributedEvaluator:
             return False
         kind, body = msg
         if kind == "train":
-            self._train(body)
+            self._train(*body)
         elif kind == "chains":
             self._chains(body)
         elif kind == "score":
@@ -456,11 +485,14 @@ class DistributedEvaluator:
             raise ValueError(f"unknown round {kind!r}")
         return True
 
-    def evaluate(self, params_list):
+    accepts_trial_ids = True
+
+    def evaluate(self, params_list, trial_ids=None):
         """Rank 0: evaluate a batch over all ranks."""
         params_list = [list(p) for p in params_list]
-        self._announce(("train", params_list))
-        return self.local.foms(params_list, self._train(params_list))
+        ids = None if trial_ids is None else [int(i) for i in trial_ids]
+        self._announce(("train", (params_list, ids)))
+        return self.local.foms(params_list, self._train(params_list, ids))
 
     def chains(self, jobs):
         """Rank 0: run ask batches (optimizer.ChainJob) over all ranks -> [(X, trace)]."""

@@ -24,9 +24,6 @@ waited for when the population that trains it is about to start
   HIP stream (a refit is ~100 latency-bound L-BFGS-B rounds of small kernels;
   several chains keep the GPU busy, and ctypes releases the GIL while a round
   waits on its stream);
-* :class:`ProcessChainExecutor` -- spawned worker processes, each with a few
-  worker threads (the chains' host-side L-BFGS-B -- scipy's ``setulb`` -- holds
-  the GIL, ~70 us per round: one interpreter saturates at ~4 chains);
 * :class:`DistributedChainExecutor` -- the batches of one population dealt over
   the torch.distributed ranks (LPT on the refit cost), each rank running its
   share on its own worker threads, results all-gathered to rank 0.
@@ -147,6 +144,7 @@ class ThreadChainExecutor:
         self.wait_s = 0.0           # seconds callers blocked waiting for a batch
         self.durations = []         # (submission number, seconds) per finished batch
         self._lock = threading.Lock()
+        self._cancelled = None      # set by cancel(): queued batches fail with it instead of running
         if start:
             for w in range(self.workers):
                 t = threading.Thread(target=self._worker, name=f"chain-{w}", daemon=True)
@@ -157,14 +155,22 @@ class ThreadChainExecutor:
         import torch
 
         stream = None
-        if self.device is not None and torch.cuda.is_available():
-            dev = torch.device(self.device)
-            torch.cuda.set_device(dev)
-            stream = torch.cuda.Stream(dev)
+        try:
+            if self.device is not None and torch.cuda.is_available():
+                dev = torch.device(self.device)
+                torch.cuda.set_device(dev)
+                stream = torch.cuda.Stream(dev)
+        except BaseException as e:  # noqa: BLE001 -- every batch this worker takes fails with it
+            setup_error = e
+        else:
+            setup_error = None
         while True:
             batch = self._q.get()
             if batch is None:
                 return
+            if setup_error is not None or self._cancelled is not None:
+                batch._set(error=setup_error or self._cancelled)
+                continue
             t0 = time.perf_counter()
             try:
                 if stream is not None:
@@ -202,154 +208,17 @@ class ThreadChainExecutor:
         batch._done.wait()
         self.wait_s += time.perf_counter() - t0
 
+    def cancel(self, reason="ask batches cancelled"):
+        """Fail every batch not started yet (the search's error path: close() then
+        does not run ~256 refits per queued batch before the error surfaces)."""
+        self._cancelled = RuntimeError(reason)
+
     def close(self):
         for _ in self._threads:
             self._q.put(None)
         for t in self._threads:
             t.join()
         self._threads = []
-
-
-def _process_init(device):
-    """Chain worker process: bind the GPU once (spawned interpreter, fresh HIP context)."""
-    if device is not None:
-        import torch
-
-        torch.cuda.set_device(torch.device(device))
-
-
-def _take_stats():
-    """This process's refit accounts since the last call (then reset)."""
-    from . import optimizer as O
-
-    with O.STATS_LOCK:
-        snap = {k: (list(v) if isinstance(v, list) else v) for k, v in O.STATS.items()}
-    O.reset_stats()
-    return snap
-
-
-def _process_main(init, device, threads, in_q, out_q):
-    """A chain worker process: ``threads`` chains at a time on its own
-    :class:`ThreadChainExecutor`; results (and the refit accounts gathered since
-    the previous result) go back in submission order."""
-    import pickle
-
-    init(device)
-    local = ThreadChainExecutor(device, threads)
-    pending = queue.Queue()
-
-    def report():
-        busy0 = 0.0
-        while True:
-            item = pending.get()
-            if item is None:
-                return
-            seq, b = item
-            b._done.wait()
-            err = b._error
-            if err is not None:
-                try:
-                    pickle.dumps(err)
-                except Exception:  # noqa: BLE001 -- an unpicklable error travels as its repr
-                    err = RuntimeError(repr(err))
-            busy = local.busy_s
-            out_q.put((seq, b._X, b._trace, err, _take_stats(), busy - busy0, b.run_s))
-            busy0 = busy
-
-    reporter = threading.Thread(target=report, daemon=True)
-    reporter.start()
-    while True:
-        msg = in_q.get()
-        if msg is None:
-            break
-        seq, job = msg
-        pending.put((seq, local.submit(job)))
-    pending.put(None)
-    reporter.join()
-    local.close()
-    out_q.put(None)
-
-
-class ProcessChainExecutor:
-    """Runs batches in ``workers`` spawned processes sharing ``device``, each running
-    ``threads`` batches at a time (its own HIP context and hardware queues, and its
-    own interpreter: the chains' host side -- scipy's L-BFGS-B, which holds the GIL
-    -- runs in parallel across processes).  Batches go to whichever process is free
-    (one shared queue); their refit accounts are merged into this process's STATS."""
-
-    def __init__(self, device=None, workers=2, threads=1):
-        import multiprocessing as mp
-
-        ctx = mp.get_context("spawn")
-        self.device = None if device is None else str(device)
-        self.workers, self.threads = int(workers), int(threads)
-        self._in, self._out = ctx.Queue(), ctx.Queue()
-        init = globals()["_process_init"]          # looked up now (tests substitute it)
-        self._procs = [ctx.Process(target=_process_main, args=(init, self.device, self.threads, self._in, self._out),
-                                   daemon=True) for _ in range(self.workers)]
-        for pr in self._procs:
-            pr.start()
-        self._seq = 0
-        self._batches = {}
-        self._lock = threading.Lock()
-        self.busy_s = 0.0
-        self.wait_s = 0.0
-        self.durations = []
-        self._collector = threading.Thread(target=self._collect, daemon=True)
-        self._collector.start()
-
-    def _collect(self):
-        from . import optimizer as O
-
-        live = len(self._procs)
-        while live:
-            try:
-                msg = self._out.get(timeout=1.0)
-            except queue.Empty:
-                dead = [pr for pr in self._procs if pr.exitcode not in (None, 0)]
-                if dead:   # a worker died: fail every batch still outstanding
-                    with self._lock:
-                        outstanding, self._batches = list(self._batches.values()), {}
-                    for b in outstanding:
-                        b._set(error=RuntimeError(f"chain worker process exited with {dead[0].exitcode}"))
-                    return
-                continue
-            if msg is None:
-                live -= 1
-                continue
-            seq, X, trace, err, stats, busy, run_s = msg
-            O.merge_stats(stats)
-            with self._lock:
-                self.busy_s += busy
-                self.durations.append((seq, run_s))
-                b = self._batches.pop(seq)
-            b.run_s = run_s
-            b._set(X, trace, err)
-
-    def submit(self, job):
-        b = LazyBatch(self, job)
-        with self._lock:
-            b.seq = self._seq
-            self._seq += 1
-            self._batches[b.seq] = b
-        self._in.put((b.seq, job))
-        return b
-
-    def run_now(self, jobs):
-        batches = [self.submit(j) for j in jobs]
-        return [(b.result(), b._trace) for b in batches]
-
-    def wait(self, batch):
-        t0 = time.perf_counter()
-        batch._done.wait()
-        self.wait_s += time.perf_counter() - t0
-
-    def close(self):
-        for _ in self._procs:
-            self._in.put(None)
-        self._collector.join()
-        for pr in self._procs:
-            pr.join()
 
 
 class DistributedChainExecutor:

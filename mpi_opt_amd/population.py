@@ -384,11 +384,24 @@ def kfold_gather(X, idx, out=None):
     return out
 
 
-def synthetic_mnist(n=60000, seed=0, device=None):
-    """x ~ U[0,1] f32 (n, 784), labels uniform 0..9, generated on device."""
+def synthetic_mnist(n=60000, seed=0, device=None, labels="uniform"):
+    """x ~ U[0,1] f32 (n, 784), generated on device.
+
+    ``labels="uniform"``: labels uniform 0..9 (§8d; nothing to learn, so every
+    trial's validation loss is the uniform-softmax BCE and a search sees a flat
+    objective).  ``labels="learnable"``: the label of an image is the argmax of a
+    fixed random linear teacher over its 4x4-average-pooled 7x7 image, centred at
+    0.5 -- a function a test_mnist CNN learns, so trials differ by their
+    hyper-parameters and the GP of a search fits a non-flat objective."""
     g = torch.Generator(device=device if device is not None else "cuda")
     g.manual_seed(seed)
     dev = torch.device(device if device is not None else "cuda")
     x = torch.rand(n, IMG * IMG, generator=g, device=dev, dtype=torch.float32)
     y = torch.randint(0, NUM_CLASSES, (n,), generator=g, device=dev, dtype=torch.int32)
+    if labels == "learnable":
+        w = torch.randn(49, NUM_CLASSES, generator=g, device=dev, dtype=torch.float32)
+        pooled = x.view(n, 7, 4, 7, 4).mean(dim=(2, 4)).reshape(n, 49) - 0.5
+        y = torch.argmax(pooled @ w, dim=1).to(torch.int32)
+    elif labels != "uniform":
+        raise ValueError(f"labels {labels!r}: 'uniform' or 'learnable'")
     return x, y

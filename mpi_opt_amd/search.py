@@ -44,9 +44,12 @@ def make_parser():
     p.add_argument("--cache-data", default="", dest="caching_dir",
                    help="mpi_learn data cache dir (no effect here: the data is resident on the GPU)")
     p.add_argument("--early-stopping", default=None, dest="early_stopping",
-                   help="patience for early stopping: N (val_loss) or METRIC,~<,N / METRIC,~>,N")
+                   help="patience for early stopping: N (val_loss) or METRIC,~<,N / METRIC,~>,N "
+                        "(Keras EarlyStopping semantics restated from the flag's help; mpi_learn is "
+                        "un-vendored, so parity unpinned)")
     p.add_argument("--target-metric", default=None, dest="target_metric",
-                   help="stop a fold once METRIC,OP,VALUE holds (e.g. val_acc,>,0.97)")
+                   help="stop a fold once METRIC,OP,VALUE holds (e.g. val_acc,>,0.97; restated from the "
+                        "flag's help, parity unpinned)")
     p.add_argument("--easgd", action="store_true", help="mpi_learn EASGD exchange (no effect here: trials train synchronously on one GPU)")
     p.add_argument("--worker-optimizer", dest="worker_optimizer", default="sgd",
                    help="mpi_learn worker optimizer (no effect here: trials train synchronously on one GPU)")
@@ -66,6 +69,10 @@ def make_parser():
     p.add_argument("--world-size", type=int, default=21,
                    help="rank count of the reference's `mpirun -n` (sets concurrent trials)")
     p.add_argument("--n-samples", type=int, default=60000, help="synthetic MNIST-shape samples")
+    p.add_argument("--synthetic-labels", default="uniform", choices=["uniform", "learnable"],
+                   dest="synthetic_labels",
+                   help="labels of the synthetic data: uniform random (SURVEY §8d; a flat objective) or a "
+                        "fixed random linear teacher on the pooled image (learnable; trials differ)")
     p.add_argument("--data-dir", default=None,
                    help="directory of *.h5 files with `features` / `labels` (option3's mnist data, "
                         "/bigdata/shared/mnist/*.h5); first 70%% of the files train, the rest validate")
@@ -80,9 +87,6 @@ def make_parser():
     p.add_argument("--population-chunks", type=int, default=1, dest="population_chunks",
                    help="train each population in this many parts, each as soon as its ask batches "
                         "resolve (overlaps the remaining batches with training; results unchanged)")
-    p.add_argument("--chain-processes", type=int, default=0,
-                   help="spawned chain worker processes per GPU, each running --chain-workers batches at "
-                        "a time (0: worker threads in this process)")
     return p
 
 
@@ -136,7 +140,7 @@ def run_search(args, x=None, y=None, log=print, progress=None, on_population=Non
     import torch
 
     from .blocks import DistributedEvaluator, PopulationComm, ShardedScorer, TrialEvaluator
-    from .chains import DistributedChainExecutor, ProcessChainExecutor, ThreadChainExecutor
+    from .chains import DistributedChainExecutor, ThreadChainExecutor
     from .models import BuilderFromFunction, mnist_space, test_mnist
     from .population import synthetic_mnist
     from .scheduler import AskTellScheduler
@@ -148,9 +152,11 @@ def run_search(args, x=None, y=None, log=print, progress=None, on_population=Non
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if ws > 1:
-        import torch.distributed as dist
+    import torch.distributed as _dist
 
+    # a group the caller set up is used even at world size 1 (the RCCL path under test)
+    if ws > 1 or (_dist.is_available() and _dist.is_initialized()):
+        dist = _dist
         if not dist.is_initialized():
             torch.cuda.set_device(local)
             dist.init_process_group("nccl")
@@ -172,7 +178,7 @@ def run_search(args, x=None, y=None, log=print, progress=None, on_population=Non
         log(f"data: {len(train_list)} train / {len(val_list)} validation files, {holdout} / "
             f"{len(yh) - holdout} samples")
     if x is None:
-        x, y = synthetic_mnist(args.n_samples, seed=0, device=dev)
+        x, y = synthetic_mnist(args.n_samples, seed=0, device=dev, labels=args.synthetic_labels)
     evaluator = TrialEvaluator(provider, x, y, n_fold=args.n_fold, epochs=args.epochs, batch=args.batch,
                                lr=args.lr, device=dev, history_dir=args.history_dir, holdout=holdout,
                                progress=progress if (dist is None or dist.get_rank() == 0) else None,
@@ -180,10 +186,7 @@ def run_search(args, x=None, y=None, log=print, progress=None, on_population=Non
     local_eval = evaluator
     chains = None
     if args.chain_workers > 0:
-        if args.chain_processes > 0:
-            chains = ProcessChainExecutor(dev, workers=args.chain_processes, threads=args.chain_workers)
-        else:
-            chains = ThreadChainExecutor(dev, workers=args.chain_workers)
+        chains = ThreadChainExecutor(dev, workers=args.chain_workers)
     if dist is not None:
         evaluator = DistributedEvaluator(evaluator)
         if chains is not None:
@@ -224,6 +227,10 @@ def run_search(args, x=None, y=None, log=print, progress=None, on_population=Non
     try:
         state = sched.run(num_iterations=args.num_iterations)
         wall = time.perf_counter() - t0
+    except BaseException:
+        if chains is not None:      # do not run the queued batches before the error surfaces
+            (getattr(chains, "local", None) or chains).cancel("search failed")
+        raise
     finally:
         if dist is not None:
             evaluator.shutdown()
@@ -245,8 +252,7 @@ def run_search(args, x=None, y=None, log=print, progress=None, on_population=Non
         "ask_s": tm["ask_s"], "tell_s": tm["tell_s"], "asks": tm["asks"], "tells": tm["tells"],
         "chain_wait_s": chain_wait, "chain_workers": args.chain_workers,
         "population_chunks": args.population_chunks,
-        "chain_pool": (f"{args.chain_processes} processes x {args.chain_workers} threads" if args.chain_processes
-                       else f"{args.chain_workers} threads") if chains is not None else None,
+        "chain_pool": f"{args.chain_workers} threads" if chains is not None else None,
         "chain_busy_s": chains.busy_s if chains is not None else 0.0,
         # seconds each ask batch ran on its worker, in submission order (one per ask)
         "chain_run_s": [d for _, d in sorted(getattr(chains, "durations", []) or

@@ -3,7 +3,10 @@ and ``--target-metric`` (/root/reference/hyperparameter_search_option3.py:66-69)
 handed unchanged to mpi_learn's ``MPIKFoldManager(..., early_stopping=...,
 target_metric=...)`` (/root/reference/process_block.py:83-90).
 
-mpi_learn is un-vendored and unpinned.  Its flags are restated as
+mpi_learn is un-vendored and unpinned, so this module's semantics
+are **parity unpinned**: no fixture of the reference pins them.  The epoch
+counts they produce are pinned by tests/test_stopping.py so that they cannot
+change silently.  Its flags are restated as
 the reference's help strings describe them, checked once per epoch after the
 validation pass (the reference validates every epoch, option3:260):
 

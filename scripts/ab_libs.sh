@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build libmpo.so of other git revisions into ab_libs/<name>/libmpo.so for same-box
-# A/B runs (a probe selects one with MPO_LIB_AB=ab_libs/<name>/libmpo.so).
+# A/B runs (a probe selects one with MPO_LIB_AB=ab_libs/<name>/libmpo.so, read by scripts/ab_lib.py).
 #   scripts/ab_libs.sh name=rev [name=rev ...]
 set -e
 cd "$(dirname "$0")/.."

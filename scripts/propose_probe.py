@@ -9,6 +9,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import scripts.ab_lib  # noqa: E402,F401 -- MPO_LIB_AB: another build's libmpo.so (same-box A/B)
 from mpi_opt_amd import gp_fit as GF  # noqa: E402
 from mpi_opt_amd import optimizer as OPT  # noqa: E402
 from mpi_opt_amd.gp import DeviceGP  # noqa: E402

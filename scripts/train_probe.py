@@ -7,6 +7,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+import scripts.ab_lib  # noqa: E402,F401 -- MPO_LIB_AB: another build's libmpo.so (same-box A/B)
 from mpi_opt_amd.population import PopulationEngine, TrialSpec, kfold_split, synthetic_mnist  # noqa: E402
 
 
@@ -27,6 +28,8 @@ def main():
     ap.add_argument("--shard", default=None,
                     help="K/N: only rank K's LPT-by-FLOPs share of the (trial, fold) units over N ranks "
                          "(what one GPU trains of the population in the distributed search)")
+    ap.add_argument("--no-eval", action="store_true",
+                    help="train steps only (bench.py's PMC passes divide by the train steps)")
     args = ap.parse_args()
     trials = sample_trials(args.trials)
     members = []
@@ -62,6 +65,8 @@ def main():
     flops = sum(m.flops_per_sample_train() for m in members) * 100
     print("train step %.2f ms  %.1f TFLOP/s  (%.1f%% of 157.3)" % (dt * 1e3, flops / dt / 1e12, flops / dt / 157.3e12 * 100))
     print("loss", eng.loss[:5].cpu().numpy())
+    if args.no_eval:
+        return
     va = np.stack([kfold_split(60000, args.folds, f)[1] for f in folds])
     vorder = torch.from_numpy(va).cuda()
     eng.eval_step(x, y, vorder, 0)

@@ -18,9 +18,10 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from mpi_opt_amd import optimizer as O
-from mpi_opt_amd.blocks import DistributedEvaluator, PopulationComm
-from mpi_opt_amd.chains import DistributedChainExecutor, LazyBatch, LazyPoint, ProcessChainExecutor, ThreadChainExecutor
-from mpi_opt_amd.models import mnist_space
+from mpi_opt_amd.blocks import DistributedEvaluator, PopulationComm, TrialEvaluator
+from mpi_opt_amd.chains import DistributedChainExecutor, LazyBatch, LazyPoint, ThreadChainExecutor
+from mpi_opt_amd.models import BuilderFromFunction, mnist_space
+from mpi_opt_amd.models import test_mnist as mnist_model_fn
 from mpi_opt_amd.scheduler import AskTellScheduler
 
 
@@ -53,9 +54,21 @@ class InstantEval:
         return [float((p[0] * 0.013 + p[1] * 0.07 + p[3] * 0.001 + p[4]) % 1.0) for p in params]
 
 
-def _search(tmp, executor=None, world=9, block=2, iters=24, chunks=1):
+class SeededEval(TrialEvaluator):
+    """A TrialEvaluator whose 'training' depends on each unit's seed (its trial
+    identity), as the device trainer's initial weights and dropout masks do."""
+
+    def __init__(self):
+        super().__init__(BuilderFromFunction(mnist_model_fn, mnist_space()), None, None, n_fold=2)
+
+    def _train_units(self, units, tid):
+        return {(t, f): {"val_loss": [(self._uid(tid(t), f) % 9973) / 9973.0], "val_acc": [0.0]}
+                for (t, f, _, _) in units}
+
+
+def _search(tmp, executor=None, world=9, block=2, iters=24, chunks=1, evaluator=None):
     nb = (world - 1) // block
-    comm = PopulationComm(nb, block, InstantEval(), chunks=chunks)
+    comm = PopulationComm(nb, block, evaluator or InstantEval(), chunks=chunks)
     kw = {"chain_executor": executor} if executor is not None else {}
     O.reset_stats()
     sched = AskTellScheduler(comm, nb, mnist_space(), checkpoint=os.path.join(tmp, "c.pkl"), optimizer_kwargs=kw)
@@ -144,7 +157,7 @@ class _Local:
     def units(self, params_list):
         return [(t, 0, None, 1.0) for t in range(len(params_list))]
 
-    def train_units(self, units, seed_base=0):
+    def train_units(self, units, seed_base=0, trial_ids=None):
         return {(t, 0): None for (t, _, _, _) in units}
 
     def foms(self, params_list, results):
@@ -198,33 +211,6 @@ def test_chains_dealt_over_gloo_ranks_equal_sequential(fake_gp, tmp_path):
         assert got[k] == want[k], k
 
 
-def _patched_process_init(device):
-    from mpi_opt_amd import chains
-
-    O.Optimizer._fit_and_propose = fake_fit_and_propose
-    chains._process_init(device)
-
-
-def test_lazy_process_search_equals_sequential(fake_gp, tmp_path, monkeypatch):
-    """ProcessChainExecutor: batches in spawned processes (the CPU surrogate is
-    installed in each worker by its initializer); same search, refit accounts merged."""
-    import random
-
-    from mpi_opt_amd import chains
-
-    random.seed(5)
-    want = _search(str(tmp_path))
-    monkeypatch.setattr(chains, "_process_init", _patched_process_init)
-    for workers, threads in ((2, 1), (2, 3)):
-        ex = ProcessChainExecutor(device=None, workers=workers, threads=threads)
-        try:
-            random.seed(5)
-            got = _search(str(tmp_path), ex)
-        finally:
-            ex.close()
-        assert got == want, (workers, threads)
-
-
 def test_chunked_populations_equal_whole_populations(fake_gp, tmp_path):
     """--population-chunks: a population trained in parts, each as soon as its own
     ask batches resolve, leaves the search unchanged (told points, FOMs, trained
@@ -241,3 +227,115 @@ def test_chunked_populations_equal_whole_populations(fake_gp, tmp_path):
         finally:
             ex.close()
         assert got == want, chunks
+
+
+def test_chunked_populations_keep_each_trials_seed(fake_gp, tmp_path):
+    """a trial's seed (initial weights, dropout masks) is its
+    population base plus its block-order position, so training a population in
+    parts (reordered by ask-batch submission) gives every trial the same seed and
+    the search the same FOMs as one whole population."""
+    import random
+
+    random.seed(5)
+    want = _search(str(tmp_path), world=17, iters=40, evaluator=SeededEval())
+    assert len(set(want["foms"])) == len(want["foms"])          # the FOMs really are seed-dependent
+    for chunks in (2, 3):
+        ex = ThreadChainExecutor(device=None, workers=3)
+        try:
+            random.seed(5)
+            got = _search(str(tmp_path), ex, world=17, iters=40, chunks=chunks, evaluator=SeededEval())
+        finally:
+            ex.close()
+        assert got == want, chunks
+
+
+class _SlowJob:
+    n_points, cost = 1, 1.0
+
+    def __init__(self, fail=False):
+        self.fail = fail
+
+    def run(self, device=None, scorer=None):
+        import time
+
+        time.sleep(0.2)
+        if self.fail:
+            raise ValueError("boom")
+        return [[1]], None
+
+
+def test_cancel_fails_queued_batches_instead_of_running_them():
+    """on the search's error path the queued batches fail at once
+    (close() does not run them first); a batch already running finishes."""
+    import time
+
+    ex = ThreadChainExecutor(device=None, workers=1)
+    bs = [ex.submit(_SlowJob()) for _ in range(4)]
+    time.sleep(0.05)
+    ex.cancel("search failed")
+    t0 = time.perf_counter()
+    ex.close()
+    assert time.perf_counter() - t0 < 0.5
+    assert bs[0].result() == [[1]]
+    for b in bs[1:]:
+        with pytest.raises(RuntimeError, match="search failed"):
+            b.result()
+
+
+def test_worker_setup_failure_fails_its_batches(monkeypatch):
+    """a worker whose device / stream setup fails does not die
+    silently: every batch it takes fails with the setup error."""
+    import torch
+
+    def bad_set_device(dev):
+        raise RuntimeError("no such device")
+
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "set_device", bad_set_device)
+    ex = ThreadChainExecutor(device="cuda:7", workers=2)
+    try:
+        b = ex.submit(_SlowJob())
+        with pytest.raises(RuntimeError, match="no such device"):
+            b.result()
+    finally:
+        ex.close()
+
+
+class _FailingRunner:
+    def __init__(self, rank):
+        self.rank = rank
+
+    def run_now(self, jobs):
+        if self.rank == 1:
+            raise ValueError("chain broke on rank 1")
+        return [([[0]], None) for _ in jobs]
+
+
+def _err_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ev = DistributedEvaluator(_Local(), chain_runner=_FailingRunner(rank))
+    try:
+        if rank == 0:
+            ev.chains([_SlowJob() for _ in range(4)])
+        else:
+            ev.serve()
+        q.put((rank, "no error"))
+    except RuntimeError as e:
+        q.put((rank, str(e)))
+    dist.destroy_process_group()
+
+
+def test_a_chain_failure_on_one_rank_raises_on_every_rank():
+    """a rank whose chains raise joins the all-gather with its error,
+    so the others do not block in it; every rank raises."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_err_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    assert all("chain broke on rank 1" in m for m in got.values()), got

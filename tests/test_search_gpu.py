@@ -134,3 +134,71 @@ def test_configs3_layout_concurrent_chains_equal_sequential(tmp_path):
     assert par["trained_params"] == seq["trained_params"]
     assert par["best_fom"] == seq["best_fom"] and par["best_params"] == seq["best_params"]
     assert par["chain_wait_s"] > 0 and seq["chain_wait_s"] == 0
+
+
+def _nccl_search3_worker(port, tmp, q):
+    """One rank over RCCL: the configs[3] layout through DistributedEvaluator,
+    DistributedChainExecutor and ShardedScorer, plus one sharded scoring round."""
+    import pathlib
+    import types
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        rep = _search3(pathlib.Path(tmp), 4)
+        from mpi_opt_amd.blocks import DistributedEvaluator, local_topk
+
+        rng = np.random.RandomState(4)
+        req = {"Xt": rng.rand(40, 5), "y": rng.rand(40), "amp": 1.3, "ls": np.full(5, 0.4), "noise": 1e-5,
+               "cand": rng.rand(20000, 5), "y_opt": 0.01, "acqs": ["EI", "LCB", "PI"], "xi": 0.01,
+               "kappa": 1.96, "k": 5}
+        ev = DistributedEvaluator(types.SimpleNamespace(device=torch.device("cuda", 0)))
+        got = ev.score(req)            # broadcast + all_gather of the top-k over RCCL
+        want = local_topk(req, 0, len(req["cand"]), device=torch.device("cuda", 0))
+        score_ok = all(np.array_equal(got[a][1], want[a][1]) and np.array_equal(got[a][0], want[a][0])
+                       for a in req["acqs"])
+        maps = open("/proc/self/maps").read()
+        rccl = sorted({ln.split()[-1] for ln in maps.splitlines() if "librccl" in ln})
+        q.put({k: rep[k] for k in ("told_params", "told_foms", "trained_params", "populations", "best_fom",
+                                   "best_params", "refit_ns")}
+              | {"refits": rep["gp"]["refits"], "backend": dist.get_backend(), "rccl": rccl,
+                 "score_ok": bool(score_ok)})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_configs3_layout_over_rccl_equals_one_process(tmp_path):
+    """the configs[3] path's collectives on RCCL.  A world-size-1
+    ``nccl`` group (the 1-GPU box cannot host two RCCL ranks) runs the search with
+    the distributed evaluator, the chains dealt over the ranks and the sharded
+    scorer: every broadcast_object_list / all_gather_object goes through RCCL's
+    device-tensor staging (the reference's send / irecv exchange,
+    coordinator.py:140-150, option3:172-205).  Told points, FOMs, trained trials
+    and the refit multiset equal the non-distributed run; a sharded scoring round
+    returns the single-device top-k bit for bit."""
+    import torch.multiprocessing as mp
+
+    s = __import__("socket").socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_search3_worker, args=(port, str(tmp_path), q))
+    p.start()
+    got = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert got["backend"] == "nccl" and got["rccl"], "RCCL was not loaded"
+    assert got["score_ok"]
+    want = _search3(tmp_path, 4)
+    assert got["populations"] == want["populations"] == [8, 8, 8, 8]
+    assert got["told_params"] == want["told_params"] and got["told_foms"] == want["told_foms"]
+    assert got["trained_params"] == want["trained_params"]
+    assert got["refits"] == want["gp"]["refits"] and got["refit_ns"] == want["refit_ns"]
+    assert got["best_fom"] == want["best_fom"] and got["best_params"] == want["best_params"]

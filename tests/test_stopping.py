@@ -90,3 +90,28 @@ def test_trial_fom_is_the_loss_at_the_stopping_epoch():
     res = ev._histories(units, hist)
     assert res[(0, 0)]["val_loss"] == [0.5, 0.4] and res[(0, 1)]["val_loss"] == [0.6, 0.3, 0.2]
     assert ev.foms([[10, 2, 2, 50, 0.1]], res) == [pytest.approx((0.4 + 0.2) / 2)]
+
+
+def test_epoch_counts_are_pinned_for_every_form():
+    """The stopping epochs each flag form gives on one scripted history (parity
+    unpinned against mpi_learn; pinned here so the behaviour cannot drift)."""
+    loss = np.array([[1.0, 0.9, 0.95, 0.96, 0.97, 0.5],
+                     [1.0, 1.0, 1.0, 1.0, 1.0, 1.0],
+                     [0.9, 0.8, 0.7, 0.6, 0.5, 0.4]])
+    acc = np.array([[0.1, 0.5, 0.4, 0.4, 0.4, 0.9],
+                    [0.2, 0.2, 0.3, 0.3, 0.3, 0.3],
+                    [0.1, 0.2, 0.3, 0.96, 0.99, 0.99]])
+
+    def epochs(es, tm):
+        st = StopRule.from_args(es, tm).start(3)
+        for e in range(loss.shape[1]):
+            st.update(e, loss[:, e], acc[:, e])
+        return st.epochs(loss.shape[1]).tolist()
+
+    assert epochs("1", None) == [3, 2, 6]
+    assert epochs("3", None) == [5, 4, 6]
+    assert epochs("val_acc,~>,1", None) == [3, 2, 6]
+    assert epochs("val_acc,~>,2", None) == [4, 5, 6]
+    assert epochs(None, "val_acc,>,0.95") == [6, 6, 4]
+    assert epochs(None, "val_loss,<=,0.6") == [6, 6, 4]
+    assert epochs("2", "val_acc,>=,0.99") == [4, 3, 5]
