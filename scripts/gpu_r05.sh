@@ -1,5 +1,5 @@
 #!/bin/bash
-# One GPU session (round 4).  Every GPU step has its own time limit; steps are
+# One GPU session (round 5).  Every GPU step has its own time limit; steps are
 # chained with && so the first failure (fault, abort, time limit) ends the script.
 #   TESTS=<pytest paths|none>  TEST_TIMEOUT=<s>  PROBES=<python commands separated by ';;'>
 #   BENCH=0|1  BENCH_ARGS=<args>  PROF=1  TAG=<suffix>
@@ -7,7 +7,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-TAG=${TAG:-r04}
+TAG=${TAG:-r05}
 TESTS=${TESTS:-tests}
 step_tests() {
   [ "$TESTS" = "none" ] && return 0
