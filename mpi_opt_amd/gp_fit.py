@@ -89,6 +89,19 @@ class DeviceLML:
         tail = (self.out_h.data_ptr(), _lib.ptr(self.io), self.io_bytes, _lib.ptr(self.ws), self.ws_bytes, self._stream)
         self._call = lambda B: fn(*args, B, *tail)
 
+    def negated_round(self, thetas, ids=None):
+        """(-lml [B], -grad [B, d+2]) for the L-BFGS-B driver: ``thetas`` is its
+        C-contiguous float64 [B, d+2] buffer; fresh arrays out."""
+        B = len(thetas)
+        if B > self._cap:
+            self._ensure(B)
+        self._th_np[:B] = thetas
+        rc = self._call(B)
+        if rc != 0:
+            _lib.check(rc, "mpo_gp_lml_grad_host")
+        h = self._out_np
+        return -h[:B], -(h[B:B + B * (self.d + 2)].reshape(B, self.d + 2))
+
     def evaluate(self, thetas):
         """thetas [B, d+2] (log space) -> (lml [B], grad [B, d+2], info [B]) as numpy:
         one ``mpo_gp_lml_grad_host`` call (copy in, objective, copy out, sync)."""
@@ -200,28 +213,68 @@ def lbfgsb_batched(evaluate, starts, bounds, ftol=MINIMIZE_FTOL, gtol=1e-5, maxi
     scipy's reverse-communication ``setulb`` exactly as ``scipy.optimize.minimize
     (method="L-BFGS-B", jac=True)`` (``ftol=MINIMIZE_FTOL``) or ``fmin_l_bfgs_b``
     (``ftol=FMIN_FTOL``) would, so each run's iterates are those of a sequential
-    scipy call.  Returns ([(x, f)] per run, number of rounds)."""
+    scipy call.  Returns ([(x, f)] per run, number of rounds).
+
+    The loop holds the GIL between the device rounds (concurrent cl_min chains,
+    mpi_opt_amd.chains, share it): the _LbfgsbRun protocol (deliver, then
+    advance) is inlined and the rows of ``g`` are handed to the runs without a
+    copy, so ``evaluate`` must return fresh arrays.  (r05: ~18 us of host time per
+    round of 3 runs on the GPU box, scripts/lbfgs_host_bench.py, the same as the
+    method-per-run form; the cProfile'd chain makes a third fewer Python calls.)"""
     setulb = _setulb()
     runs = [_LbfgsbRun(x0, bounds, ftol, gtol, maxiter, maxfun) for x0 in starts]
-    want = {i: r.request() for i, r in enumerate(runs)}
-    buf = np.empty((len(runs), runs[0].x.size), dtype=np.float64)   # the round's points (no np.stack)
+    r0 = runs[0]
+    m, low, up, nbd, factr, pgtol, maxls = r0.m, r0.low, r0.up, r0.nbd, r0.factr, r0.pgtol, r0.maxls
+    live = list(range(len(runs)))
+    want = [r.request() for r in runs]
+    buf = np.empty((len(runs), r0.x.size), dtype=np.float64)   # the round's points (no np.stack)
     rounds = 0
-    while want:
-        ids = sorted(want)
-        X = buf[:len(ids)]
-        for k, i in enumerate(ids):
-            X[k] = want[i]
-        f, g = evaluate(X, ids)
+    while live:
+        nl = len(live)
+        X = buf[:nl]
+        for k in range(nl):
+            X[k] = want[live[k]]
+        f, g = evaluate(X, live)
         rounds += 1
-        g = np.asarray(g, dtype=np.float64)
-        for k, i in enumerate(ids):
-            runs[i].deliver(want[i], float(f[k]), g[k].copy())
-        nxt = {}
-        for i in ids:
-            x = runs[i].advance(setulb)
-            if x is not None:
-                nxt[i] = x
-        want = nxt
+        nxt = []
+        for k in range(nl):
+            i = live[k]
+            r = runs[i]
+            # deliver: the ScalarFunction cache, then (after the first) the run's f, g
+            x = want[i]
+            fk, gk = float(f[k]), g[k]
+            r.sf_x, r.sf_f, r.sf_g = x, fk, gk
+            sfx = x.tolist()
+            r.nfev += 1
+            if r.started:
+                r.f, r.g = fk, gk
+            r.started = True
+            # advance: setulb until it asks for f, g at a new point or stops
+            task, rx = r.task, r.x
+            while True:
+                rg = r.g
+                if rg.dtype != np.float64:      # scipy's g.astype(np.float64) (the START call only)
+                    rg = r.g = rg.astype(np.float64)
+                setulb(m, rx, low, up, nbd, r.f, rg, factr, pgtol, r.wa, r.iwa, task, r.lsave, r.isave, r.dsave,
+                       maxls, r.ln_task)
+                t0 = task[0]
+                if t0 == 3:
+                    if rx.tolist() == sfx:      # ScalarFunction's cache: the same x (elementwise ==)
+                        r.f, r.g = r.sf_f, r.sf_g
+                        continue
+                    want[i] = rx.copy()
+                    nxt.append(i)
+                    break
+                if t0 == 1:
+                    r.nit += 1
+                    if r.nit >= r.maxiter:
+                        task[0], task[1] = 5, 504
+                    elif r.nfev > r.maxfun:
+                        task[0], task[1] = 5, 502
+                    continue
+                r.done = True
+                break
+        live = nxt
     return [(r.x, float(r.f)) for r in runs], rounds
 
 
@@ -297,9 +350,13 @@ def lockstep_lbfgsb(evaluate, d, random_state=None, n_restarts_optimizer=2, retu
         starts.append(rng.uniform(bounds[:, 0], bounds[:, 1]))
 
     if _setulb() is not None:                # one thread, setulb in reverse communication
-        def neg(thetas, ids):
-            v, g = evaluate(thetas)[:2]
-            return -np.asarray(v), -np.asarray(g)
+        fast = getattr(evaluate, "__self__", None)
+        if isinstance(fast, DeviceLML):
+            neg = fast.negated_round             # the device round, negated, without the checks
+        else:
+            def neg(thetas, ids):
+                v, g = evaluate(thetas)[:2]
+                return -np.asarray(v), -np.asarray(g)
         optima, launches = lbfgsb_batched(neg, starts, bounds)
         return _pick(optima, starts, launches, d, return_details)
 

@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--jobs", type=int, default=32)
     ap.add_argument("--threads", type=int, nargs="+", default=[1, 4, 8])
     a = ap.parse_args()
+    if os.environ.get("PY_SWITCH"):
+        sys.setswitchinterval(float(os.environ["PY_SWITCH"]))
+    print("switch interval", sys.getswitchinterval())
     dev = torch.device("cuda:0")
     space = Space(mnist_space())
     rng = np.random.RandomState(0)
