@@ -75,6 +75,7 @@ struct ConvArgs {
     float* out; long long out_ms; int out_ps;
     int H, W, Cin, N, R;
     int pool;      // 1: out is AvgPool2D((2,2)) of the conv output, [B][H/2][W/2] (R, y0 even)
+    int c1x1;      // 1x1 convs: dn_conv1x1_kernel where it applies (DnPlan::conv1x1)
 };
 
 struct WgArgs {
@@ -427,6 +428,100 @@ __global__ __launch_bounds__(256) void dn_conv_kernel(ConvArgs a) {
             for (int r = 0; r < 4; ++r) {
                 const int mm = mt * 16 + krow * 4 + r;
                 if (mm < Mc) dst[(long long)mm * a.out_ps + n] = acc[i][j][r];
+            }
+        }
+    }
+}
+
+// ============================================================================
+// 1x1 convolution (the transitions: forward with BN + ELU and the AvgPool2 epilogue,
+// and the input gradient), streamed without LDS staging (r05).  K = cin is small
+// (40, 64 at the reference config), so dn_conv_kernel's per-workgroup staging and
+// barriers dominated it (conv<1, 3>: 0.36 ms per launch, 2.7x the HBM time).  Here
+// a wave owns a 2 x 8 pixel patch: lane (t = l % 16, q = l / 16) loads pixel t's
+// channels [16 v + 4 q, +4) as one float4 per 16-channel block v, applies BN + ELU
+// in registers, and component i of block v is MFMA k-step (v, i) over the channels
+// {16 v + 4 q' + i}; the B rows are the same channels.  Every load of the wave is
+// issued before its first MFMA.  The pooled epilogue adds the 2 x 2 neighbours
+// across lanes l and l + 32 in dn_pool_fwd's order, ((x00 + x01) + x10) + x11.
+// ============================================================================
+template <int NT, int CB, bool POOL>
+__global__ __launch_bounds__(256) void dn_conv1x1_kernel(ConvArgs a) {
+    const int m = blockIdx.z, b = blockIdx.y;
+    const int H = a.H, W = a.W, Cin = a.Cin;
+    const int lane = threadIdx.x & 63;
+    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int tw = W >> 3, ntile = (H >> 1) * tw;
+    if (tile >= ntile) return;
+    const int h0 = 2 * (tile / tw), w0 = 8 * (tile % tw);
+    const int t = lane & 15, q = lane >> 4;
+    const int hy = h0 + (t >> 3), wx = w0 + (t & 7);
+    const float* src = a.in + m * a.in_ms + (((long long)b * H + hy) * W + wx) * a.in_ps;
+    float4 xv[CB];
+#pragma unroll
+    for (int v = 0; v < CB; ++v) {
+        const int c = 16 * v + 4 * q;
+        xv[v] = *reinterpret_cast<const float4*>(src + min(c, (Cin - 4) & ~3));   // clamped, zeroed below
+    }
+    const float* Wt = a.w + m * a.w_ms;
+    constexpr int N16 = NT * 16;
+    float bw[CB][4][NT];
+#pragma unroll
+    for (int v = 0; v < CB; ++v)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) bw[v][i][j] = Wt[(16 * v + 4 * q + i) * N16 + 16 * j + t];
+    float sc = 1.f, sh = 0.f;
+    if (a.bnc) {
+        const float* bnc = a.bnc + m * a.bnc_ms;
+        sc = bnc[2 * H + hy];
+        sh = bnc[3 * H + hy];
+    }
+    f32x4 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int v = 0; v < CB; ++v) {
+        const int c = 16 * v + 4 * q;
+        float z[4] = {xv[v].x, xv[v].y, xv[v].z, xv[v].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (a.bnc) z[i] = bn_elu(z[i], sc, sh);
+            if (c + i >= Cin) z[i] = 0.f;
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(z[i], bw[v][i][j], acc[j], 0, 0, 0);
+        }
+    }
+    // C: lane (col n = 16 j + t, row group q) holds rows 4 q + r = patch pixels
+    // (row (4 q + r) / 8, column (4 q + r) % 8)
+    if constexpr (POOL) {
+        const int H2 = H >> 1, W2 = W >> 1;
+        float* dst = a.out + m * a.out_ms + ((long long)b * H2 + (h0 >> 1)) * W2 * a.out_ps;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int n = 16 * j + t;
+            // lanes q = 0, 1 own the top row's pairs (r0, r1), (r2, r3); q + 2 the bottom row's
+            const float lo0 = acc[j][0] + acc[j][1], lo1 = acc[j][2] + acc[j][3];
+            const float b00 = __shfl_xor(acc[j][0], 32), b01 = __shfl_xor(acc[j][1], 32);
+            const float b10 = __shfl_xor(acc[j][2], 32), b11 = __shfl_xor(acc[j][3], 32);
+            if (q < 2 && n < a.N) {
+                const int pc = (w0 >> 1) + 2 * q;   // pooled column of (r0, r1)
+                dst[(long long)pc * a.out_ps + n] = 0.25f * ((lo0 + b00) + b01);
+                dst[(long long)(pc + 1) * a.out_ps + n] = 0.25f * ((lo1 + b10) + b11);
+            }
+        }
+    } else {
+        float* dst = a.out + m * a.out_ms + ((long long)b * H * W) * a.out_ps;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int n = 16 * j + t;
+            if (n >= a.N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int pt = 4 * q + r;
+                const int py = h0 + (pt >> 3), px = w0 + (pt & 7);
+                dst[((long long)py * W + px) * a.out_ps + n] = acc[j][r];
             }
         }
     }
@@ -1318,6 +1413,8 @@ struct DnPlan {
     // stream beside the input-gradient convs and BN backward (MPO_DN_PLAN=streams=1:
     // one stream); see enqueue_backward for what they read and write
     mpo::SideStream side;
+    // the transitions' 1x1 convs streamed by dn_conv1x1_kernel (MPO_DN_PLAN=c1x1=0: dn_conv_kernel)
+    bool conv1x1 = true;
 };
 
 // (member stride, offset) allocator over the member-major activation arena
@@ -1515,8 +1612,47 @@ void launch_wg3_t(const WgArgs& a, dim3 grid, size_t lds, hipStream_t s) {
     hipLaunchKernelGGL(kern, grid, dim3(kWgWaves * 64), lds, s, a);
 }
 
+// dn_conv1x1_kernel: a 2 x 8 patch per wave (even H, W % 8 == 0), float4 channel
+// blocks (cin % 4 == 0, 16-B aligned rows), cin <= 16 CB with CB <= 4, N <= 64
+bool conv1x1_ok(const ConvArgs& a) {
+    auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+    return !a.order && a.H % 2 == 0 && a.W % 8 == 0 && a.Cin % 4 == 0 && a.Cin <= 64 && a.N <= 64 &&
+           a.in_ps % 4 == 0 && a.in_ms % 4 == 0 && al(a.in);
+}
+
+template <int NT, int CB>
+void launch_c1x1(const ConvArgs& a, dim3 grid, hipStream_t s) {
+    if (a.pool) hipLaunchKernelGGL((dn_conv1x1_kernel<NT, CB, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((dn_conv1x1_kernel<NT, CB, false>), grid, dim3(256), 0, s, a);
+}
+
+template <int NT>
+void launch_c1x1_cb(const ConvArgs& a, dim3 grid, int cb, hipStream_t s) {
+    switch (cb) {
+        case 1: launch_c1x1<NT, 1>(a, grid, s); break;
+        case 2: launch_c1x1<NT, 2>(a, grid, s); break;
+        case 3: launch_c1x1<NT, 3>(a, grid, s); break;
+        default: launch_c1x1<NT, 4>(a, grid, s); break;
+    }
+}
+
+int launch_conv1x1(const ConvArgs& a, int n_members, int B, hipStream_t s) {
+    const int tiles = (a.H / 2) * (a.W / 8);
+    const dim3 grid((tiles + 3) / 4, B, n_members);
+    const int cb = (a.Cin + 15) / 16;
+    switch ((a.N + 15) / 16) {
+        case 1: launch_c1x1_cb<1>(a, grid, cb, s); break;
+        case 2: launch_c1x1_cb<2>(a, grid, cb, s); break;
+        case 3: launch_c1x1_cb<3>(a, grid, cb, s); break;
+        default: launch_c1x1_cb<4>(a, grid, cb, s); break;
+    }
+    MPO_LAUNCH_CHECK();
+    return MPO_OK;
+}
+
 template <int KS>
 int launch_conv(const ConvArgs& a, int n_members, int B, hipStream_t s) {
+    if (KS == 1 && a.c1x1 && conv1x1_ok(a)) return launch_conv1x1(a, n_members, B, s);
     const int nt = (a.N + 15) / 16;
     const dim3 grid((a.H + a.R - 1) / a.R, B, n_members);
     size_t lds = conv_lds(a.R, a.W, KS, a.Cin);
@@ -1697,11 +1833,12 @@ int enqueue_forward(DnPlan& p, const float* x, const int* labels, const int* ord
         c.bnc = bn.coef; c.bnc_ms = bn.coef_ms;
         c.w = p.act + ly.wf_off; c.w_ms = ((long long)ly.wf_rows * ly.wf_n16 + 63) & ~63LL;
         c.H = ly.H; c.W = ly.W; c.Cin = ly.cin; c.N = ly.cout; c.R = ly.R;
+        c.c1x1 = p.conv1x1 ? 1 : 0;
         if (ly.kind == K_DENSE) {
             c.out = p.act + p.cat_off[st] + ly.coff; c.out_ms = p.cat_ms[st]; c.out_ps = p.sC[st];
             DN_TRY(launch_conv<3>(c, n, B, s));
         } else {
-            if (ly.R % 2 == 0) {
+            if (ly.R % 2 == 0 || (c.c1x1 && conv1x1_ok(c))) {
                 // AvgPool2 in the conv's epilogue: straight into the next stage's concat
                 c.out = p.act + p.cat_off[st + 1]; c.out_ms = p.cat_ms[st + 1]; c.out_ps = p.sC[st + 1];
                 c.pool = 1;
@@ -1798,6 +1935,7 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
         c.w = p.act + ly.wd_off_act; c.w_ms = ((long long)ly.wd_rows * ly.wd_n16 + 63) & ~63LL;
         c.out = p.act + p.dz_off; c.out_ms = p.dz_ms; c.out_ps = ly.cin;
         c.H = ly.H; c.W = ly.W; c.Cin = ly.cout; c.N = ly.cin; c.R = ly.R;
+        c.c1x1 = p.conv1x1 ? 1 : 0;
         if (ly.ks == 3) DN_TRY(launch_conv<3>(c, n, B, s));
         else DN_TRY(launch_conv<1>(c, n, B, s));
         bn.dz = p.act + p.dz_off; bn.dz_ms = p.dz_ms;
@@ -1829,7 +1967,10 @@ int mpo_dn_create(const MpoDnArch* arch, int n_members, int batch, void** handle
     p->n = n_members;
     p->B = batch;
     // A/B switch (one variable, as MPO_POP_PLAN for the MNIST population): streams=1
-    if (const char* e = getenv("MPO_DN_PLAN")) p->side.enabled = strstr(e, "streams=1") == nullptr;
+    if (const char* e = getenv("MPO_DN_PLAN")) {
+        p->side.enabled = strstr(e, "streams=1") == nullptr;
+        p->conv1x1 = strstr(e, "c1x1=0") == nullptr;
+    }
     const int rc = build_plan(*p);
     if (rc != MPO_OK) {
         mpo::set_error("mpo_dn_create: architecture outside the kernels' range (W <= %d, C <= 1024)", kMaxPix);

@@ -215,3 +215,28 @@ def test_side_stream_weight_gradients_bit_identical(monkeypatch):
         out.append((pop.params.clone(), pop.state.clone()))
     assert torch.equal(out[0][0], out[1][0])
     assert torch.equal(out[0][1], out[1][1])
+
+
+def test_streamed_1x1_conv_matches_the_staged_kernel(monkeypatch):
+    """r05: the transitions' 1x1 convs (forward with BN + ELU and the AvgPool2
+    epilogue, and their input gradient) run on dn_conv1x1_kernel, which streams
+    each wave's 2 x 8 pixel patch from HBM without LDS staging and walks K in
+    16-channel float4 blocks.  Only the order of the K sum differs from
+    dn_conv_kernel (MPO_DN_PLAN=c1x1=0): one step's gradients agree to f32
+    rounding, and the oracle tests above run on the streamed kernel."""
+    case = CASES[0]
+    grads = []
+    for plan in ("", "c1x1=0"):
+        if plan:
+            monkeypatch.setenv("MPO_DN_PLAN", plan)
+        else:
+            monkeypatch.delenv("MPO_DN_PLAN", raising=False)
+        pop, layers, init, x, y, order, xd, yd, od_ = _setup(case["img"], case["classes"], case["depth"],
+                                                             case["blocks"], case["growth"], case["nbf"],
+                                                             [1e-3, 3e-2], case["B"], 4 * case["B"], seed=5)
+        pop.train_step(xd, yd, od_, 0)
+        torch.cuda.synchronize()
+        grads.append((pop.grads.clone(), pop.loss.clone()))
+    (ga, la), (gb, lb) = grads
+    assert float((ga - gb).abs().max()) <= 1e-5 * float(gb.abs().max())
+    assert torch.allclose(la, lb, rtol=1e-5, atol=0)
