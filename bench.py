@@ -58,22 +58,23 @@ PMC_FAMILIES = (("conv_img_kernel<0", "conv1_fwd"), ("conv_img_kernel<1", "conv2
                 ("dense_kernel", "dense_kernel"))
 # DenseNet kernels that issue MFMAs (csrc/densenet.hip): the convs (3x3 growth / initial,
 # 1x1 transitions, their input gradients) and the two weight-gradient kernels
-DN_PMC_FAMILIES = (("dn_conv_kernel<3", "conv3x3"), ("dn_conv_kernel<1", "conv1x1"), ("dn_wgrad3_kernel", "wgrad3"),
-                   ("dn_wgrad1_kernel", "wgrad1"))
+DN_PMC_FAMILIES = (("dn_conv_kernel<3", "conv3x3"), ("dn_conv_kernel<1", "conv1x1"), ("dn_conv1x1_kernel", "conv1x1"),
+                   ("dn_wgrad3_kernel", "wgrad3"), ("dn_wgrad1_kernel", "wgrad1"))
 
 
 def mfma_busy(rows, families):
     """SQ_VALU_MFMA_BUSY_CYCLES over the SIMD cycles of the matching dispatches
     (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs), per family and pooled."""
-    per, num, den = {}, 0.0, 0.0
+    acc, num, den = {}, 0.0, 0.0
     for needle, fam in families:
         busy = sum(_per_dispatch(rows, "SQ_VALU_MFMA_BUSY_CYCLES", lambda k: needle in k).values())
         gui = sum(_per_dispatch(rows, "GRBM_GUI_ACTIVE", lambda k: needle in k).values())
         if gui:
-            per[fam] = busy / (gui / 8 * 1024)
+            b0, g0 = acc.get(fam, (0.0, 0.0))
+            acc[fam] = (b0 + busy, g0 + gui / 8 * 1024)   # families sharing a label are pooled
             num += busy
             den += gui / 8 * 1024
-    return (num / den if den else None), per
+    return (num / den if den else None), {f: b / g for f, (b, g) in acc.items()}
 
 
 def pmc_pass(counters, prog, timeout=150):

@@ -162,7 +162,7 @@ def hbm_bytes_train(layers, batch, n_params):
             per_sample += hw * ly["cin"] * 2 + hw * ly["cin"] * 2      # GAP read fwd; dGAP fold + input read bwd
             continue
         q = (ly["H"] // 2) * (ly["W"] // 2) * ly["cout"]
-        if ly["kind"] == "trans" and _pool_fused(ly["H"], ly["W"]):
+        if ly["kind"] == "trans" and (_pool_fused(ly["H"], ly["W"]) or _conv1x1_streamed(ly)):
             per_sample += hw * ly["cin"] + q                           # forward: conv + AvgPool2
             per_sample += hw * ly["cout"] + q                          # AvgPool2 backward
         else:
@@ -173,6 +173,13 @@ def hbm_bytes_train(layers, batch, n_params):
         if ly["kind"] != "conv0":
             per_sample += hw * ly["cin"]                               # input gradient
     return 4 * (batch * per_sample + 8 * n_params)
+
+
+def _conv1x1_streamed(ly):
+    """csrc/densenet.hip conv1x1_ok for a transition: even H, W % 8 == 0, channels
+    multiples of 4 and <= 64 (both its forward and its input gradient)."""
+    H, W, cin, cout = ly["H"], ly["W"], ly["cin"], ly["cout"]
+    return H % 2 == 0 and W % 8 == 0 and cin % 4 == 0 and cout % 4 == 0 and cin <= 64 and cout <= 64
 
 
 def hbm_bytes_train_by_kernel(layers, batch, n_params):
@@ -215,14 +222,16 @@ def hbm_bytes_train_by_kernel(layers, batch, n_params):
             by["dn_bn_bwd_apply_kernel"] += 4 * hw * cin              # dz, x, dcat in; dcat out
         else:                                                         # transition
             q = (ly["H"] // 2) * (ly["W"] // 2) * cout
-            if _pool_fused(ly["H"], ly["W"]):
-                by["dn_conv_kernel"] += hw * cin + q                  # AvgPool2 in the epilogue
+            # r05: the 1x1 convs stream on dn_conv1x1_kernel where it applies
+            c1 = "dn_conv1x1_kernel" if _conv1x1_streamed(ly) else "dn_conv_kernel"
+            if c1 == "dn_conv1x1_kernel" or _pool_fused(ly["H"], ly["W"]):
+                by[c1] += hw * cin + q                                # AvgPool2 in the epilogue
             else:
-                by["dn_conv_kernel"] += hw * (cin + cout)
+                by[c1] += hw * (cin + cout)
                 by["dn_pool_fwd_kernel"] += hw * cout + q
             by["dn_pool_bwd_kernel"] += q + hw * cout
             by["dn_wgrad1_kernel"] += hw * (cin + cout)
-            by["dn_conv_kernel"] += hw * (cout + cin)
+            by[c1] += hw * (cout + cin)
             by["dn_bn_bwd_reduce_kernel"] += 2 * hw * cin
             by["dn_bn_bwd_apply_kernel"] += 3 * hw * cin              # dz, x in; dcat stored
         prev = ly

@@ -108,20 +108,22 @@ def test_python_layer_geometry_matches_oracle_and_spec_ingestion():
 
 
 def test_hbm_models_follow_the_pooled_transition_epilogue(monkeypatch):
-    """The transition's AvgPool2 runs in the 1x1 conv's epilogue when the conv's
-    row chunk is even (csrc/densenet.hip enqueue_forward): the reference grid's
-    transitions (32x32, 16x16: 4- and 8-row chunks) have no separate pool pass
-    and no pre-pool tensor in either HBM model; a 24-wide image (5-row chunks)
-    keeps both."""
+    """The transition's AvgPool2 runs in the 1x1 conv's epilogue when the streamed
+    1x1 kernel applies (even H, W % 8 == 0; r05) or the staged conv's row chunk is
+    even (csrc/densenet.hip enqueue_forward): the reference grid's transitions
+    (32x32, 16x16) have no separate pool pass and no pre-pool tensor in either HBM
+    model, and their 1x1 convs are dn_conv1x1_kernel's; an 18-wide image (7-row
+    chunks, 18 % 8 != 0) keeps both."""
     from mpi_opt_amd import densenet as dn
 
     ref = dn.DenseNetArch().layers()
     by = dn.hbm_bytes_train_by_kernel(ref, 100, 0)
-    assert "dn_pool_fwd_kernel" not in by and by["dn_pool_bwd_kernel"] > 0
-    odd = dn.DenseNetArch(img_dim=(24, 24, 3)).layers()
+    assert "dn_pool_fwd_kernel" not in by and by["dn_pool_bwd_kernel"] > 0 and by["dn_conv1x1_kernel"] > 0
+    odd = dn.DenseNetArch(img_dim=(18, 18, 3)).layers()
     assert dn.hbm_bytes_train_by_kernel(odd, 100, 0)["dn_pool_fwd_kernel"] > 0
     fused_floor, fused_by = dn.hbm_bytes_train(ref, 100, 0), sum(by.values())
     monkeypatch.setattr(dn, "_pool_fused", lambda H, W: False)
+    monkeypatch.setattr(dn, "_conv1x1_streamed", lambda ly: False)
     # unfused, each transition writes its pre-pool output and the pool pass reads it back
     saved = 4 * 100 * sum(2 * ly["H"] * ly["W"] * ly["cout"] for ly in ref if ly["kind"] == "trans")
     assert dn.hbm_bytes_train(ref, 100, 0) - fused_floor == saved
