@@ -1388,7 +1388,8 @@ int env_int(const char* name, int dflt) {
 }
 
 // Planner overrides for tuning sweeps, one variable: MPO_POP_PLAN="key=value,..."
-// (keys: dg_tiles, dg_kb, conv_mt, conv_kb1, conv_kb2, wg_spg1, wg_spg2, streams = 1 | 2 | 3).  Every
+// (keys: dg_tiles, dg_kb, conv_mt, conv_kb1, conv_kb2, wg_spg1, wg_spg2, streams = 1 | 2 | 3,
+// occmerge = 0 | 1).  Every
 // value only changes how work is cut into items or ordered over streams, never the arithmetic.
 int plan_knob(const char* key, int dflt) {
     const char* v = getenv("MPO_POP_PLAN");
@@ -1474,8 +1475,12 @@ int choose_rows(int Ho, Fn lds_of, int kb1 = 52, int kb2 = 78, int mcap = 128) {
 int lds_class(size_t lds) { return (int)std::min<size_t>(8, ((size_t)160 << 10) / std::max<size_t>(lds, 1)); }
 
 template <class T>
-void bucket_segs(std::vector<T>& items, Bucketed& bk, const std::vector<Member>& mem, const std::vector<size_t>& lds) {
-    auto key = [&](const T& x) { return (mem[x.member].nt * 8 + item_sub(x)) * 16 + (8 - lds_class(lds[x.member])); };
+void bucket_segs(std::vector<T>& items, Bucketed& bk, const std::vector<Member>& mem, const std::vector<size_t>& lds,
+                 bool by_occupancy = true) {
+    // by_occupancy = false: one segment per (NT, sub) at the largest member's LDS (fewer, fuller launches)
+    auto key = [&](const T& x) {
+        return (mem[x.member].nt * 8 + item_sub(x)) * 16 + (by_occupancy ? 8 - lds_class(lds[x.member]) : 0);
+    };
     std::stable_sort(items.begin(), items.end(), [&](const T& x, const T& y) { return key(x) < key(y); });
     bk.segs.clear();
     for (int i = 0; i < (int)items.size();) {
@@ -1644,11 +1649,16 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
     long long wmax = 0;
     for (auto& m : P.mem) wmax = std::max(wmax, (long long)m.k * m.k * m.F * m.F + m.F);
     P.wred_blocks = (int)((wmax + P.wred_per_block - 1) / P.wred_per_block);
-    bucket_segs(P.conv1, P.bc1, P.mem, L1);
-    bucket_segs(P.conv2, P.bc2, P.mem, L2);
-    bucket_segs(P.dgrad, P.bdg, P.mem, LD);
-    bucket_segs(P.wg1, P.bw1, P.mem, LW1);
-    bucket_segs(P.wg2, P.bw2, P.mem, LW2);
+    // Small populations (a distributed shard, configs[0]) launch too few workgroups per occupancy class
+    // to fill the chip, so their classes merge; measured on MI355X (profiles/r05/occmerge_o.log):
+    // 20 members 3.82 -> 3.52 ms, 40: 5.93 -> 5.70, 80: 10.94 -> 10.96, 160: 19.81 -> 20.30,
+    // 320: 36.92 -> 39.06 ms per train step. The segmenting changes no arithmetic.
+    const bool occ = plan_knob("occmerge", n <= 64 ? 1 : 0) == 0;
+    bucket_segs(P.conv1, P.bc1, P.mem, L1, occ);
+    bucket_segs(P.conv2, P.bc2, P.mem, L2, occ);
+    bucket_segs(P.dgrad, P.bdg, P.mem, LD, occ);
+    bucket_segs(P.wg1, P.bw1, P.mem, LW1, occ);
+    bucket_segs(P.wg2, P.bw2, P.mem, LW2, occ);
 
     // ---- serialise tables (one device upload)
     size_t off = 0;
