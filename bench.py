@@ -20,6 +20,7 @@ import collections
 import math
 import json
 import os
+import random
 import shutil
 import sys
 import time
@@ -703,6 +704,11 @@ def bench_search(args, torch, dist, ws, rank, dev):
     a = search.make_parser().parse_args(SEARCH_ARGV + list(args.search_args or []))
     with tempfile.TemporaryDirectory() as tmp:
         a.checkpoint = os.path.join(tmp, "coordinator.pkl")
+        # the scheduler polls blocks in random.shuffle order (unseeded in the reference,
+        # coordinator.py:114), which decides which trials train and are told when: seeded
+        # here so every bench run measures the same trials (scripts/search_repeat.py:
+        # unseeded, two runs of this leg trained different trials, 30 s vs 51 s)
+        random.seed(0)
         if ws > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
@@ -757,6 +763,11 @@ def bench_search_gp(args, torch, dist, ws, rank, dev):
     a = search.make_parser().parse_args(argv)
     with tempfile.TemporaryDirectory() as tmp:
         a.checkpoint = os.path.join(tmp, "coordinator.pkl")
+        # the scheduler polls blocks in random.shuffle order (unseeded in the reference,
+        # coordinator.py:114), which decides which trials train and are told when: seeded
+        # here so every bench run measures the same trials (scripts/search_repeat.py:
+        # unseeded, two runs of this leg trained different trials, 30 s vs 51 s)
+        random.seed(0)
         if ws > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)

@@ -1,8 +1,9 @@
 """Run bench.py's configs[0] search twice in one process and compare the runs
-(diagnostic: are the trained trials, their fold losses and the training time
+(diagnostic, ``--seed S`` seeds the block shuffle: are the trained trials, their fold losses and the training time
 reproducible from run to run?)."""
 import json
 import os
+import random
 import sys
 import tempfile
 import time
@@ -14,7 +15,9 @@ ARGV = ["--world-size", "21", "--block-size", "5", "--epochs", "10", "--num-iter
         "--n-fold", "5", "--n-samples", "60000", "--synthetic-labels", "learnable"]
 
 
-def one(extra):
+def one(extra, seed):
+    if seed is not None:
+        random.seed(seed)       # the scheduler's block shuffle (bench.py seeds it)
     a = search.make_parser().parse_args(ARGV + extra)
     with tempfile.TemporaryDirectory() as tmp:
         a.checkpoint = os.path.join(tmp, "coordinator.pkl")
@@ -26,7 +29,10 @@ def one(extra):
 
 def main():
     extra = sys.argv[1:]
-    reps = [one(extra) for _ in range(2)]
+    seed = None
+    if extra[:1] == ["--seed"]:
+        seed, extra = int(extra[1]), extra[2:]
+    reps = [one(extra, seed) for _ in range(2)]
     for r in reps:
         print(json.dumps({"wall_s": r["wall_s"], "train_s": r["train_s"], "populations": r["populations"],
                           "best_fom": r["best_fom"], "told_foms": r["told_foms"]}), flush=True)
