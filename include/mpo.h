@@ -188,6 +188,57 @@ int mpo_gp_acq_grad_host(const MpoGpModel* model, const double* x_host, int batc
                          double y_opt, double xi, double kappa, double* f_host, double* g_host, void* stream);
 
 /* ------------------------------------------------------------------------
+ * L-BFGS-B drivers (host C++, no Python in the loop).  skopt's refit runs
+ * scipy.optimize.minimize(method="L-BFGS-B") from sklearn's
+ * _constrained_optimization (_gpr.py:296-337) and its polish runs
+ * fmin_l_bfgs_b(maxiter=20); both are reached from Coordinator.fit / ask
+ * (coordinator.py:63-79, 46-50).  These run L-BFGS-B 3.0 with scipy's driver
+ * rules over `nruns` independent starts whose objective evaluations are batched:
+ * every round evaluates the point each live run needs in one call.  Outputs:
+ * x_out [nruns][nvar], f_out [nruns] (scipy's OptimizeResult.fun), stats
+ * [nruns][4] = (nit, nfev, status, 0) with status 1 = projected gradient <= gtol,
+ * 2 = relative reduction <= ftol, 3 = maxiter, 4 = maxfun, 5 = abnormal line
+ * search; *rounds = objective rounds.  bounds [nvar][2] = (lower, upper).
+ * ---------------------------------------------------------------------- */
+typedef struct MpoLbfgsbOptions {
+    double ftol;        /* scipy ftol (factr * eps): minimize's default 2.22e-9, fmin_l_bfgs_b's 1e7 * eps */
+    double gtol;        /* scipy gtol / pgtol (1e-5) */
+    int32_t maxiter;    /* 15000 (minimize), 20 (skopt's polish) */
+    int32_t maxfun;     /* 15000 */
+    int32_t maxcor;     /* 10 */
+    int32_t maxls;      /* 20 */
+} MpoLbfgsbOptions;
+
+/* Objective of mpo_lbfgsb_batched: f [batch], g [batch][nvar] at the points X
+ * [batch][nvar] of runs ids [batch]; nonzero return aborts the minimisation. */
+typedef int (*mpo_fg_batch_fn)(int batch, const double* X, const int32_t* ids, double* f, double* g, void* user);
+
+/* The driver over a caller objective (host; the CPU tests compare it with scipy). */
+int mpo_lbfgsb_batched(int nvar, int nruns, const double* x0, const double* bounds, const MpoLbfgsbOptions* opts,
+                       mpo_fg_batch_fn fg, void* user, double* x_out, double* f_out, int32_t* stats,
+                       int32_t* rounds);
+
+/* skopt's whole refit on the device objective: L-BFGS-B from starts [nruns][d+2]
+ * (log theta) on -mpo_gp_lml_grad, one mpo_gp_lml_grad_host round per iteration
+ * of all live runs (theta_host [nruns][d+2] and out_host as that call's pinned
+ * buffers).  Replaces sklearn's restart loop (_gpr.py:296-337) around
+ * scipy.optimize.minimize.  Synchronises `stream` every round. */
+int mpo_gp_fit_lml_host(const double* X, const double* y_norm, int n, int d, const double* starts, int nruns,
+                        const double* bounds, const MpoLbfgsbOptions* opts, double* theta_host, double* out_host,
+                        void* dev_io, size_t io_bytes, void* ws, size_t ws_bytes, double* x_out, double* f_out,
+                        int32_t* stats, int32_t* rounds, void* stream);
+
+/* skopt's polish of the best candidates: L-BFGS-B from starts [nruns][d] on the
+ * minimised acquisition acq[r] of run r (mpo_gp_acq_grad_host rounds through the
+ * pinned x_host [nruns][d], acq_host [nruns], f_host [nruns], g_host [nruns][d]).
+ * Replaces skopt's fmin_l_bfgs_b(gaussian_acquisition_1D, x0, bounds, maxiter=20)
+ * loop over the n_restarts_optimizer best candidates. */
+int mpo_gp_polish_host(const MpoGpModel* model, const double* starts, const int32_t* acq, int nruns,
+                       const double* bounds, const MpoLbfgsbOptions* opts, double y_opt, double xi, double kappa,
+                       double* x_host, int32_t* acq_host, double* f_host, double* g_host, double* x_out,
+                       double* f_out, int32_t* stats, int32_t* rounds, void* stream);
+
+/* ------------------------------------------------------------------------
  * Population training of ragged MNIST-CNN trials.
  * Replaces ProcessBlock.train_model -> mpi_learn MPIKFoldManager.train()
  * (process_block.py:71-96) for test_mnist (mpiLAPI.py:138-176): every member

@@ -38,6 +38,17 @@ class MpoGpModel(ctypes.Structure):
     ]
 
 
+class MpoLbfgsbOptions(ctypes.Structure):
+    _fields_ = [("ftol", ctypes.c_double), ("gtol", ctypes.c_double), ("maxiter", ctypes.c_int32),
+                ("maxfun", ctypes.c_int32), ("maxcor", ctypes.c_int32), ("maxls", ctypes.c_int32)]
+
+
+#: objective callback of mpo_lbfgsb_batched (tests drive the host L-BFGS-B with it)
+FG_BATCH_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                               ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double),
+                               ctypes.POINTER(ctypes.c_double), ctypes.c_void_p)
+
+
 class MpoCnnSpec(ctypes.Structure):
     _fields_ = [("nb_filters", ctypes.c_int32), ("kernel_size", ctypes.c_int32), ("pool_size", ctypes.c_int32),
                 ("dense", ctypes.c_int32), ("lr", ctypes.c_float), ("dropout", ctypes.c_float),
@@ -87,6 +98,12 @@ SIGNATURES = {
     "mpo_gp_ei_score": (_I, [ctypes.POINTER(MpoGpModel), _P, _I64, _D, _D, _P, _P, _P, _P, _P, _SZ, _P]),
     "mpo_gp_acq_grad": (_I, [ctypes.POINTER(MpoGpModel), _P, _I, _P, _D, _D, _D, _P, _P, _P]),
     "mpo_gp_acq_grad_host": (_I, [ctypes.POINTER(MpoGpModel), _P, _I, _P, _D, _D, _D, _P, _P, _P]),
+    "mpo_lbfgsb_batched": (_I, [_I, _I, _P, _P, ctypes.POINTER(MpoLbfgsbOptions), FG_BATCH_FN, _P, _P, _P, _P,
+                                _P]),
+    "mpo_gp_fit_lml_host": (_I, [_P, _P, _I, _I, _P, _I, _P, ctypes.POINTER(MpoLbfgsbOptions), _P, _P, _P, _SZ, _P,
+                                 _SZ, _P, _P, _P, _P, _P]),
+    "mpo_gp_polish_host": (_I, [ctypes.POINTER(MpoGpModel), _P, _P, _I, _P, ctypes.POINTER(MpoLbfgsbOptions), _D,
+                                _D, _D, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "mpo_pop_create": (_I, [ctypes.POINTER(MpoCnnSpec), _I, _I, ctypes.POINTER(ctypes.c_void_p)]),
     "mpo_pop_destroy": (_I, [_P]),
     "mpo_pop_sizes": (_I, [_P, ctypes.POINTER(MpoPopSizes)]),

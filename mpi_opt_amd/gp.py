@@ -161,17 +161,11 @@ class DeviceGP:
                   "mpo_gp_ei_score")
         return mu, sd, ei, am
 
-    def acq_grad(self, X, acq_codes, y_opt, xi=0.01, kappa=1.96):
-        """``mpo_gp_acq_grad_host``: minimised acquisition value and gradient at
-        the rows of X (B, d) (transformed space), acquisition ``acq_codes[b]``
-        (MPO_ACQ_* flag values).  The kernel reads X and the codes from pinned
-        host memory and writes f, g into it (no staging copies: a polish round is
-        ~30 us of device time, torch's copies and stream context cost as much);
-        returns numpy (f (B,), g (B, d))."""
-        X = np.asarray(X, dtype=np.float64).reshape(-1, self.d)
-        B, d = X.shape
+    def _ensure_ag(self, B):
+        """Pinned host buffers of one polish round (x, acquisition codes, f, g) for B points."""
         if getattr(self, "_ag_cap", 0) < B:
             cap = max(16, B)
+            d = self.d
             self._ag_x = torch.empty(cap * d, dtype=torch.float64).pin_memory()
             self._ag_a = torch.empty(cap, dtype=torch.int32).pin_memory()
             self._ag_f = torch.empty(cap, dtype=torch.float64).pin_memory()
@@ -181,6 +175,17 @@ class DeviceGP:
                              self._ag_g.data_ptr())
             self._ag_stream = _lib.stream_handle(self.device)
             self._ag_cap = cap
+
+    def acq_grad(self, X, acq_codes, y_opt, xi=0.01, kappa=1.96):
+        """``mpo_gp_acq_grad_host``: minimised acquisition value and gradient at
+        the rows of X (B, d) (transformed space), acquisition ``acq_codes[b]``
+        (MPO_ACQ_* flag values).  The kernel reads X and the codes from pinned
+        host memory and writes f, g into it (no staging copies: a polish round is
+        ~30 us of device time, torch's copies and stream context cost as much);
+        returns numpy (f (B,), g (B, d))."""
+        X = np.asarray(X, dtype=np.float64).reshape(-1, self.d)
+        B, d = X.shape
+        self._ensure_ag(B)
         xn, an, fn, gn = self._ag_np
         xn[:B * d] = X.reshape(-1)
         an[:B] = acq_codes
@@ -190,6 +195,32 @@ class DeviceGP:
         if rc != 0:
             check(rc, "mpo_gp_acq_grad_host")
         return fn[:B].copy(), gn[:B * d].reshape(B, d).copy()
+
+    def polish(self, starts, acq_codes, y_opt, xi, kappa, bounds, ftol, maxiter=20, gtol=1e-5, maxfun=15000):
+        """skopt's polish of its best candidates, whole, in ``mpo_gp_polish_host``:
+        L-BFGS-B (libmpo.so's host driver) from each row of ``starts`` (B, d) on
+        acquisition ``acq_codes[r]``, one ``mpo_gp_acq_grad_host`` round per
+        iteration of all live runs.  Returns [(x, f)] per run."""
+        starts = np.ascontiguousarray(np.asarray(starts, dtype=np.float64))
+        B, d = starts.shape
+        if d != self.d:
+            raise ValueError(f"polish starts must be (B, {self.d}), got {starts.shape}")
+        self._ensure_ag(B)
+        codes = np.ascontiguousarray(np.asarray(acq_codes, dtype=np.int32))
+        b = np.ascontiguousarray(np.asarray(bounds, dtype=np.float64).reshape(d, 2))
+        opts = _lib.MpoLbfgsbOptions(ftol, gtol, maxiter, maxfun, 10, 20)
+        x = np.empty((B, d))
+        f = np.empty(B)
+        stats = np.empty((B, 4), np.int32)
+        rounds = ctypes.c_int32(0)
+        xp, ap, fp, gp = self._ag_ptrs
+        rc = lib().mpo_gp_polish_host(ctypes.byref(self.model), starts.ctypes.data, codes.ctypes.data, B,
+                                      b.ctypes.data, ctypes.byref(opts), float(y_opt), float(xi), float(kappa),
+                                      xp, ap, fp, gp, x.ctypes.data, f.ctypes.data, stats.ctypes.data,
+                                      ctypes.byref(rounds), self._ag_stream)
+        if rc != 0:
+            check(rc, "mpo_gp_polish_host")
+        return [(x[r], float(f[r])) for r in range(B)]
 
     def predict(self, Xc, return_std=True):
         """skopt ``predict(X, return_std=True)`` -> numpy (mu, sd)."""

@@ -19,6 +19,7 @@ an optimisation path.
 """
 from __future__ import annotations
 
+import ctypes
 import threading
 
 import numpy as np
@@ -101,6 +102,31 @@ class DeviceLML:
             _lib.check(rc, "mpo_gp_lml_grad_host")
         h = self._out_np
         return -h[:B], -(h[B:B + B * (self.d + 2)].reshape(B, self.d + 2))
+
+    def fit(self, starts, bounds, ftol=None, gtol=1e-5, maxiter=15000, maxfun=15000):
+        """L-BFGS-B from every start on -LML, all in ``mpo_gp_fit_lml_host`` (the
+        host L-BFGS-B of csrc/lbfgsb.cpp; one device round per iteration of all
+        live runs; ctypes releases the GIL for the whole fit).  Returns
+        ([(theta, -lml)] per start, rounds)."""
+        starts = np.ascontiguousarray(np.asarray(starts, dtype=np.float64))
+        B, k = starts.shape
+        if k != self.d + 2:
+            raise ValueError(f"theta has {k} entries, expected d+2={self.d + 2}")
+        self._ensure(B)
+        b = np.ascontiguousarray(np.asarray(bounds, dtype=np.float64).reshape(k, 2))
+        opts = _lib.MpoLbfgsbOptions(MINIMIZE_FTOL if ftol is None else ftol, gtol, maxiter, maxfun, 10, 20)
+        x = np.empty((B, k))
+        f = np.empty(B)
+        stats = np.empty((B, 4), np.int32)
+        rounds = ctypes.c_int32(0)
+        rc = _lib.lib().mpo_gp_fit_lml_host(
+            _lib.ptr(self.X), _lib.ptr(self.y), self.n, self.d, starts.ctypes.data, B, b.ctypes.data,
+            ctypes.byref(opts), self.theta_h.data_ptr(), self.out_h.data_ptr(), _lib.ptr(self.io), self.io_bytes,
+            _lib.ptr(self.ws), self.ws_bytes, x.ctypes.data, f.ctypes.data, stats.ctypes.data, ctypes.byref(rounds),
+            self._stream)
+        _lib.check(rc, "mpo_gp_fit_lml_host")
+        self.last_stats = stats
+        return [(x[r], float(f[r])) for r in range(B)], rounds.value
 
     def evaluate(self, thetas):
         """thetas [B, d+2] (log space) -> (lml [B], grad [B, d+2], info [B]) as numpy:
@@ -325,32 +351,43 @@ class _Lockstep:
         self.cv.notify_all()
 
 
-def fit_lml(X, y, random_state=None, n_restarts_optimizer=2, device=None, return_details=False):
+def fit_lml(X, y, random_state=None, n_restarts_optimizer=2, device=None, return_details=False, driver="native"):
     """skopt's GP refit with the objective on the device.
 
     Returns (amp, length_scale, noise) -- the fitted ConstantKernel, Matern and
     WhiteKernel parameters, exactly what sklearn's ``kernel_`` would hold -- and,
     with ``return_details``, a dict with the per-start optima and launch count.
+    ``driver``: "native" runs L-BFGS-B in libmpo.so (``DeviceLML.fit``, no GIL
+    held during the fit); "scipy" drives scipy's own setulb from Python
+    (``lbfgsb_batched``: scipy's iterates bit for bit, given the objective).
     """
     X = np.asarray(X, dtype=np.float64)
     yn, _, _ = normalize_targets(y)
     lml = DeviceLML(X, yn, device=device)
-    return lockstep_lbfgsb(lml.evaluate, X.shape[1], random_state, n_restarts_optimizer, return_details)
+    return lockstep_lbfgsb(lml.evaluate, X.shape[1], random_state, n_restarts_optimizer, return_details, driver)
 
 
-def lockstep_lbfgsb(evaluate, d, random_state=None, n_restarts_optimizer=2, return_details=False):
+def lockstep_lbfgsb(evaluate, d, random_state=None, n_restarts_optimizer=2, return_details=False, driver="native"):
     """sklearn's restart loop (_gpr.py:296-337) over a batched objective
     ``evaluate(thetas[B, d+2]) -> (lml[B], grad[B, d+2], info[B])``: the start
     theta and ``n_restarts_optimizer`` uniform draws, L-BFGS-B each (one thread
-    per start, evaluations batched in lockstep), best = lowest -lml (first on ties)."""
+    per start, evaluations batched in lockstep), best = lowest -lml (first on ties).
+    A ``DeviceLML.evaluate`` objective with ``driver="native"`` runs the whole
+    fit in ``mpo_gp_fit_lml_host``."""
     bounds = theta_bounds(d)
     rng = check_random_state(random_state)   # GaussianProcessRegressor._rng
     starts = [np.log(np.ones(d + 2))]        # kernel start: amp 1, ls 1, noise 1
     for _ in range(n_restarts_optimizer):
         starts.append(rng.uniform(bounds[:, 0], bounds[:, 1]))
 
+    fast = getattr(evaluate, "__self__", None)
+    if driver == "native" and isinstance(fast, DeviceLML):
+        optima, launches = fast.fit(np.array(starts), bounds)
+        return _pick(optima, starts, launches, d, return_details)
+    if driver not in ("native", "scipy"):
+        raise ValueError(f"driver {driver!r}: 'native' or 'scipy'")
+
     if _setulb() is not None:                # one thread, setulb in reverse communication
-        fast = getattr(evaluate, "__self__", None)
         if isinstance(fast, DeviceLML):
             neg = fast.negated_round             # the device round, negated, without the checks
         else:

@@ -77,15 +77,21 @@ class GPModel:
         return mu
 
 
-def polish_lockstep(model, starts, acqs, y_opt, xi, kappa, bounds, maxiter=20):
+def polish_lockstep(model, starts, acqs, y_opt, xi, kappa, bounds, maxiter=20, driver="native"):
     """skopt's acquisition polish: ``fmin_l_bfgs_b(gaussian_acquisition_1D, x0,
     bounds, approx_grad=False, maxiter=20)`` from every start ``starts[w]`` of
-    acquisition ``acqs[w]``.  The runs are independent; they step in lockstep (one
-    thread each, gp_fit._Lockstep) so that each round of evaluations is one
-    ``mpo_gp_acq_grad`` launch over all live runs.  Returns [(x, f)] per run."""
+    acquisition ``acqs[w]``.  The runs are independent; they step in lockstep so
+    that each round of evaluations is one ``mpo_gp_acq_grad`` launch over all live
+    runs.  ``driver="native"``: the whole polish in ``mpo_gp_polish_host`` (the host
+    L-BFGS-B of libmpo.so, no GIL held); "scipy": scipy's setulb driven from
+    Python.  Returns [(x, f)] per run."""
     from .gp_fit import FMIN_FTOL, _Lockstep, _setulb, lbfgsb_batched
 
     codes = np.array([_lib.ACQ_FLAGS[a] for a in acqs], dtype=np.int32)
+    if driver == "native":
+        return model.dev.polish(np.array(starts), codes, y_opt, xi, kappa, bounds, ftol=FMIN_FTOL, maxiter=maxiter)
+    if driver != "scipy":
+        raise ValueError(f"driver {driver!r}: 'native' or 'scipy'")
 
     def evaluate(X, ids):
         return model.dev.acq_grad(X, codes[ids], y_opt, xi, kappa)

@@ -1,8 +1,9 @@
 """Throughput of concurrent cl_min chains on one GPU (the configs[3] search's
 optimizer term): an optimizer told n points of a synthetic objective in the mnist
 space, then ``jobs`` ask(k) batches (ChainJob) run on T worker threads; reports
-refits per second for each T (MPO_FIT_GRAPH=0 / 1 selects direct launches / graph
-replay of the LML rounds).  Also the single-thread refit latency split."""
+refits per second for each T.  ``--driver scipy`` runs the refits and polishes
+with scipy's setulb driven from Python instead of libmpo.so's host L-BFGS-B.
+Also the single-thread refit latency."""
 import argparse
 import os
 import sys
@@ -32,7 +33,12 @@ def main():
     ap.add_argument("--k", type=int, default=8, help="points per ask batch")
     ap.add_argument("--jobs", type=int, default=32)
     ap.add_argument("--threads", type=int, nargs="+", default=[1, 4, 8])
+    ap.add_argument("--driver", choices=["native", "scipy"], default="native")
     a = ap.parse_args()
+    if a.driver == "scipy":
+        fit0, pol0 = GF.fit_lml, O.polish_lockstep
+        O.fit_lml = lambda *args, **kw: fit0(*args, driver="scipy", **kw)
+        O.polish_lockstep = lambda *args, **kw: pol0(*args, driver="scipy", **kw)
     if os.environ.get("PY_SWITCH"):
         sys.setswitchinterval(float(os.environ["PY_SWITCH"]))
     print("switch interval", sys.getswitchinterval())
@@ -48,9 +54,9 @@ def main():
     Xt = space.transform(pts)
     t0 = time.perf_counter()
     for s in range(5):
-        _, det = GF.fit_lml(Xt, np.asarray(ys), random_state=s, device=dev, return_details=True)
+        _, det = GF.fit_lml(Xt, np.asarray(ys), random_state=s, device=dev, return_details=True, driver=a.driver)
     torch.cuda.synchronize()
-    print(f"graph={os.environ.get('MPO_FIT_GRAPH', '1')} n={a.n}: one refit {(time.perf_counter() - t0) / 5 * 1e3:.2f} ms "
+    print(f"driver={a.driver} n={a.n}: one refit {(time.perf_counter() - t0) / 5 * 1e3:.2f} ms "
           f"({det['launches']} rounds)", flush=True)
     for T in a.threads:
         ex = ThreadChainExecutor(dev, workers=T)

@@ -109,19 +109,22 @@ def test_non_finite_theta_reports_cholesky_failure():
     assert np.isfinite(lml[0])
 
 
+@pytest.mark.parametrize("driver", ["native", "scipy"])
 @pytest.mark.parametrize("name", CASES)
-def test_device_fit_matches_sklearn_fit(name):
+def test_device_fit_matches_sklearn_fit(name, driver):
+    """Both L-BFGS-B drivers on the device objective: libmpo.so's host L-BFGS-B
+    (mpo_gp_fit_lml_host) and scipy's setulb driven from Python."""
     from mpi_opt_amd.gp_fit import fit_lml
 
     X, y = G[name + "_X"], G[name + "_y"]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     (amp, ls, noise), det = fit_lml(X, y, random_state=int(G[name + "_seed"]), device="cuda:0",
-                                    return_details=True)
+                                    return_details=True, driver=driver)
     dt = time.perf_counter() - t0
     theta = np.log(np.r_[amp, ls, noise])
     ref = G[name + "_fit_theta"]
-    print(f"{name}: device fit {dt * 1e3:.1f} ms, {det['launches']} launches, lml {det['lml']:.9f}")
+    print(f"{name} ({driver}): device fit {dt * 1e3:.1f} ms, {det['launches']} launches, lml {det['lml']:.9f}")
     # the LML at the optimum agrees tightly; theta within the optimiser's resolution
     assert abs(det["lml"] - float(G[name + "_fit_lml"])) <= 1e-7 * abs(float(G[name + "_fit_lml"]))
     assert np.max(np.abs(theta - ref)) <= 1e-3, (theta, ref)

@@ -135,9 +135,11 @@ def test_acq_grad_mixed_batch_and_finite_differences():
         np.testing.assert_allclose(grad[b], fd, rtol=1e-4, atol=1e-7, err_msg=acqs[b])
 
 
-def test_polish_lockstep_matches_sequential_lbfgs():
+@pytest.mark.parametrize("driver", ["native", "scipy"])
+def test_polish_lockstep_matches_sequential_lbfgs(driver):
     """The 3 x 5 lockstep polishes give what sequential fmin_l_bfgs_b runs on the
-    oracle objective give (same starts, bounds, maxiter=20)."""
+    oracle objective give (same starts, bounds, maxiter=20), with libmpo.so's host
+    L-BFGS-B (mpo_gp_polish_host) and with scipy's setulb driven from Python."""
     from scipy.optimize import fmin_l_bfgs_b
 
     from mpi_opt_amd.optimizer import GPModel, polish_lockstep
@@ -151,7 +153,7 @@ def test_polish_lockstep_matches_sequential_lbfgs():
     starts = [rng.uniform(size=5) for _ in acqs]
     bounds = [(0.0, 1.0)] * 5
     y_opt = float(np.min(y))
-    got = polish_lockstep(model, starts, acqs, y_opt, 0.01, 1.96, bounds)
+    got = polish_lockstep(model, starts, acqs, y_opt, 0.01, 1.96, bounds, driver=driver)
     for w, (a, x0) in enumerate(zip(acqs, starts)):
         xr, fr, _ = fmin_l_bfgs_b(lambda v, a=a: O.acquisition_and_grad(st, v, y_opt, a), x0, bounds=bounds,
                                   approx_grad=False, maxiter=20)
