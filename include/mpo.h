@@ -218,15 +218,25 @@ int mpo_lbfgsb_batched(int nvar, int nruns, const double* x0, const double* boun
                        mpo_fg_batch_fn fg, void* user, double* x_out, double* f_out, int32_t* stats,
                        int32_t* rounds);
 
+/* A rendezvous for the concurrent refits on one device (the cl_min chains):
+ * fits that share it evaluate their pending rounds together, one grouped launch
+ * set per round of all registered fits, each theta's result unchanged.  Thread
+ * safe; stats = grouped launch sets and the rounds they carried. */
+int mpo_gp_lml_batcher_create(int device, void** handle);
+int mpo_gp_lml_batcher_destroy(void* handle);
+int mpo_gp_lml_batcher_stats(const void* handle, int64_t* launches, int64_t* rounds);
+
 /* skopt's whole refit on the device objective: L-BFGS-B from starts [nruns][d+2]
  * (log theta) on -mpo_gp_lml_grad, one mpo_gp_lml_grad_host round per iteration
  * of all live runs (theta_host [nruns][d+2] and out_host as that call's pinned
- * buffers).  Replaces sklearn's restart loop (_gpr.py:296-337) around
- * scipy.optimize.minimize.  Synchronises `stream` every round. */
+ * buffers).  With a `batcher` (or NULL) of the stream's device, each round goes
+ * through it and may launch together with other fits' rounds.  Replaces sklearn's
+ * restart loop (_gpr.py:296-337) around scipy.optimize.minimize.  Synchronises
+ * every round. */
 int mpo_gp_fit_lml_host(const double* X, const double* y_norm, int n, int d, const double* starts, int nruns,
                         const double* bounds, const MpoLbfgsbOptions* opts, double* theta_host, double* out_host,
                         void* dev_io, size_t io_bytes, void* ws, size_t ws_bytes, double* x_out, double* f_out,
-                        int32_t* stats, int32_t* rounds, void* stream);
+                        int32_t* stats, int32_t* rounds, void* batcher, void* stream);
 
 /* skopt's polish of the best candidates: L-BFGS-B from starts [nruns][d] on the
  * minimised acquisition acq[r] of run r (mpo_gp_acq_grad_host rounds through the

@@ -100,8 +100,11 @@ SIGNATURES = {
     "mpo_gp_acq_grad_host": (_I, [ctypes.POINTER(MpoGpModel), _P, _I, _P, _D, _D, _D, _P, _P, _P]),
     "mpo_lbfgsb_batched": (_I, [_I, _I, _P, _P, ctypes.POINTER(MpoLbfgsbOptions), FG_BATCH_FN, _P, _P, _P, _P,
                                 _P]),
+    "mpo_gp_lml_batcher_create": (_I, [_I, ctypes.POINTER(ctypes.c_void_p)]),
+    "mpo_gp_lml_batcher_destroy": (_I, [_P]),
+    "mpo_gp_lml_batcher_stats": (_I, [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     "mpo_gp_fit_lml_host": (_I, [_P, _P, _I, _I, _P, _I, _P, ctypes.POINTER(MpoLbfgsbOptions), _P, _P, _P, _SZ, _P,
-                                 _SZ, _P, _P, _P, _P, _P]),
+                                 _SZ, _P, _P, _P, _P, _P, _P]),
     "mpo_gp_polish_host": (_I, [ctypes.POINTER(MpoGpModel), _P, _P, _I, _P, ctypes.POINTER(MpoLbfgsbOptions), _D,
                                 _D, _D, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "mpo_pop_create": (_I, [ctypes.POINTER(MpoCnnSpec), _I, _I, ctypes.POINTER(ctypes.c_void_p)]),
@@ -154,6 +157,22 @@ def ptr(t) -> int:
     if t is None:
         return None
     return t.data_ptr()
+
+
+_BATCHERS = {}
+_BATCHERS_LOCK = __import__("threading").Lock()
+
+
+def lml_batcher(device_index: int):
+    """The process-wide LML round batcher of one GPU (mpo_gp_lml_batcher_create),
+    shared by every refit on that device; lives as long as the process."""
+    with _BATCHERS_LOCK:
+        h = _BATCHERS.get(device_index)
+        if h is None:
+            out = ctypes.c_void_p()
+            check(lib().mpo_gp_lml_batcher_create(int(device_index), ctypes.byref(out)), "mpo_gp_lml_batcher_create")
+            h = _BATCHERS[device_index] = out.value
+        return h
 
 
 def stream_handle(device=None) -> int:

@@ -36,6 +36,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <string>
+#include <vector>
 
 namespace {
 
@@ -557,12 +558,38 @@ struct SsPtrs {
     __device__ double* C(int k) const { return (k & 1) ? C1 : C0; }
 };
 
-__device__ __forceinline__ SsPtrs ss_ptrs(const LmlArgs& a, int b) {
+// The split sweep's launches take a table of thetas (LmlGroup, by value in the
+// kernel arguments): each entry carries its own problem (X, y, n), workspace and
+// outputs, so one launch set can evaluate the pending L-BFGS-B rounds of several
+// concurrent refits (different training sets and n; the same d).  Every theta's
+// arithmetic depends only on its own entry -- its work split follows its own n,
+// and launch dimensions sized for the largest n only add workgroups that exit --
+// so a theta gives the same bits alone, in a batch or grouped with other problems.
+constexpr int kMaxGroup = 40;
+struct LmlTheta {
+    const double* X;          // [n][d]
+    const double* y;          // [n]
+    const double* theta;      // [d+2] device copy (written by the build from theta_src when set)
+    const double* theta_src;  // [d+2] pinned host (device view) or nullptr
+    double* lml;              // [1]
+    double* grad;             // [d+2]
+    int32_t* info;            // [1]
+    double* ws;               // ss_ws_doubles(n, d)
+    double* partials;         // [kPairGroups][DP + 2]
+    int n;
+    int pad_;
+};
+struct LmlGroup {
+    int d, count, stop, pad_;
+    LmlTheta th[kMaxGroup];
+};
+
+__device__ __forceinline__ SsPtrs ss_ptrs_t(const LmlTheta& t, int d) {
     auto al = [](long long x) { return (x + 31) & ~31LL; };
-    const long long np = sw_np(a.n);
+    const long long np = sw_np(t.n);
     SsPtrs p;
-    p.xs = a.ws + (long long)b * a.ws_stride;
-    p.alpha = p.xs + al((long long)a.n * a.d);
+    p.xs = t.ws;
+    p.alpha = p.xs + al((long long)t.n * d);
     p.A = p.alpha + al(np);
     p.C0 = p.A + np * np;
     p.C1 = p.C0 + np * kSwNb;
@@ -572,29 +599,30 @@ __device__ __forceinline__ SsPtrs ss_ptrs(const LmlArgs& a, int b) {
 }
 
 template <int DP>
-__device__ __forceinline__ void ss_theta(const LmlArgs& a, int b, double& amp, double& noise, double (&ls)[DP],
-                                         const double* src = nullptr) {
-    const double* th = (src ? src : a.theta) + (long long)b * (a.d + 2);
+__device__ __forceinline__ void ss_theta_t(const LmlTheta& t, int d, double& amp, double& noise, double (&ls)[DP],
+                                           bool src) {
+    const double* th = src && t.theta_src ? t.theta_src : t.theta;
     amp = exp(th[0]);
-    noise = exp(th[a.d + 1]);
+    noise = exp(th[d + 1]);
 #pragma unroll
-    for (int c = 0; c < DP; ++c) ls[c] = c < a.d ? exp(th[1 + c]) : 1.0;
+    for (int c = 0; c < DP; ++c) ls[c] = c < d ? exp(th[1 + c]) : 1.0;
 }
 
 // grid (1, B): xs = X / ls, the log det / failure accumulators
 template <int DP>
-__global__ __launch_bounds__(256) void sw_xs_kernel(LmlArgs a) {
+__global__ __launch_bounds__(256) void sw_xs_kernel(LmlGroup grp) {
     const int b = blockIdx.y;
-    const SsPtrs p = ss_ptrs(a, b);
+    const LmlTheta& T = grp.th[b];
+    const SsPtrs p = ss_ptrs_t(T, grp.d);
     double amp, noise, ls[DP];
-    ss_theta<DP>(a, b, amp, noise, ls);
-    for (int e = threadIdx.x; e < a.n * a.d; e += blockDim.x) {
-        const int c = e % a.d;
+    ss_theta_t<DP>(T, grp.d, amp, noise, ls, false);
+    for (int e = threadIdx.x; e < T.n * grp.d; e += blockDim.x) {
+        const int c = e % grp.d;
         double lc = 1.0;
 #pragma unroll
         for (int q = 0; q < DP; ++q)
             if (q == c) lc = ls[q];
-        p.xs[e] = a.X[e] / lc;
+        p.xs[e] = T.X[e] / lc;
     }
     if (threadIdx.x == 0) { p.acc[0] = 0.0; p.acc[1] = 0.0; }
 }
@@ -602,11 +630,14 @@ __global__ __launch_bounds__(256) void sw_xs_kernel(LmlArgs a) {
 // grid (np/16, B): K rows [16 bx, 16 bx + 16) -- the lower triangle and the full
 // diagonal 16x16 tiles, identity on the padding
 template <int DP>
-__global__ __launch_bounds__(256) void sw_build_kernel(LmlArgs a) {
-    const int b = blockIdx.y, n = a.n, d = a.d, np = (int)sw_np(n);
-    const SsPtrs p = ss_ptrs(a, b);
+__global__ __launch_bounds__(256) void sw_build_kernel(LmlGroup grp) {
+    const int b = blockIdx.y;
+    const LmlTheta& T = grp.th[b];
+    const int n = T.n, d = grp.d, np = (int)sw_np(n);
+    if ((int)blockIdx.x >= np / 16) return;   // a larger problem of the group sized the grid
+    const SsPtrs p = ss_ptrs_t(T, grp.d);
     double amp, noise, ls[DP];
-    ss_theta<DP>(a, b, amp, noise, ls);
+    ss_theta_t<DP>(T, grp.d, amp, noise, ls, false);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int i = 16 * blockIdx.x + wave; i < 16 * blockIdx.x + 16; i += 4) {
         double xi[DP];
@@ -648,14 +679,17 @@ __global__ __launch_bounds__(256) void sw_build_kernel(LmlArgs a) {
 // wave with sw_build_kernel's arithmetic (the same bits).  Workgroup 0 resets the
 // log det / failure accumulators and the pair kernel's arrival counter.
 template <int DP>
-__global__ __launch_bounds__(1024) void sw_xs_build_kernel(LmlArgs a) {
+__global__ __launch_bounds__(1024) void sw_xs_build_kernel(LmlGroup grp) {
     extern __shared__ __attribute__((aligned(16))) double xsl[];   // [rows][DP]
-    const int b = blockIdx.y, n = a.n, d = a.d, np = (int)sw_np(n);
-    const SsPtrs p = ss_ptrs(a, b);
+    const int b = blockIdx.y;
+    const LmlTheta& T = grp.th[b];
+    const int n = T.n, d = grp.d, np = (int)sw_np(n);
+    if ((int)blockIdx.x >= np / 16) return;   // a larger problem of the group sized the grid
+    const SsPtrs p = ss_ptrs_t(T, grp.d);
     double amp, noise, ls[DP];
-    ss_theta<DP>(a, b, amp, noise, ls, a.theta_src);   // host-staged call: theta straight from pinned memory
-    if (a.theta_src && blockIdx.x == 0 && threadIdx.x < d + 2)   // ... and the device copy the later kernels read
-        const_cast<double*>(a.theta)[(long long)b * (d + 2) + threadIdx.x] = a.theta_src[(long long)b * (d + 2) + threadIdx.x];
+    ss_theta_t<DP>(T, grp.d, amp, noise, ls, true);   // host-staged call: theta straight from pinned memory
+    if (T.theta_src && blockIdx.x == 0 && threadIdx.x < d + 2)   // ... and the device copy the later kernels read
+        const_cast<double*>(T.theta)[threadIdx.x] = T.theta_src[threadIdx.x];
     const int rows = min(n, 16 * (int)blockIdx.x + 16);
     for (int e = threadIdx.x; e < rows * d; e += blockDim.x) {
         const int i = e / d, c = e % d;
@@ -663,7 +697,7 @@ __global__ __launch_bounds__(1024) void sw_xs_build_kernel(LmlArgs a) {
 #pragma unroll
         for (int q = 0; q < DP; ++q)
             if (q == c) lc = ls[q];
-        const double v = a.X[e] / lc;
+        const double v = T.X[e] / lc;
         xsl[i * DP + c] = v;
         if (i >= 16 * (int)blockIdx.x) p.xs[e] = v;
     }
@@ -798,9 +832,12 @@ __device__ __forceinline__ void pivot_block_sweep2(const double* __restrict__ C,
 // diagonal tile (I, I) also writes G_I into block column k of A (and row I's entries
 // of C_{k+1}), tile (I, I) of block k writes -P^-1 there.  Workgroup 0 keeps the
 // log det and the failure column.
-__global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlArgs a, int k) {
-    const int b = blockIdx.y, np = (int)sw_np(a.n), ntile = np / 16, k0 = k * kSwNb;
-    const SsPtrs p = ss_ptrs(a, b);
+__global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlGroup grp, int k) {
+    const int b = blockIdx.y;
+    const LmlTheta& T = grp.th[b];
+    const int np = (int)sw_np(T.n), ntile = np / 16, k0 = k * kSwNb;
+    if (k0 >= np) return;                     // this problem has fewer pivot blocks
+    const SsPtrs p = ss_ptrs_t(T, grp.d);
     const double* Cc = p.C(k);
     __shared__ double gl[kUpdThreads / 64][16 * kSwNb];   // per wave: G_I, A-operand order
     __shared__ double Pl[kSwNb * kSwNb];                  // P^-1 of this step
@@ -842,7 +879,7 @@ __global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlArgs a, int k) 
         const int l = lane & 31, h = lane >> 5;
         double r[16], prod;
         int bad;
-        if (a.stop == 23) {   // diagnostics only (MPO_FIT_DEBUG=23): the sweep skipped, timing of the rest
+        if (grp.stop == 23) {   // diagnostics only (MPO_FIT_DEBUG=23): the sweep skipped, timing of the rest
             prod = 1.0;
             bad = 0;
 #pragma unroll
@@ -928,10 +965,13 @@ __global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlArgs a, int k) 
 // grid (np/16, B), 256 threads: alpha = K^-1 y for the 16 rows of row tile I;
 // wave w sums the column tiles J = w (mod 4), each tile read from the lower
 // storage (transposed above the diagonal); fixed-order reductions
-__global__ __launch_bounds__(256) void sw_alpha_kernel(LmlArgs a) {
+__global__ __launch_bounds__(256) void sw_alpha_kernel(LmlGroup grp) {
     __shared__ double part[4][16];
-    const int b = blockIdx.y, n = a.n, np = (int)sw_np(n), ntile = np / 16, I = blockIdx.x;
-    const SsPtrs p = ss_ptrs(a, b);
+    const int b = blockIdx.y;
+    const LmlTheta& T = grp.th[b];
+    const int n = T.n, np = (int)sw_np(n), ntile = np / 16, I = blockIdx.x;
+    if (I >= ntile) return;
+    const SsPtrs p = ss_ptrs_t(T, grp.d);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & 15, cq = lane >> 4;
     const int i = 16 * I + r;
@@ -941,7 +981,7 @@ __global__ __launch_bounds__(256) void sw_alpha_kernel(LmlArgs a) {
         for (int u = 0; u < 4; ++u) {
             const int j = 16 * J + cq + 4 * u;
             const double kij = j <= i ? -p.A[(long long)i * np + j] : -p.A[(long long)j * np + i];
-            sacc = fma(kij, j < n ? a.y[j] : 0.0, sacc);
+            sacc = fma(kij, j < n ? T.y[j] : 0.0, sacc);
         }
     }
     sacc += __shfl_xor(sacc, 16);
@@ -962,12 +1002,14 @@ constexpr int kPairGroups = 64;
 // grid (kPairGroups, B), 256 threads: pairs i >= j of rows i = gw (mod waves),
 // W_ij dK_ij/dtheta; one partial per workgroup
 template <int DP>
-__global__ __launch_bounds__(256) void sw_pairs_kernel(LmlArgs a, double* __restrict__ partials) {
+__global__ __launch_bounds__(256) void sw_pairs_kernel(LmlGroup grp) {
     __shared__ double red[4][DP + 2];
-    const int b = blockIdx.y, n = a.n, d = a.d, np = (int)sw_np(n);
-    const SsPtrs p = ss_ptrs(a, b);
+    const int b = blockIdx.y;
+    const LmlTheta& T = grp.th[b];
+    const int n = T.n, d = grp.d, np = (int)sw_np(n);
+    const SsPtrs p = ss_ptrs_t(T, grp.d);
     double amp, noise, ls[DP];
-    ss_theta<DP>(a, b, amp, noise, ls);
+    ss_theta_t<DP>(T, grp.d, amp, noise, ls, false);
     (void)ls;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int gw = blockIdx.x * 4 + wave, nw = gridDim.x * 4;
@@ -1013,33 +1055,35 @@ __global__ __launch_bounds__(256) void sw_pairs_kernel(LmlArgs a, double* __rest
     __syncthreads();
     if (threadIdx.x < DP + 2) {
         const int c = threadIdx.x;
-        partials[((long long)b * gridDim.x + blockIdx.x) * (DP + 2) + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+        T.partials[(long long)blockIdx.x * (DP + 2) + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
     }
 }
 
 // grid (1, B), 64 threads: y.alpha, the LML, the gradient from the pair partials
 // (fixed order), or sklearn's LinAlgError branch (-inf, zeros)
 template <int DP>
-__global__ __launch_bounds__(64) void sw_final_kernel(LmlArgs a, const double* __restrict__ partials, int groups) {
-    const int b = blockIdx.y, n = a.n, d = a.d, lane = threadIdx.x;
-    const SsPtrs p = ss_ptrs(a, b);
-    double* out = a.grad + (long long)b * (d + 2);
+__global__ __launch_bounds__(64) void sw_final_kernel(LmlGroup grp, int groups) {
+    const int b = blockIdx.y;
+    const LmlTheta& T = grp.th[b];
+    const int n = T.n, d = grp.d, lane = threadIdx.x;
+    const SsPtrs p = ss_ptrs_t(T, grp.d);
+    double* out = T.grad;
     if (p.acc[1] != 0.0) {
-        if (lane == 0) { a.lml[b] = -INFINITY; a.info[b] = (int)p.acc[1]; }
+        if (lane == 0) { T.lml[0] = -INFINITY; T.info[0] = (int)p.acc[1]; }
         for (int c = lane; c < d + 2; c += 64) out[c] = 0.0;
         return;
     }
     double ya = 0.0;
-    for (int i = lane; i < n; i += 64) ya = fma(a.y[i], p.alpha[i], ya);
+    for (int i = lane; i < n; i += 64) ya = fma(T.y[i], p.alpha[i], ya);
     ya = wave_sum_bcast(ya);
     if (lane == 0) {
-        a.lml[b] = -0.5 * ya - 0.5 * p.acc[0] - 0.5 * n * kLog2Pi;
-        a.info[b] = 0;
+        T.lml[0] = -0.5 * ya - 0.5 * p.acc[0] - 0.5 * n * kLog2Pi;
+        T.info[0] = 0;
     }
     if (lane < d + 2) {
         const int src = lane == 0 ? 0 : (lane == d + 1 ? DP + 1 : lane);
         double sum = 0.0;
-        for (int w = 0; w < groups; ++w) sum += partials[((long long)b * groups + w) * (DP + 2) + src];
+        for (int w = 0; w < groups; ++w) sum += T.partials[(long long)w * (DP + 2) + src];
         out[lane] = 0.5 * sum;
     }
 }
@@ -1050,14 +1094,16 @@ __global__ __launch_bounds__(64) void sw_final_kernel(LmlArgs a, const double* _
 // added in sw_final_kernel's fixed order -- and writes y.alpha, the LML and the
 // gradient (the same bits as the two-launch form).
 template <int DP>
-__global__ __launch_bounds__(256) void sw_pairs_final_kernel(LmlArgs a, double* __restrict__ partials) {
+__global__ __launch_bounds__(256) void sw_pairs_final_kernel(LmlGroup grp) {
     __shared__ double red[4][DP + 2];
     __shared__ double pl[kPairGroups * (DP + 2)];
     __shared__ int last;
-    const int b = blockIdx.y, n = a.n, d = a.d, np = (int)sw_np(n);
-    const SsPtrs p = ss_ptrs(a, b);
+    const int b = blockIdx.y;
+    const LmlTheta& T = grp.th[b];
+    const int n = T.n, d = grp.d, np = (int)sw_np(n);
+    const SsPtrs p = ss_ptrs_t(T, grp.d);
     double amp, noise, ls[DP];
-    ss_theta<DP>(a, b, amp, noise, ls);
+    ss_theta_t<DP>(T, grp.d, amp, noise, ls, false);
     (void)ls;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int gw = blockIdx.x * 4 + wave, nw = gridDim.x * 4;
@@ -1104,7 +1150,7 @@ __global__ __launch_bounds__(256) void sw_pairs_final_kernel(LmlArgs a, double* 
     __syncthreads();
     if (threadIdx.x < DP + 2) {
         const int c = threadIdx.x;
-        partials[((long long)b * gridDim.x + blockIdx.x) * (DP + 2) + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+        T.partials[(long long)blockIdx.x * (DP + 2) + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1118,22 +1164,22 @@ __global__ __launch_bounds__(256) void sw_pairs_final_kernel(LmlArgs a, double* 
     if (!last) return;
     __threadfence();
     const int groups = gridDim.x;
-    double* out = a.grad + (long long)b * (d + 2);
+    double* out = T.grad;
     if (failed) {
-        if (threadIdx.x == 0) { a.lml[b] = -INFINITY; a.info[b] = (int)p.acc[1]; }
+        if (threadIdx.x == 0) { T.lml[0] = -INFINITY; T.info[0] = (int)p.acc[1]; }
         for (int c = threadIdx.x; c < d + 2; c += 256) out[c] = 0.0;
         return;
     }
     for (int e = threadIdx.x; e < groups * (DP + 2); e += 256)
-        pl[e] = partials[(long long)b * groups * (DP + 2) + e];
+        pl[e] = T.partials[e];
     __syncthreads();
     if (wave != 0) return;
     double ya = 0.0;
-    for (int i = lane; i < n; i += 64) ya = fma(a.y[i], p.alpha[i], ya);
+    for (int i = lane; i < n; i += 64) ya = fma(T.y[i], p.alpha[i], ya);
     ya = wave_sum_bcast(ya);
     if (lane == 0) {
-        a.lml[b] = -0.5 * ya - 0.5 * p.acc[0] - 0.5 * n * kLog2Pi;
-        a.info[b] = 0;
+        T.lml[0] = -0.5 * ya - 0.5 * p.acc[0] - 0.5 * n * kLog2Pi;
+        T.info[0] = 0;
     }
     if (lane < d + 2) {
         const int src = lane == 0 ? 0 : (lane == d + 1 ? DP + 1 : lane);
@@ -1143,45 +1189,98 @@ __global__ __launch_bounds__(256) void sw_pairs_final_kernel(LmlArgs a, double* 
     }
 }
 
+// One evaluation of the thetas th[0 .. count) (any problems of dimension d, DP =
+// fit_dp(d)): the split sweep's launches, in chunks of kMaxGroup thetas, the grids
+// sized for the chunk's largest n (the smaller problems' extra workgroups exit).
+// The fused build / finish while the largest problem's xs rows fit 64 KiB of LDS;
+// past it separate xs / build / pairs / final launches (the same arithmetic; those
+// read theta from the device copy, so a group there carries no theta_src).
+inline int fit_dp(int d);
+
 template <int DP>
-int launch_split(const LmlArgs& a, int B, hipStream_t s) {
-    const int np = (int)sw_np(a.n), nbk = np / kSwNb, ntile = np / 16;
-    const int nt_low = ntile * (ntile + 1) / 2;
-    const int nwg = std::max(1, (nt_low + 4 * kUpdTilesPerWave - 1) / (4 * kUpdTilesPerWave));
-    // the fused build (sw_xs_build_kernel) and finish (sw_pairs_final_kernel) while
-    // the workgroup's xs rows fit 64 KiB of LDS; past it separate xs / build / pairs
-    // / final launches
-    const size_t xs_lds = (size_t)np * DP * sizeof(double);
-    const bool fuse_build = xs_lds <= 64 * 1024;
-    double* partials = a.ws + (long long)B * a.ws_stride;   // [B][kPairGroups][DP + 2]
-    if (fuse_build) {
-        auto kb = sw_xs_build_kernel<DP>;
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kb), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)xs_lds);
-        hipLaunchKernelGGL(kb, dim3(ntile, B), dim3(1024), xs_lds, s, a);
+int launch_split_group(const LmlTheta* th, int count, int d, int stop, hipStream_t s) {
+    for (int c0 = 0; c0 < count; c0 += kMaxGroup) {
+        LmlGroup g{};
+        g.d = d;
+        g.stop = stop;
+        g.count = std::min(kMaxGroup, count - c0);
+        int nmax = 0;
+        for (int i = 0; i < g.count; ++i) {
+            g.th[i] = th[c0 + i];
+            nmax = std::max(nmax, g.th[i].n);
+        }
+        const int np = (int)sw_np(nmax), nbk = np / kSwNb, ntile = np / 16, B = g.count;
+        const int nt_low = ntile * (ntile + 1) / 2;
+        const int nwg = std::max(1, (nt_low + 4 * kUpdTilesPerWave - 1) / (4 * kUpdTilesPerWave));
+        const size_t xs_lds = (size_t)np * DP * sizeof(double);
+        const bool fuse_build = xs_lds <= 64 * 1024;
+        if (fuse_build) {
+            auto kb = sw_xs_build_kernel<DP>;
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kb), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)xs_lds);
+            hipLaunchKernelGGL(kb, dim3(ntile, B), dim3(1024), xs_lds, s, g);
+            MPO_LAUNCH_CHECK();
+        } else {
+            for (int i = 0; i < B; ++i)
+                if (g.th[i].theta_src) {
+                    mpo::set_error("mpo_gp_lml_grad: a host theta source needs the fused split sweep");
+                    return MPO_EINVAL;
+                }
+            hipLaunchKernelGGL(sw_xs_kernel<DP>, dim3(1, B), dim3(256), 0, s, g);
+            MPO_LAUNCH_CHECK();
+            hipLaunchKernelGGL(sw_build_kernel<DP>, dim3(ntile, B), dim3(256), 0, s, g);
+            MPO_LAUNCH_CHECK();
+        }
+        for (int k = 0; k < nbk; ++k) {
+            hipLaunchKernelGGL(sw_step_kernel, dim3(nwg, B), dim3(kUpdThreads), 0, s, g, k);
+            MPO_LAUNCH_CHECK();
+        }
+        hipLaunchKernelGGL(sw_alpha_kernel, dim3(ntile, B), dim3(256), 0, s, g);
         MPO_LAUNCH_CHECK();
-    } else {
-        hipLaunchKernelGGL(sw_xs_kernel<DP>, dim3(1, B), dim3(256), 0, s, a);
-        MPO_LAUNCH_CHECK();
-        hipLaunchKernelGGL(sw_build_kernel<DP>, dim3(ntile, B), dim3(256), 0, s, a);
-        MPO_LAUNCH_CHECK();
-    }
-    for (int k = 0; k < nbk; ++k) {
-        hipLaunchKernelGGL(sw_step_kernel, dim3(nwg, B), dim3(kUpdThreads), 0, s, a, k);
-        MPO_LAUNCH_CHECK();
-    }
-    hipLaunchKernelGGL(sw_alpha_kernel, dim3(ntile, B), dim3(256), 0, s, a);
-    MPO_LAUNCH_CHECK();
-    if (fuse_build) {   // the arrival counter is reset by sw_xs_build_kernel
-        hipLaunchKernelGGL(sw_pairs_final_kernel<DP>, dim3(kPairGroups, B), dim3(256), 0, s, a, partials);
-        MPO_LAUNCH_CHECK();
-    } else {
-        hipLaunchKernelGGL(sw_pairs_kernel<DP>, dim3(kPairGroups, B), dim3(256), 0, s, a, partials);
-        MPO_LAUNCH_CHECK();
-        hipLaunchKernelGGL(sw_final_kernel<DP>, dim3(1, B), dim3(64), 0, s, a, partials, kPairGroups);
-        MPO_LAUNCH_CHECK();
+        if (fuse_build) {   // the arrival counter is reset by sw_xs_build_kernel
+            hipLaunchKernelGGL(sw_pairs_final_kernel<DP>, dim3(kPairGroups, B), dim3(256), 0, s, g);
+            MPO_LAUNCH_CHECK();
+        } else {
+            hipLaunchKernelGGL(sw_pairs_kernel<DP>, dim3(kPairGroups, B), dim3(256), 0, s, g);
+            MPO_LAUNCH_CHECK();
+            hipLaunchKernelGGL(sw_final_kernel<DP>, dim3(1, B), dim3(64), 0, s, g, kPairGroups);
+            MPO_LAUNCH_CHECK();
+        }
     }
     return MPO_OK;
+}
+
+// the thetas of one problem (X, y, n): theta / lml / grad / info as mpo_gp_lml_grad
+// lays them out, workspace per theta then the pair partials per theta
+inline void problem_thetas(std::vector<LmlTheta>& out, const double* X, const double* y, int n, int d, int dp,
+                           const double* theta, const double* theta_src, int batch, double* lml, double* grad,
+                           int32_t* info, double* ws) {
+    const long long stride = ss_ws_doubles(n, d);
+    double* partials = ws + (long long)batch * stride;
+    for (int b = 0; b < batch; ++b) {
+        LmlTheta t{};
+        t.X = X;
+        t.y = y;
+        t.theta = theta + (long long)b * (d + 2);
+        t.theta_src = theta_src ? theta_src + (long long)b * (d + 2) : nullptr;
+        t.lml = lml + b;
+        t.grad = grad + (long long)b * (d + 2);
+        t.info = info + b;
+        t.ws = ws + (long long)b * stride;
+        t.partials = partials + (long long)b * kPairGroups * (dp + 2);
+        t.n = n;
+        out.push_back(t);
+    }
+}
+
+int launch_split_any(const std::vector<LmlTheta>& th, int d, int stop, hipStream_t s) {
+    switch (fit_dp(d)) {
+        case 4: return launch_split_group<4>(th.data(), (int)th.size(), d, stop, s);
+        case 8: return launch_split_group<8>(th.data(), (int)th.size(), d, stop, s);
+        case 12: return launch_split_group<12>(th.data(), (int)th.size(), d, stop, s);
+        case 16: return launch_split_group<16>(th.data(), (int)th.size(), d, stop, s);
+        default: return launch_split_group<32>(th.data(), (int)th.size(), d, stop, s);
+    }
 }
 
 inline int fit_dp(int d) {
@@ -1223,6 +1322,29 @@ int launch_lml(const LmlArgs& a, int B, hipStream_t s) {
 
 }  // namespace
 
+namespace mpo {
+
+bool lml_groupable(int n, int d) {
+    const int dp = fit_dp(d);
+    return dp > 0 && n > 0 && n <= kFitMaxN && fit_fused_split(n, dp);
+}
+
+int lml_launch_rounds(const LmlRound* r, int count, hipStream_t s) {
+    if (count <= 0) return MPO_OK;
+    const int d = r[0].d, dp = fit_dp(d), k = d + 2;
+    std::vector<LmlTheta> th;
+    for (int i = 0; i < count; ++i) {
+        MPO_CHECK_ARG(r[i].d == d && lml_groupable(r[i].n, d), "lml_launch_rounds: round %d not groupable", i);
+        double* od = r[i].out;
+        const int B = r[i].batch;
+        problem_thetas(th, r[i].X, r[i].y, r[i].n, d, dp, r[i].theta_dev, r[i].theta_src, B, od, od + B,
+                       reinterpret_cast<int32_t*>(od + B + (long long)B * k), r[i].ws);
+    }
+    return launch_split_any(th, d, 0, s);
+}
+
+}  // namespace mpo
+
 extern "C" {
 
 size_t mpo_gp_lml_ws_bytes(int n, int d, int batch) {
@@ -1255,22 +1377,18 @@ static int lml_grad_impl(const double* X, const double* y_norm, int n, int d, co
                   ws_bytes, mpo_gp_lml_ws_bytes(n, d, batch));
     const bool use_lds = n <= kFitLdsMaxN;
     const bool split = use_split(n);
-    LmlArgs a{X, y_norm, n, d, theta, lml, grad, info,
-              reinterpret_cast<double*>(mpo::align_up(reinterpret_cast<uintptr_t>(ws), 256)),
-              split ? ss_ws_doubles(n, d) : fit_ws_doubles(n, d, use_lds), 0};
-    if (const char* e = getenv("MPO_FIT_DEBUG")) a.stop = atoi(e);
+    double* wsa = reinterpret_cast<double*>(mpo::align_up(reinterpret_cast<uintptr_t>(ws), 256));
+    LmlArgs a{X, y_norm, n, d, theta, lml, grad, info, wsa, fit_ws_doubles(n, d, use_lds), 0};
+    int stop = 0;
+    if (const char* e = getenv("MPO_FIT_DEBUG")) stop = a.stop = atoi(e);
     a.theta_src = split && fit_fused_split(n, dp) ? theta_src : nullptr;
     MPO_CHECK_ARG(!theta_src || a.theta_src, "mpo_gp_lml_grad: a host theta source needs the fused split sweep");
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (split) {
-        MPO_CHECK_ARG(batch <= 65535, "mpo_gp_lml_grad: batch %d too large", batch);
-        switch (dp) {
-            case 4: return launch_split<4>(a, batch, s);
-            case 8: return launch_split<8>(a, batch, s);
-            case 12: return launch_split<12>(a, batch, s);
-            case 16: return launch_split<16>(a, batch, s);
-            default: return launch_split<32>(a, batch, s);
-        }
+        std::vector<LmlTheta> th;
+        th.reserve(batch);
+        problem_thetas(th, X, y_norm, n, d, dp, theta, a.theta_src, batch, lml, grad, info, wsa);
+        return launch_split_any(th, d, stop, s);
     }
     if (use_lds) {
         switch (dp) {

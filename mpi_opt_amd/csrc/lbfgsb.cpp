@@ -29,8 +29,12 @@
 #pragma clang fp contract(off)
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
+#include <string>
 #include <vector>
 
 #include "mpo_internal.h"
@@ -1052,9 +1056,120 @@ Options to_options(const MpoLbfgsbOptions* o) {
     return Options{o->ftol, o->gtol, o->maxiter, o->maxfun, o->maxcor, o->maxls};
 }
 
+// Rendezvous of the concurrent refits on one device (the cl_min chains' worker
+// threads).  A fit registers for its duration; each of its rounds is queued, and
+// the first thread that finds every registered fit either queued or already in a
+// launched group -- or whose wait reached the window -- launches all queued rounds
+// as ONE grouped split sweep on its own stream (mpo::lml_launch_rounds),
+// synchronises, and wakes the others; several groups may be in flight on their
+// leaders' streams.  A lone fit leads at once.  The grouping changes no result (each theta's arithmetic is its
+// own, gp_fit.hip LmlGroup); it divides the launches per round of all chains by
+// their number -- the one-GPU bound of concurrent refits (r05: ~115k small kernels/s
+// over 8 chains, ~6 per round, profiles/r05/).
+struct LmlBatcher {
+    int device = -1;
+    std::chrono::microseconds window{40};
+    std::mutex mu;
+    std::condition_variable cv;
+    int active = 0;      // registered fits
+    int inflight = 0;    // rounds in launched groups, not yet done
+    struct Req {
+        mpo::LmlRound round;
+        bool taken = false, done = false;
+        int rc = 0;
+        std::string err;
+    };
+    std::vector<Req*> pend;
+    long long launches = 0, rounds = 0;
+
+    void enter() {
+        std::lock_guard<std::mutex> lk(mu);
+        ++active;
+    }
+    void leave() {
+        std::lock_guard<std::mutex> lk(mu);
+        --active;
+        cv.notify_all();     // a waiting leader may now have every registered fit
+    }
+
+    int run(Req& q, hipStream_t s) {
+        std::unique_lock<std::mutex> lk(mu);
+        pend.push_back(&q);
+        cv.notify_all();
+        const auto deadline = std::chrono::steady_clock::now() + window;
+        for (;;) {
+            if (q.done) {
+                if (q.rc != MPO_OK) mpo::set_error("%s", q.err.c_str());
+                return q.rc;
+            }
+            if (q.taken) {
+                cv.wait(lk);
+                continue;
+            }
+            if ((int)pend.size() >= active - inflight || std::chrono::steady_clock::now() >= deadline) {
+                std::vector<Req*> mine;
+                mine.swap(pend);
+                for (Req* m : mine) m->taken = true;
+                inflight += (int)mine.size();
+                lk.unlock();
+                std::vector<mpo::LmlRound> rs;
+                rs.reserve(mine.size());
+                for (Req* m : mine) rs.push_back(m->round);
+                int rc = mpo::lml_launch_rounds(rs.data(), (int)rs.size(), s);
+                if (rc == MPO_OK) {
+                    const hipError_t e = hipStreamSynchronize(s);
+                    if (e != hipSuccess) {
+                        mpo::set_error("lml batcher: hipStreamSynchronize: %s", hipGetErrorString(e));
+                        rc = MPO_EHIP;
+                    }
+                }
+                const std::string err = rc != MPO_OK ? std::string(mpo_last_error()) : std::string();
+                lk.lock();
+                inflight -= (int)mine.size();
+                ++launches;
+                rounds += (long long)mine.size();
+                for (Req* m : mine) {
+                    m->rc = rc;
+                    m->err = err;
+                    m->done = true;
+                }
+                cv.notify_all();
+                continue;
+            }
+            cv.wait_until(lk, deadline);
+        }
+    }
+};
+
 }  // namespace
 
 extern "C" {
+
+int mpo_gp_lml_batcher_create(int device, void** handle) {
+    MPO_GUARD_BEGIN
+    MPO_CHECK_ARG(handle && device >= 0, "mpo_gp_lml_batcher_create: bad arguments");
+    auto* b = new LmlBatcher();
+    b->device = device;
+    *handle = b;
+    return MPO_OK;
+    MPO_GUARD_END
+}
+
+int mpo_gp_lml_batcher_destroy(void* handle) {
+    MPO_GUARD_BEGIN
+    delete static_cast<LmlBatcher*>(handle);
+    return MPO_OK;
+    MPO_GUARD_END
+}
+
+int mpo_gp_lml_batcher_stats(const void* handle, int64_t* launches, int64_t* rounds) {
+    MPO_CHECK_ARG(handle && launches && rounds, "mpo_gp_lml_batcher_stats: null pointer");
+    auto* b = const_cast<LmlBatcher*>(static_cast<const LmlBatcher*>(handle));
+    std::lock_guard<std::mutex> lk(b->mu);
+    *launches = b->launches;
+    *rounds = b->rounds;
+    return MPO_OK;
+}
 
 int mpo_lbfgsb_batched(int nvar, int nruns, const double* x0, const double* bounds, const MpoLbfgsbOptions* opts,
                        mpo_fg_batch_fn fg, void* user, double* x_out, double* f_out, int32_t* stats,
@@ -1074,7 +1189,7 @@ int mpo_lbfgsb_batched(int nvar, int nruns, const double* x0, const double* boun
 int mpo_gp_fit_lml_host(const double* X, const double* y_norm, int n, int d, const double* starts, int nruns,
                         const double* bounds, const MpoLbfgsbOptions* opts, double* theta_host, double* out_host,
                         void* dev_io, size_t io_bytes, void* ws, size_t ws_bytes, double* x_out, double* f_out,
-                        int32_t* stats, int32_t* rounds, void* stream) {
+                        int32_t* stats, int32_t* rounds, void* batcher, void* stream) {
     MPO_GUARD_BEGIN
     const int k = d + 2;
     MPO_CHECK_ARG(X && y_norm && theta_host && out_host && x_out && f_out && n > 0 && d > 0,
@@ -1082,11 +1197,51 @@ int mpo_gp_fit_lml_host(const double* X, const double* y_norm, int n, int d, con
     MPO_CHECK_ARG(options_ok(k, nruns, starts, bounds, opts), "mpo_gp_fit_lml_host: bad options / bounds");
     MPO_CHECK_ARG(io_bytes >= mpo_gp_lml_io_bytes(d, nruns), "mpo_gp_fit_lml_host: io buffer too small");
     MPO_CHECK_ARG(ws_bytes >= mpo_gp_lml_ws_bytes(n, d, nruns), "mpo_gp_fit_lml_host: workspace too small");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    mpo::StreamDeviceScope on_device(s);
+    // grouped rounds through the batcher: the fused split sweep, pinned theta / out
+    // buffers (their device views), a batcher of this stream's device
+    LmlBatcher* bt = static_cast<LmlBatcher*>(batcher);
+    mpo::LmlRound base{};
+    if (bt) {
+        int dev = -1;
+        hipPointerAttribute_t ta{}, oa{};
+        const bool ok = hipStreamGetDevice(s, &dev) == hipSuccess && dev == bt->device && mpo::lml_groupable(n, d) &&
+                        hipPointerGetAttributes(&ta, theta_host) == hipSuccess && ta.type == hipMemoryTypeHost &&
+                        ta.devicePointer && hipPointerGetAttributes(&oa, out_host) == hipSuccess &&
+                        oa.type == hipMemoryTypeHost && oa.devicePointer;
+        if (!ok) {
+            (void)hipGetLastError();
+            bt = nullptr;
+        } else {
+            base.X = X;
+            base.y = y_norm;
+            base.n = n;
+            base.d = d;
+            base.theta_dev = static_cast<double*>(dev_io);
+            base.theta_src = static_cast<const double*>(ta.devicePointer);
+            base.out = static_cast<double*>(oa.devicePointer);
+            base.ws = reinterpret_cast<double*>(mpo::align_up(reinterpret_cast<uintptr_t>(ws), 256));
+        }
+    }
+    struct Registration {
+        LmlBatcher* b;
+        explicit Registration(LmlBatcher* b_) : b(b_) { if (b) b->enter(); }
+        ~Registration() { if (b) b->leave(); }
+    } reg(bt);
     // one round: theta (pinned) -> lml | grad | info (pinned); the objective is -lml, -grad
     auto eval = [&](int b, const double* T, const int32_t*, double* f, double* g) -> int {
         std::memcpy(theta_host, T, sizeof(double) * (size_t)b * k);
-        const int rc = mpo_gp_lml_grad_host(X, y_norm, n, d, theta_host, b, out_host, dev_io, io_bytes, ws, ws_bytes,
-                                            stream);
+        int rc;
+        if (bt) {
+            LmlBatcher::Req q;
+            q.round = base;
+            q.round.batch = b;
+            rc = bt->run(q, s);
+        } else {
+            rc = mpo_gp_lml_grad_host(X, y_norm, n, d, theta_host, b, out_host, dev_io, io_bytes, ws, ws_bytes,
+                                      stream);
+        }
         if (rc != MPO_OK) return rc;
         for (int i = 0; i < b; ++i) f[i] = -out_host[i];
         for (size_t i = 0; i < (size_t)b * k; ++i) g[i] = -out_host[b + i];

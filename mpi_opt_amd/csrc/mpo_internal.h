@@ -117,6 +117,22 @@ inline size_t static_lds_bytes(const void* kern) {
     return at.sharedSizeBytes;
 }
 
+// One pending L-BFGS-B round of one GP refit (gp_fit.hip): `batch` thetas of the
+// problem (X, y, n) in the layout mpo_gp_lml_grad_host uses.  lml_launch_rounds
+// evaluates the rounds of several refits in one launch set (same d, every n
+// lml_groupable: the fused split sweep), enqueued on `s`, not synchronised.
+struct LmlRound {
+    const double* X;
+    const double* y;
+    int n, d, batch;
+    double* theta_dev;         // [batch][d+2] device: the build's copy of theta_src
+    const double* theta_src;   // [batch][d+2] pinned host, device view
+    double* out;               // pinned host, device view: lml [batch] | grad [batch][d+2] | info
+    double* ws;                // 256-B aligned, mpo_gp_lml_ws_bytes(n, d, batch)
+};
+bool lml_groupable(int n, int d);
+int lml_launch_rounds(const LmlRound* r, int count, hipStream_t s);
+
 }  // namespace mpo
 
 #define MPO_CHECK_ARG(cond, ...)              \

@@ -27,6 +27,16 @@ def objective(x):
                  + (drop - 0.3) ** 2 + 0.05 * np.sin(nb * dense / 300.0))
 
 
+def batcher_stats():
+    import ctypes
+
+    from mpi_opt_amd import _lib
+
+    la, ro = ctypes.c_int64(), ctypes.c_int64()
+    _lib.check(_lib.lib().mpo_gp_lml_batcher_stats(_lib.lml_batcher(0), ctypes.byref(la), ctypes.byref(ro)))
+    return la.value, ro.value
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=96)
@@ -65,13 +75,16 @@ def main():
         ex.run_now(jobs[:T])
         O.reset_stats()
         t0 = time.perf_counter()
+        la0, ro0 = batcher_stats()
         ex.run_now(jobs)
         dt = time.perf_counter() - t0
+        la1, ro1 = batcher_stats()
         st = dict(O.STATS)
         ex.close()
         print(f"  threads {T}: {st['refits']} refits in {dt:.2f} s = {st['refits'] / dt:.1f} refits/s; per refit "
               f"fit {st['refit_s'] / st['refits'] * 1e3:.2f} ms, proposal {st['propose_s'] / st['refits'] * 1e3:.2f} ms "
-              f"(polish {st['polish_s'] / st['refits'] * 1e3:.2f})", flush=True)
+              f"(polish {st['polish_s'] / st['refits'] * 1e3:.2f}); {ro1 - ro0} LML rounds in {la1 - la0} grouped launch sets",
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -130,6 +130,59 @@ def test_device_fit_matches_sklearn_fit(name, driver):
     assert np.max(np.abs(theta - ref)) <= 1e-3, (theta, ref)
 
 
+def _batcher_stats():
+    import ctypes
+
+    from mpi_opt_amd import _lib
+
+    la, ro = ctypes.c_int64(), ctypes.c_int64()
+    _lib.check(_lib.lib().mpo_gp_lml_batcher_stats(_lib.lml_batcher(0), ctypes.byref(la), ctypes.byref(ro)))
+    return la.value, ro.value
+
+
+def test_concurrent_fits_share_launches_with_identical_results():
+    """Refits on several threads at once (the cl_min chains) go through the
+    device's batcher: rounds of different problems (n = 60 ... 201) launch
+    together, and every fit's optima, values and counts equal its lone run."""
+    import threading
+
+    from mpi_opt_amd.gp_fit import DeviceLML, normalize_targets, theta_bounds
+
+    probs = []
+    for n, seed in [(60, 1), (96, 2), (150, 3), (201, 4), (96, 5), (75, 6)]:
+        X, y = O.synthetic_problem(n, 5, seed=seed)
+        probs.append((X, normalize_targets(y)[0]))
+    b = theta_bounds(5)
+    rng = np.random.RandomState(0)
+    starts = [np.array([np.zeros(7)] + [rng.uniform(b[:, 0], b[:, 1]) for _ in range(2)]) for _ in probs]
+    seq = [DeviceLML(X, yn, device="cuda:0").fit(st, b) for (X, yn), st in zip(probs, starts)]
+    l0, r0 = _batcher_stats()
+    out = [None] * len(probs)
+    errors = []
+
+    def run(i):
+        try:
+            torch.cuda.set_device(0)
+            with torch.cuda.stream(torch.cuda.Stream()):
+                out[i] = DeviceLML(*probs[i], device="cuda:0").fit(starts[i], b)
+        except BaseException as e:  # noqa: BLE001
+            errors.append(e)
+
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(len(probs))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errors, errors
+    l1, r1 = _batcher_stats()
+    print(f"{r1 - r0} rounds in {l1 - l0} grouped launch sets")
+    for (a, ra), (c, rc) in zip(seq, out):
+        assert ra == rc
+        for (x1, f1), (x2, f2) in zip(a, c):
+            assert np.array_equal(x1, x2) and f1 == f2
+    assert r1 - r0 == sum(r for _, r in seq) and l1 - l0 <= r1 - r0
+
+
 def test_fused_split_sweep_reports_failure():
     dev, _ = _lml("n230_d4")
     T = G["n230_d4_theta"][:3].copy()
