@@ -81,9 +81,10 @@ def make_parser():
     p.add_argument("--checkpoint", default="coordinator.pkl")
     p.add_argument("--ei-candidates", type=int, default=10000,
                    help="acquisition candidates per ask (skopt n_points); split over the GPUs when distributed")
-    p.add_argument("--chain-workers", type=int, default=4,
-                   help="concurrent cl_min ask batches per GPU (worker threads, one HIP stream each); "
-                        "0 runs every ask inline, as the reference's Coordinator does")
+    p.add_argument("--chain-workers", type=int, default=8,
+                   help="concurrent cl_min ask batches per GPU (worker threads, one HIP stream each; their "
+                        "refit rounds share launches); 0 runs every ask inline, as the reference's "
+                        "Coordinator does")
     p.add_argument("--population-chunks", type=int, default=1, dest="population_chunks",
                    help="train each population in this many parts, each as soon as its ask batches "
                         "resolve (overlaps the remaining batches with training; results unchanged)")
