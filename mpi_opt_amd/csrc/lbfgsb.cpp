@@ -27,6 +27,10 @@
 // matrix, so iterates agree with scipy's to rounding (tests/test_lbfgsb.py
 // compares them on the GP objective and on bound-constrained test functions).
 #pragma clang fp contract(off)
+// max / min of doubles are fmax / fmin throughout: a NaN operand yields the other one, as
+// the scipy build's L-BFGS-B does -- an infinite objective value (sklearn's LinAlgError
+// branch: -LML = +inf) turns the cubic step of dcstep into NaN, which then clamps to the
+// step bounds instead of propagating (tests/test_lbfgsb.py::test_infinite_objective_*).
 
 #include <algorithm>
 #include <chrono>
@@ -54,7 +58,7 @@ void dcstep(double& stx, double& fx, double& dx, double& sty, double& fy, double
     double stpf;
     if (fp > fx) {
         const double theta = 3.0 * (fx - fp) / (stp - stx) + dx + dp;
-        const double s = std::max(std::max(std::fabs(theta), std::fabs(dx)), std::fabs(dp));
+        const double s = std::fmax(std::fmax(std::fabs(theta), std::fabs(dx)), std::fabs(dp));
         double gamma = s * std::sqrt((theta / s) * (theta / s) - (dx / s) * (dp / s));
         if (stp < stx) gamma = -gamma;
         const double p = (gamma - dx) + theta;
@@ -67,7 +71,7 @@ void dcstep(double& stx, double& fx, double& dx, double& sty, double& fy, double
         brackt = true;
     } else if (sgnd < 0.0) {
         const double theta = 3.0 * (fx - fp) / (stp - stx) + dx + dp;
-        const double s = std::max(std::max(std::fabs(theta), std::fabs(dx)), std::fabs(dp));
+        const double s = std::fmax(std::fmax(std::fabs(theta), std::fabs(dx)), std::fabs(dp));
         double gamma = s * std::sqrt((theta / s) * (theta / s) - (dx / s) * (dp / s));
         if (stp > stx) gamma = -gamma;
         const double p = (gamma - dp) + theta;
@@ -79,8 +83,8 @@ void dcstep(double& stx, double& fx, double& dx, double& sty, double& fy, double
         brackt = true;
     } else if (std::fabs(dp) < std::fabs(dx)) {
         const double theta = 3.0 * (fx - fp) / (stp - stx) + dx + dp;
-        const double s = std::max(std::max(std::fabs(theta), std::fabs(dx)), std::fabs(dp));
-        double gamma = s * std::sqrt(std::max(0.0, (theta / s) * (theta / s) - (dx / s) * (dp / s)));
+        const double s = std::fmax(std::fmax(std::fabs(theta), std::fabs(dx)), std::fabs(dp));
+        double gamma = s * std::sqrt(std::fmax(0.0, (theta / s) * (theta / s) - (dx / s) * (dp / s)));
         if (stp > stx) gamma = -gamma;
         const double p = (gamma - dp) + theta;
         const double q = (gamma + (dx - dp)) + gamma;
@@ -92,17 +96,17 @@ void dcstep(double& stx, double& fx, double& dx, double& sty, double& fy, double
         const double stpq = stp + (dp / (dp - dx)) * (stx - stp);
         if (brackt) {
             stpf = std::fabs(stpc - stp) < std::fabs(stpq - stp) ? stpc : stpq;
-            if (stp > stx) stpf = std::min(stp + 0.66 * (sty - stp), stpf);
-            else stpf = std::max(stp + 0.66 * (sty - stp), stpf);
+            if (stp > stx) stpf = std::fmin(stp + 0.66 * (sty - stp), stpf);
+            else stpf = std::fmax(stp + 0.66 * (sty - stp), stpf);
         } else {
             stpf = std::fabs(stpc - stp) > std::fabs(stpq - stp) ? stpc : stpq;
-            stpf = std::min(stpmax, stpf);
-            stpf = std::max(stpmin, stpf);
+            stpf = std::fmin(stpmax, stpf);
+            stpf = std::fmax(stpmin, stpf);
         }
     } else {
         if (brackt) {
             const double theta = 3.0 * (fp - fy) / (sty - stp) + dy + dp;
-            const double s = std::max(std::max(std::fabs(theta), std::fabs(dy)), std::fabs(dp));
+            const double s = std::fmax(std::fmax(std::fabs(theta), std::fabs(dy)), std::fabs(dp));
             double gamma = s * std::sqrt((theta / s) * (theta / s) - (dy / s) * (dp / s));
             if (stp > sty) gamma = -gamma;
             const double p = (gamma - dp) + theta;
@@ -182,14 +186,14 @@ struct Dcsrch {
             width = std::fabs(sty - stx);
         }
         if (brackt) {
-            stmin = std::min(stx, sty);
-            stmax = std::max(stx, sty);
+            stmin = std::fmin(stx, sty);
+            stmax = std::fmax(stx, sty);
         } else {
             stmin = stp + 1.1 * (stp - stx);
             stmax = stp + 4.0 * (stp - stx);
         }
-        stp = std::max(stp, stpmin);
-        stp = std::min(stp, stpmax);
+        stp = std::fmax(stp, stpmin);
+        stp = std::fmin(stp, stpmax);
         if ((brackt && (stp <= stmin || stp >= stmax)) || (brackt && stmax - stmin <= xtol * stmax)) stp = stx;
         task = FG;
     }
@@ -297,12 +301,12 @@ class Lbfgsb {
             double gi = g_[i];
             if (nbd_[i] != 0) {
                 if (gi < 0.0) {
-                    if (nbd_[i] >= 2) gi = std::max(x_[i] - u_[i], gi);
+                    if (nbd_[i] >= 2) gi = std::fmax(x_[i] - u_[i], gi);
                 } else {
-                    if (nbd_[i] <= 2) gi = std::min(x_[i] - l_[i], gi);
+                    if (nbd_[i] <= 2) gi = std::fmin(x_[i] - l_[i], gi);
                 }
             }
-            s = std::max(s, std::fabs(gi));
+            s = std::fmax(s, std::fabs(gi));
         }
         return s;
     }
@@ -557,7 +561,7 @@ class Lbfgsb {
                     f1 += dibp * wmc;
                     f2 += 2.0 * dibp * wmp - dibp2 * wmw;
                 }
-                f2 = std::max(epsmch_ * f2_org, f2);
+                f2 = std::fmax(epsmch_ * f2_org, f2);
                 if (nleft > 0) {
                     dtm = -f1 / f2;
                     continue;
@@ -725,14 +729,14 @@ class Lbfgsb {
             const int nb = nbd_[k - 1];
             if (nb != 0) {
                 if (nb == 1) {
-                    z_[k - 1] = std::max(l_[k - 1], xk + dk);
+                    z_[k - 1] = std::fmax(l_[k - 1], xk + dk);
                     if (z_[k - 1] == l_[k - 1]) iword = 1;
                 } else if (nb == 2) {
-                    xk = std::max(l_[k - 1], xk + dk);
-                    z_[k - 1] = std::min(u_[k - 1], xk);
+                    xk = std::fmax(l_[k - 1], xk + dk);
+                    z_[k - 1] = std::fmin(u_[k - 1], xk);
                     if (z_[k - 1] == l_[k - 1] || z_[k - 1] == u_[k - 1]) iword = 1;
                 } else if (nb == 3) {
-                    z_[k - 1] = std::min(u_[k - 1], xk + dk);
+                    z_[k - 1] = std::fmin(u_[k - 1], xk + dk);
                     if (z_[k - 1] == u_[k - 1]) iword = 1;
                 }
             } else {
@@ -882,7 +886,7 @@ class Lbfgsb {
                         }
                     }
                 }
-                stp_ = (iter_ == 0 && !boxed_) ? std::min(1.0 / dnorm_, stpmx_) : 1.0;
+                stp_ = (iter_ == 0 && !boxed_) ? std::fmin(1.0 / dnorm_, stpmx_) : 1.0;
                 t_ = x_;
                 r_ = g_;
                 fold_ = f_;
@@ -933,7 +937,7 @@ class Lbfgsb {
             if (nit_ >= maxiter_) return finish(kStopMaxiter);
             if (nfev_ > maxfun_) return finish(kStopMaxfun);
             if (sbgnrm_ <= pgtol_) return finish(kConvPgtol);
-            const double ddum = std::max(std::max(std::fabs(fold_), std::fabs(f_)), 1.0);
+            const double ddum = std::fmax(std::fmax(std::fabs(fold_), std::fabs(f_)), 1.0);
             if (fold_ - f_ <= tol_ * ddum) return finish(kConvFactr);
             for (int i = 0; i < n_; ++i) r_[i] = g_[i] - r_[i];
             const double rr = ddot(n_, r_.data(), r_.data());

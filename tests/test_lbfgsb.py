@@ -222,3 +222,47 @@ def test_refit_optimum_agrees_with_scipy_driver(seed, n, d):
     j = int(np.argmin([f for _, f in ref]))
     assert abs(got[i][1] - ref[j][1]) <= 1e-8 * abs(ref[j][1])
     assert np.max(np.abs(got[i][0] - ref[j][0])) <= 1e-3
+
+
+def test_infinite_objective_values_as_scipy():
+    """sklearn's LinAlgError branch makes -LML = +inf (gradient 0) at some thetas.
+    An infinite trial value turns the line search's cubic step into NaN; scipy's
+    build clamps it to the step bounds (max / min ignore a NaN), which ends that
+    line search at the previous point.  The C++ driver does the same: equal
+    iterations, evaluations and end points."""
+    def f_inf(X):
+        f, g = rosen(X)
+        bad = X[:, 0] > 0.9
+        f, g = f.copy(), g.copy()
+        f[bad] = np.inf
+        g[bad] = 0.0
+        return f, g
+
+    starts = np.array([[-1.5, 2.0], [0.5, -1.0], [-0.3, 0.8], [0.85, 0.2]])
+    got, stats, _, _ = native(f_inf, starts, [(-2.0, 2.0)] * 2)
+    for s0, (x, f), st in zip(starts, got, stats):
+        r = scipy.optimize.minimize(lambda v: tuple(a[0] for a in f_inf(v[None])), s0, method="L-BFGS-B",
+                                    jac=True, bounds=[(-2.0, 2.0)] * 2)
+        assert int(st[0]) == r.nit and int(st[1]) == r.nfev
+        assert np.max(np.abs(x - r.x)) <= 1e-8 and abs(f - r.fun) <= 1e-9 * max(1.0, abs(r.fun))
+        assert np.isfinite(f)
+
+
+def test_nan_objective_values_as_scipy():
+    """A NaN value and gradient (no LinAlgError guard) ends the run abnormally at
+    the same point and counts as scipy's."""
+    def f_nan(X):
+        f, g = rosen(X)
+        bad = X[:, 0] > 0.9
+        f, g = f.copy(), g.copy()
+        f[bad] = np.nan
+        g[bad] = np.nan
+        return f, g
+
+    starts = np.array([[-1.5, 2.0], [0.5, -1.0], [0.85, 0.2], [1.5, 1.5]])
+    got, stats, _, _ = native(f_nan, starts, [(-2.0, 2.0)] * 2)
+    for s0, (x, f), st in zip(starts, got, stats):
+        r = scipy.optimize.minimize(lambda v: tuple(a[0] for a in f_nan(v[None])), s0, method="L-BFGS-B",
+                                    jac=True, bounds=[(-2.0, 2.0)] * 2)
+        assert int(st[0]) == r.nit and int(st[1]) == r.nfev and int(st[2]) == 5 and r.status == 2
+        assert np.max(np.abs(x - r.x)) <= 1e-8 and np.isnan(f) and np.isnan(r.fun)
