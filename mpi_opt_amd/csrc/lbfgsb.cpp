@@ -1116,10 +1116,22 @@ struct LmlBatcher {
                 for (Req* m : mine) m->taken = true;
                 inflight += (int)mine.size();
                 lk.unlock();
+                // one launch set per dimension d present (a process may run searches over
+                // different spaces on one GPU), in queue order
                 std::vector<mpo::LmlRound> rs;
                 rs.reserve(mine.size());
-                for (Req* m : mine) rs.push_back(m->round);
-                int rc = mpo::lml_launch_rounds(rs.data(), (int)rs.size(), s);
+                std::vector<bool> used(mine.size(), false);
+                int rc = MPO_OK;
+                for (size_t i = 0; i < mine.size() && rc == MPO_OK; ++i) {
+                    if (used[i]) continue;
+                    rs.clear();
+                    for (size_t j = i; j < mine.size(); ++j)
+                        if (!used[j] && mine[j]->round.d == mine[i]->round.d) {
+                            rs.push_back(mine[j]->round);
+                            used[j] = true;
+                        }
+                    rc = mpo::lml_launch_rounds(rs.data(), (int)rs.size(), s);
+                }
                 if (rc == MPO_OK) {
                     const hipError_t e = hipStreamSynchronize(s);
                     if (e != hipSuccess) {

@@ -142,20 +142,21 @@ def _batcher_stats():
 
 def test_concurrent_fits_share_launches_with_identical_results():
     """Refits on several threads at once (the cl_min chains) go through the
-    device's batcher: rounds of different problems (n = 60 ... 201) launch
-    together, and every fit's optima, values and counts equal its lone run."""
+    device's batcher: rounds of different problems (n = 60 ... 201, d = 5 and 3:
+    one launch set per d) launch together, and every fit's optima, values and
+    counts equal its lone run."""
     import threading
 
     from mpi_opt_amd.gp_fit import DeviceLML, normalize_targets, theta_bounds
 
-    probs = []
-    for n, seed in [(60, 1), (96, 2), (150, 3), (201, 4), (96, 5), (75, 6)]:
-        X, y = O.synthetic_problem(n, 5, seed=seed)
+    probs, bounds = [], []
+    for n, seed, d in [(60, 1, 5), (96, 2, 5), (150, 3, 3), (201, 4, 5), (96, 5, 3), (75, 6, 5)]:
+        X, y = O.synthetic_problem(n, d, seed=seed)
         probs.append((X, normalize_targets(y)[0]))
-    b = theta_bounds(5)
+        bounds.append(theta_bounds(d))
     rng = np.random.RandomState(0)
-    starts = [np.array([np.zeros(7)] + [rng.uniform(b[:, 0], b[:, 1]) for _ in range(2)]) for _ in probs]
-    seq = [DeviceLML(X, yn, device="cuda:0").fit(st, b) for (X, yn), st in zip(probs, starts)]
+    starts = [np.array([np.zeros(len(b))] + [rng.uniform(b[:, 0], b[:, 1]) for _ in range(2)]) for b in bounds]
+    seq = [DeviceLML(X, yn, device="cuda:0").fit(st, b) for (X, yn), st, b in zip(probs, starts, bounds)]
     l0, r0 = _batcher_stats()
     out = [None] * len(probs)
     errors = []
@@ -164,7 +165,7 @@ def test_concurrent_fits_share_launches_with_identical_results():
         try:
             torch.cuda.set_device(0)
             with torch.cuda.stream(torch.cuda.Stream()):
-                out[i] = DeviceLML(*probs[i], device="cuda:0").fit(starts[i], b)
+                out[i] = DeviceLML(*probs[i], device="cuda:0").fit(starts[i], bounds[i])
         except BaseException as e:  # noqa: BLE001
             errors.append(e)
 
