@@ -266,3 +266,15 @@ def test_nan_objective_values_as_scipy():
                                     jac=True, bounds=[(-2.0, 2.0)] * 2)
         assert int(st[0]) == r.nit and int(st[1]) == r.nfev and int(st[2]) == 5 and r.status == 2
         assert np.max(np.abs(x - r.x)) <= 1e-8 and np.isnan(f) and np.isnan(r.fun)
+
+
+@pytest.mark.parametrize("maxfun", [3, 5, 8])
+def test_maxfun_stops_as_scipy(maxfun):
+    """scipy's driver stops once more than maxfun evaluations were made (checked on NEW_X)."""
+    starts = np.array([[-1.5, 2.0], [1.8, -1.0]])
+    got, stats, _, _ = native(rosen, starts, [(-2.0, 2.0)] * 2, maxfun=maxfun)
+    for s0, (x, f), st in zip(starts, got, stats):
+        r = scipy.optimize.minimize(lambda v: tuple(a[0] for a in rosen(v[None])), s0, method="L-BFGS-B",
+                                    jac=True, bounds=[(-2.0, 2.0)] * 2, options={"maxfun": maxfun})
+        assert int(st[0]) == r.nit and int(st[1]) == r.nfev and int(st[2]) == 4 and r.status == 1
+        assert np.max(np.abs(x - r.x)) <= 1e-12 and abs(f - r.fun) <= 1e-12 * max(1.0, abs(r.fun))
