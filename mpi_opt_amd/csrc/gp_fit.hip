@@ -542,6 +542,11 @@ __host__ __device__ inline long long sw_np(int n) { return (n + kSwNb - 1) / kSw
 constexpr int kSplitMinN = 48;    // past it the split beats both single-workgroup kernels (0.09 vs 0.20 ms at n = 64)
 constexpr int kUpdThreads = 256;
 constexpr int kUpdTilesPerWave = 1;   // one lower tile per wave: latency-bound steps want many waves
+// sw_step workgroups per launch before waves take more tiles (one per CU).  Chains at
+// n = 448, 8 / 16 threads: 72 / 82 refits/s with one tile per wave, 93 / 120 at 256,
+// 98 / 112 at 512, 84 / 94 at 1024, 79 / 96 at 128, 68 / 85 at 64; n = 256: 150 / 189
+// -> 175 / 210 (profiles/r05/tpw_*.log); MPO_FIT_STEP_WG overrides it for sweeps
+constexpr long long kStepWgTarget = 256;
 
 // per-theta workspace (doubles): xs | alpha | A [np][np] | C0, C1 [np][32]
 // | P^-1 [32][32] | logdet, fail.  C_k (block column k before sweep k, row-major
@@ -834,15 +839,32 @@ __device__ __forceinline__ void pivot_block_sweep2(const double* __restrict__ C,
     }
 }
 
-// grid (nwg, B), kUpdThreads, nwg * 4 >= the lower tile count (one tile per wave):
-// the whole sweep step k in one launch.  Every workgroup sweeps the 32x32 pivot
-// block of C_k itself (wave 0, pivot_block_sweep2: the same instructions on the same
-// data, so the same P^-1 bits in every workgroup) into its LDS while the other waves
-// load their tile's operands; then each wave forms its own G_I = C_I P^-1 (16 MFMAs,
-// turned into the A-operand layout through its LDS slice) and updates its tile; the
-// diagonal tile (I, I) also writes G_I into block column k of A (and row I's entries
-// of C_{k+1}), tile (I, I) of block k writes -P^-1 there.  Workgroup 0 keeps the
-// log det and the failure column.
+// grid (nwg, B), kUpdThreads, nwg * 4 * tpw >= the lower tile count: the whole sweep
+// step k in one launch.  Every workgroup sweeps the 32x32 pivot block of C_k itself
+// (wave 0, pivot_block_sweep2: the same instructions on the same data, so the same
+// P^-1 bits in every workgroup) into its LDS while the other waves load their first
+// tile's operands; then each wave forms G_I = C_I P^-1 (16 MFMAs, turned into the
+// A-operand layout through its LDS slice) and updates its tile -- tpw tiles per wave,
+// tiles t, t + 4 nwg, ...; the diagonal tile (I, I) also writes G_I into block column
+// k of A (and row I's entries of C_{k+1}), tile (I, I) of block k writes -P^-1 there.
+// Workgroup 0 keeps the log det and the failure column.  A tile's arithmetic does not
+// depend on which wave computes it, so tpw changes no bits: it trades latency (one
+// tile per wave: the step is the sweep plus one update) for fewer redundant sweeps
+// when a grouped launch carries many thetas (launch_split_group).
+__device__ __forceinline__ void step_tile_of(int t, int nt_low, int k, int& I, int& J, int& kind) {
+    I = J = kind = 0;   // kind 0: nothing, 1: rows of block k <- -P^-1, 2: update tile (I, J)
+    if (t < nt_low) {
+        I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+        while (I * (I + 1) / 2 > t) --I;
+        while ((I + 1) * (I + 2) / 2 <= t) ++I;
+        J = t - I * (I + 1) / 2;
+        kind = (I >> 1) == k ? (I == J ? 1 : 0) : ((J >> 1) == k ? 0 : 2);
+    }
+    I = __builtin_amdgcn_readfirstlane(I);
+    J = __builtin_amdgcn_readfirstlane(J);
+    kind = __builtin_amdgcn_readfirstlane(kind);
+}
+
 __global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlGroup grp, int k) {
     const int b = blockIdx.y;
     const LmlTheta& T = grp.th[b];
@@ -857,21 +879,13 @@ __global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlGroup grp, int 
     double* Cn = k1 < np ? p.C(k + 1) : nullptr;
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
-    const int t = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kUpdThreads / 64) + wv));
     const int nt_low = ntile * (ntile + 1) / 2;
-    int I = 0, J = 0, kind = 0;   // 0: nothing, 1: rows of block k <- -P^-1, 2: update tile (I, J)
-    if (t < nt_low) {
-        I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-        while (I * (I + 1) / 2 > t) --I;
-        while ((I + 1) * (I + 2) / 2 <= t) ++I;
-        J = t - I * (I + 1) / 2;
-        kind = (I >> 1) == k ? (I == J ? 1 : 0) : ((J >> 1) == k ? 0 : 2);
-    }
-    I = __builtin_amdgcn_readfirstlane(I);
-    J = __builtin_amdgcn_readfirstlane(J);
-    kind = __builtin_amdgcn_readfirstlane(kind);
-    // the tile's operands that do not depend on P^-1: waves 1-3 load them while wave 0
-    // sweeps (if / else, so that they are not live across the sweep's registers)
+    const int stride = (int)gridDim.x * (kUpdThreads / 64);
+    int t = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kUpdThreads / 64) + wv));
+    int I, J, kind;
+    step_tile_of(t, nt_low, k, I, J, kind);
+    // the tile's operands that do not depend on P^-1: waves 1-3 load their first tile's
+    // while wave 0 sweeps (if / else, so that they are not live across the sweep's registers)
     double av[8], cb[8];
     f64x4 acc = {0.0, 0.0, 0.0, 0.0};
     auto load_tile = [&]() {
@@ -909,67 +923,75 @@ __global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlGroup grp, int 
         load_tile();
     }
     __syncthreads();
-    if (kind == 1) {
-#pragma unroll
-        for (int e = lane; e < 16 * kSwNb; e += 64) {
-            const int i = 16 * I + (e >> 5), c = e & 31;
-            p.A[(long long)i * np + k0 + c] = -Pl[(i - k0) * kSwNb + c];
-        }
-        return;
-    }
-    if (kind != 2) return;
     double* g = gl[wv];
-    {
-        double b0[8], b1[8];
-        const double* br = Pl + (lane >> 4) * kSwNb + (lane & 15);
+    for (;;) {
+        if (kind == 1) {
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks) {
-            b0[ks] = br[4 * ks * kSwNb];
-            b1[ks] = br[4 * ks * kSwNb + 16];
+            for (int e = lane; e < 16 * kSwNb; e += 64) {
+                const int i = 16 * I + (e >> 5), c = e & 31;
+                p.A[(long long)i * np + k0 + c] = -Pl[(i - k0) * kSwNb + c];
+            }
+        } else if (kind == 2) {
+            {
+                double b0[8], b1[8];
+                const double* br = Pl + (lane >> 4) * kSwNb + (lane & 15);
+#pragma unroll
+                for (int ks = 0; ks < 8; ++ks) {
+                    b0[ks] = br[4 * ks * kSwNb];
+                    b1[ks] = br[4 * ks * kSwNb + 16];
+                }
+                f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int ks = 0; ks < 8; ++ks) {
+                    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ks], b0[ks], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ks], b1[ks], acc1, 0, 0, 0);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int rr = (lane >> 4) + 4 * q, c0 = lane & 15, c1 = 16 + c0;
+                    g[(c0 >> 2) * 64 + rr + 16 * (c0 & 3)] = acc0[q];
+                    g[(c1 >> 2) * 64 + rr + 16 * (c1 & 3)] = acc1[q];
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's G_I stores (LDS ops of one wave complete in order)
+            double ga[8];
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) ga[ks] = g[ks * 64 + lane];
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks)
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-ga[ks], cb[ks], acc, 0, 0, 0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                p.A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)] = acc[q];
+            if (Cn && ((J >> 1) == k + 1 || (I >> 1) == k + 1)) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int i = 16 * I + (lane >> 4) + 4 * q, j = 16 * J + (lane & 15);
+                    if (i < j) continue;                                    // upper half of a diagonal tile
+                    if ((j >> 5) == k + 1) Cn[(long long)i * kSwNb + (j - k1)] = acc[q];
+                    if ((i >> 5) == k + 1) Cn[(long long)j * kSwNb + (i - k1)] = acc[q];
+                }
+            }
+            if (I == J) {
+                // block column k, rows 16 I .. 16 I + 15, <- G_I (lower storage: below
+                // block k at A[i][j], above it transposed at A[j][i]); a row of block k+1
+                // also gives row j of C_{k+1}
+#pragma unroll
+                for (int e = lane; e < 16 * kSwNb; e += 64) {
+                    const int ri = e >> 5, c = e & 31, i = 16 * I + ri, j = k0 + c;
+                    const double gv = g[(c >> 2) * 64 + ri + 16 * (c & 3)];
+                    if (i > j) p.A[(long long)i * np + j] = gv;
+                    else p.A[(long long)j * np + i] = gv;
+                    if (Cn && (i >> 5) == k + 1) Cn[(long long)j * kSwNb + (i - k1)] = gv;
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // g's reads before the next tile's stores
         }
-        f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int ks = 0; ks < 8; ++ks) {
-            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ks], b0[ks], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ks], b1[ks], acc1, 0, 0, 0);
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int rr = (lane >> 4) + 4 * q, c0 = lane & 15, c1 = 16 + c0;
-            g[(c0 >> 2) * 64 + rr + 16 * (c0 & 3)] = acc0[q];
-            g[(c1 >> 2) * 64 + rr + 16 * (c1 & 3)] = acc1[q];
-        }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's G_I stores (LDS ops of one wave complete in order)
-    double ga[8];
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) ga[ks] = g[ks * 64 + lane];
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks)
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-ga[ks], cb[ks], acc, 0, 0, 0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) p.A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)] = acc[q];
-    if (Cn && ((J >> 1) == k + 1 || (I >> 1) == k + 1)) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int i = 16 * I + (lane >> 4) + 4 * q, j = 16 * J + (lane & 15);
-            if (i < j) continue;                                    // upper half of a diagonal tile
-            if ((j >> 5) == k + 1) Cn[(long long)i * kSwNb + (j - k1)] = acc[q];
-            if ((i >> 5) == k + 1) Cn[(long long)j * kSwNb + (i - k1)] = acc[q];
-        }
-    }
-    if (I == J) {
-        // block column k, rows 16 I .. 16 I + 15, <- G_I (lower storage: below
-        // block k at A[i][j], above it transposed at A[j][i]); a row of block k+1
-        // also gives row j of C_{k+1}
-#pragma unroll
-        for (int e = lane; e < 16 * kSwNb; e += 64) {
-            const int ri = e >> 5, c = e & 31, i = 16 * I + ri, j = k0 + c;
-            const double gv = g[(c >> 2) * 64 + ri + 16 * (c & 3)];
-            if (i > j) p.A[(long long)i * np + j] = gv;
-            else p.A[(long long)j * np + i] = gv;
-            if (Cn && (i >> 5) == k + 1) Cn[(long long)j * kSwNb + (i - k1)] = gv;
-        }
+        t += stride;
+        if (t >= nt_low) break;
+        step_tile_of(t, nt_low, k, I, J, kind);
+        acc = f64x4{0.0, 0.0, 0.0, 0.0};
+        load_tile();
     }
 }
 
@@ -1222,7 +1244,16 @@ int launch_split_group(const LmlTheta* th, int count, int d, int stop, hipStream
         }
         const int np = (int)sw_np(nmax), nbk = np / kSwNb, ntile = np / 16, B = g.count;
         const int nt_low = ntile * (ntile + 1) / 2;
-        const int nwg = std::max(1, (nt_low + 4 * kUpdTilesPerWave - 1) / (4 * kUpdTilesPerWave));
+        // tiles per wave: one while the launch's workgroups fit ~4 per CU (latency: a step
+        // is one sweep plus one tile update); more when a grouped launch carries many
+        // thetas, so fewer workgroups repeat the pivot sweep
+        static const long long wg_target = [] {   // MPO_FIT_STEP_WG: tuning sweeps only
+            const char* e = getenv("MPO_FIT_STEP_WG");
+            return e && *e ? std::max(1LL, atoll(e)) : kStepWgTarget;
+        }();
+        int tpw = kUpdTilesPerWave;
+        while (tpw < 16 && (long long)B * nt_low / (4LL * tpw) > wg_target) tpw *= 2;
+        const int nwg = std::max(1, (nt_low + 4 * tpw - 1) / (4 * tpw));
         const size_t xs_lds = (size_t)np * DP * sizeof(double);
         const bool fuse_build = xs_lds <= 64 * 1024;
         if (fuse_build) {

@@ -22,6 +22,10 @@ def main():
         T[0] = 0.0
         lml, grad, info = dev.evaluate(T)
         out[f"n{n}_lml"], out[f"n{n}_grad"], out[f"n{n}_info"] = lml, grad, info
+        if n >= 256:   # a full group: the step kernel's tiles-per-wave > 1 path
+            T40 = np.random.RandomState(d + 1).uniform(b[:, 0], b[:, 1], size=(40, d + 2))
+            lml, grad, info = dev.evaluate(T40)
+            out[f"n{n}_b40_lml"], out[f"n{n}_b40_grad"], out[f"n{n}_b40_info"] = lml, grad, info
     np.savez(sys.argv[1], **out)
     if len(sys.argv) > 2:
         ref = np.load(sys.argv[2])
