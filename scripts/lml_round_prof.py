@@ -10,6 +10,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import scripts.ab_lib  # noqa: E402,F401
 from mpi_opt_amd import gp_fit as GF  # noqa: E402
 
 

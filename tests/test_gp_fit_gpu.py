@@ -73,6 +73,23 @@ def test_batching_does_not_change_results(name):
         assert l1[0] == lml[b] and np.array_equal(g1[0], grad[b])
 
 
+@pytest.mark.parametrize("name", ["n256_d10", "n500_d10"])
+def test_full_batch_step_tiles_per_wave_keep_bits(name):
+    """40 thetas in one launch set: the step kernel's waves take several tiles each
+    (csrc/gp_fit.hip kStepWgTarget), one theta alone takes one tile per wave -- the
+    same bits either way."""
+    from mpi_opt_amd.gp_fit import theta_bounds
+
+    dev, X = _lml(name)
+    b = theta_bounds(X.shape[1])
+    T = np.random.RandomState(7).uniform(b[:, 0], b[:, 1], size=(40, X.shape[1] + 2))
+    lml, grad, info = dev.evaluate(T)
+    for i in range(len(T)):
+        l1, g1, i1 = dev.evaluate(T[i:i + 1])
+        assert i1[0] == info[i]
+        assert (l1[0] == lml[i] or (np.isnan(l1[0]) and np.isnan(lml[i]))) and np.array_equal(g1[0], grad[i]), i
+
+
 @pytest.mark.parametrize("name,kernel", [("n200_d10", "panel"), ("n130_d6", "panel"), ("n57_d3", "split")])
 def test_other_kernel_still_matches_sklearn(name, kernel, monkeypatch):
     """Each LML kernel outside its default range: the Cholesky kernel at n <= 200,
