@@ -539,8 +539,12 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 __host__ __device__ inline long long sw_np(int n) { return (n + kSwNb - 1) / kSwNb * kSwNb; }
 
+#ifndef MPO_SWEEP_NW
+#define MPO_SWEEP_NW 4
+#endif
 constexpr int kSplitMinN = 48;    // past it the split beats both single-workgroup kernels (0.09 vs 0.20 ms at n = 64)
 constexpr int kUpdThreads = 256;
+constexpr int kSweepNW = MPO_SWEEP_NW;   // waves that share the pivot sweep of a step (2 or 4)
 constexpr int kUpdTilesPerWave = 1;   // one lower tile per wave: latency-bound steps want many waves
 // sw_step workgroups per launch before waves take more tiles (one per CU).  Chains at
 // n = 448, 8 / 16 threads: 72 / 82 refits/s with one tile per wave, 93 / 120 at 256,
@@ -743,25 +747,6 @@ __global__ __launch_bounds__(1024) void sw_xs_build_kernel(LmlGroup grp) {
     }
 }
 
-// Gauss-Jordan sweep of the 32x32 pivot block rows k0 .. k0+31 of C (row-major
-// [np][32]) by one wave: lane l + 32 h holds columns [16 h, 16 h + 16) of row l,
-// eliminating with the pivot row (not the symmetric column: that measured 10-100x
-// less accurate at cond(K) ~ 1e5).  Two steps per LDS round: the pivot rows c and
-// c + 1 are broadcast together, and every lane forms row c + 1 after step c itself
-// (row2' = fma(-t21, row1, row2), its column c = t21, pv2 = row2'[c + 1]) and the
-// column-(c+1) entry of its own row after step c (colv2' = fma(f1, row1[c+1], colv2),
-// 0 for the zeroed pivot row) with exactly the operations the owning lanes perform
-// in a one-step sweep (r03: the same bits, tested against it before that form was
-// removed) -- half the LDS round trips and serial latency chains, 16 more FMAs per
-// two steps.  On return r holds -P^-1 (lane's half row), prod the product of the
-// pivots, bad the first non-positive pivot (1-based) or 0.  rowb: 64 doubles.
-// r = 0 on the active lanes as 16 exec-masked v_mov_b64 (a branch): written as plain
-// stores the compiler if-converts the branch into two v_cndmask_b32 per double
-__device__ __forceinline__ void zero_row(double (&r)[16]) {
-#pragma unroll
-    for (int jj = 0; jj < 16; ++jj) asm volatile("v_mov_b64 %0, 0" : "=v"(r[jj]));
-}
-
 // 1 / x for the pivot sweep's serial chain: v_rcp_f64 and two Newton steps (a few
 // fp64 FMAs instead of the IEEE division's scale / fixup sequence; within an ulp).
 // LML launch 3-4% shorter at n = 128-512 (profiles/r05/fit_pivot_rcp_ab_ag.log)
@@ -773,54 +758,88 @@ __device__ __forceinline__ double pivot_rcp(double x) {
     return fma(r, e, r);
 }
 
-__device__ __forceinline__ void pivot_block_sweep2(const double* __restrict__ C, int k0, double* rowb,
-                                                   double (&r)[16], double& prod, int& bad) {
+// Gauss-Jordan sweep of the 32x32 pivot block rows k0 .. k0+31 of C (row-major
+// [np][32]), eliminating with the pivot row (not the symmetric column: that measured
+// 10-100x less accurate at cond(K) ~ 1e5).  Two steps per LDS round: the pivot rows c
+// and c + 1 are broadcast together, and every lane forms row c + 1 after step c itself
+// (row2' = fma(-t21, row1, row2), its column c = t21, pv2 = row2'[c + 1]) and the
+// column-(c+1) entry of its own row after step c (colv2' = fma(f1, row1[c+1], colv2),
+// 0 for the zeroed pivot row) with exactly the operations the owning lanes perform in
+// a one-step sweep (r03: the same bits, tested against it before that form was
+// removed) -- half the LDS round trips and serial latency chains, 16 more FMAs per two
+// steps.  On return r holds -P^-1 (the lane's columns of its row), prod the product of
+// the pivots, bad the first non-positive pivot (1-based) or 0.  A zeroed pivot row is
+// written as exec-masked v_mov_b64 (a branch): as plain stores the compiler
+// if-converts the branch into two v_cndmask_b32 per double.
+//
+// The sweep on NW waves (2 or 4): wave w's lane l + 32 h holds the CW =
+// 16 / NW columns [16 h + CW w, 16 h + CW w + CW) of row l, so each lane issues 1 / NW
+// of the FMAs.  Every element sees exactly the operations of the one-wave form (the
+// pivot rows and the pivot columns' entries go through the LDS instead of a cross-lane
+// shuffle), so the bits are the same.  One barrier per two sweep steps (the LDS rounds
+// alternate between two buffers); waves of the workgroup that do not sweep must meet
+// the kSweepBarriers barriers too.  rowb: [2][64] doubles, colb: [2][64].
+constexpr int kSweepBarriers = kSwNb / 2;
+template <int CW>
+__device__ __forceinline__ void zero_cols(double (&r)[CW]) {
+#pragma unroll
+    for (int jj = 0; jj < CW; ++jj) asm volatile("v_mov_b64 %0, 0" : "=v"(r[jj]));
+}
+
+template <int NW>
+__device__ __forceinline__ void pivot_block_sweep_nw(const double* __restrict__ C, int k0, double* rowb, double* colb,
+                                                     int w, double (&r)[16 / NW], double& prod, int& bad) {
+    constexpr int CW = 16 / NW;
     const int lane = threadIdx.x & 63;
     const int l = lane & 31, h = lane >> 5;
+    const int col0 = 16 * h + CW * w;   // this lane's first column
 #pragma unroll
-    for (int jj = 0; jj < 16; ++jj) r[jj] = C[(long long)(k0 + l) * kSwNb + 16 * h + jj];
+    for (int jj = 0; jj < CW; ++jj) r[jj] = C[(long long)(k0 + l) * kSwNb + col0 + jj];
     prod = 1.0;
     bad = 0;
 #pragma unroll
     for (int c = 0; c < kSwNb; c += 2) {
-        const int hc = c >> 4, jc = c & 15;       // columns c, c + 1: same half, jc even
-        const double colv1 = __shfl(r[jc], l + 32 * hc);       // A[l][c]
-        const double colv2 = __shfl(r[jc + 1], l + 32 * hc);   // A[l][c+1], before step c
+        double* rb = rowb + ((c >> 1) & 1) * 64;
+        double* cl = colb + ((c >> 1) & 1) * 64;
+        const int hc = c >> 4, wc = (c & 15) / CW, jc = c % CW;   // columns c, c + 1: one lane's, jc even
+        if (h == hc && w == wc) {
+            cl[2 * l] = r[jc];           // A[l][c]
+            cl[2 * l + 1] = r[jc + 1];   // A[l][c+1], before step c
+        }
         const bool piv1 = l == c, piv2 = l == c + 1;
         if (piv1 || piv2) {
 #pragma unroll
-            for (int jj = 0; jj < 16; ++jj) rowb[32 * (l - c) + 16 * h + jj] = r[jj];
+            for (int jj = 0; jj < CW; ++jj) rb[32 * (l - c) + col0 + jj] = r[jj];
         }
-        if (piv1) zero_row(r);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (piv1) zero_cols<CW>(r);
+        __syncthreads();
+        const double colv1 = cl[2 * l], colv2 = cl[2 * l + 1];
         // ---- step c
-        const double pv1 = rowb[c];
+        const double pv1 = rb[c];
         if (!(pv1 > 0.0) || !isfinite(pv1)) bad = bad ? bad : c + 1;
         prod *= pv1;
         const double ip1 = pivot_rcp(pv1);
         const double t1 = colv1 * ip1;
         const double f1 = piv1 ? ip1 : -t1;
-        const double p1c1 = rowb[c + 1], p2c = rowb[32 + c], p2c1 = rowb[32 + c + 1];
-        double q1[16], q2[16];
+        const double p1c1 = rb[c + 1], p2c = rb[32 + c], p2c1 = rb[32 + c + 1];
+        double q1[CW], q2[CW];
 #pragma unroll
-        for (int jj = 0; jj < 16; ++jj) {
-            q1[jj] = rowb[16 * h + jj];
-            q2[jj] = rowb[32 + 16 * h + jj];
+        for (int jj = 0; jj < CW; ++jj) {
+            q1[jj] = rb[col0 + jj];
+            q2[jj] = rb[32 + col0 + jj];
         }
-        // row c + 1 after step c, as its own lanes form it (t21 = their t1)
         const double t21 = p2c * ip1;
 #pragma unroll
-        for (int jj = 0; jj < 16; ++jj) {
+        for (int jj = 0; jj < CW; ++jj) {
             const double u = fma(-t21, q1[jj], q2[jj]);
-            q2[jj] = (jj == jc && h == hc) ? t21 : u;
+            q2[jj] = col0 + jj == c ? t21 : u;
         }
         const double pv2 = fma(-t21, p1c1, p2c1);
         const double colv2p = fma(f1, p1c1, piv1 ? 0.0 : colv2);
 #pragma unroll
-        for (int jj = 0; jj < 16; ++jj) {
+        for (int jj = 0; jj < CW; ++jj) {
             const double upd = fma(f1, q1[jj], r[jj]);
-            if (jj == jc) r[jj] = h == hc ? (piv1 ? -ip1 : t1) : upd;
-            else r[jj] = upd;
+            r[jj] = col0 + jj == c ? (piv1 ? -ip1 : t1) : upd;
         }
         // ---- step c + 1 (pivot row = q2)
         if (!(pv2 > 0.0) || !isfinite(pv2)) bad = bad ? bad : c + 2;
@@ -828,12 +847,11 @@ __device__ __forceinline__ void pivot_block_sweep2(const double* __restrict__ C,
         const double ip2 = pivot_rcp(pv2);
         const double t2 = colv2p * ip2;
         const double f2 = piv2 ? ip2 : -t2;
-        if (piv2) zero_row(r);
+        if (piv2) zero_cols<CW>(r);
 #pragma unroll
-        for (int jj = 0; jj < 16; ++jj) {
+        for (int jj = 0; jj < CW; ++jj) {
             const double upd = fma(f2, q2[jj], r[jj]);
-            if (jj == jc + 1) r[jj] = h == hc ? (piv2 ? -ip2 : t2) : upd;
-            else r[jj] = upd;
+            r[jj] = col0 + jj == c + 1 ? (piv2 ? -ip2 : t2) : upd;
         }
         asm volatile("" ::: "memory");
     }
@@ -841,9 +859,9 @@ __device__ __forceinline__ void pivot_block_sweep2(const double* __restrict__ C,
 
 // grid (nwg, B), kUpdThreads, nwg * 4 * tpw >= the lower tile count: the whole sweep
 // step k in one launch.  Every workgroup sweeps the 32x32 pivot block of C_k itself
-// (wave 0, pivot_block_sweep2: the same instructions on the same data, so the same
-// P^-1 bits in every workgroup) into its LDS while the other waves load their first
-// tile's operands; then each wave forms G_I = C_I P^-1 (16 MFMAs, turned into the
+// (pivot_block_sweep_nw on kSweepNW waves: the same instructions on the same data, so
+// the same P^-1 bits in every workgroup) into its LDS while its waves' first tile
+// operands land; then each wave forms G_I = C_I P^-1 (16 MFMAs, turned into the
 // A-operand layout through its LDS slice) and updates its tile -- tpw tiles per wave,
 // tiles t, t + 4 nwg, ...; the diagonal tile (I, I) also writes G_I into block column
 // k of A (and row I's entries of C_{k+1}), tile (I, I) of block k writes -P^-1 there.
@@ -851,6 +869,9 @@ __device__ __forceinline__ void pivot_block_sweep2(const double* __restrict__ C,
 // depend on which wave computes it, so tpw changes no bits: it trades latency (one
 // tile per wave: the step is the sweep plus one update) for fewer redundant sweeps
 // when a grouped launch carries many thetas (launch_split_group).
+// r05: the sweep on 4 waves instead of 1 (bit-identical): an LML round of 3 thetas
+// 166 -> 153 us at n = 256, 316 -> 288 us at n = 448; 2 waves measured the same as 4
+// (profiles/r05/lml_sweep2w_ab_a.log, lml_sweep4w_ab_a.log)
 __device__ __forceinline__ void step_tile_of(int t, int nt_low, int k, int& I, int& J, int& kind) {
     I = J = kind = 0;   // kind 0: nothing, 1: rows of block k <- -P^-1, 2: update tile (I, J)
     if (t < nt_low) {
@@ -874,7 +895,8 @@ __global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlGroup grp, int 
     const double* Cc = p.C(k);
     __shared__ double gl[kUpdThreads / 64][16 * kSwNb];   // per wave: G_I, A-operand order
     __shared__ double Pl[kSwNb * kSwNb];                  // P^-1 of this step
-    __shared__ double rowb[2 * kSwNb];
+    __shared__ double rowb[2 * 2 * kSwNb];
+    __shared__ double colb[2 * 2 * kSwNb];
     const int k1 = k0 + kSwNb;
     double* Cn = k1 < np ? p.C(k + 1) : nullptr;
     const int lane = threadIdx.x & 63;
@@ -900,27 +922,30 @@ __global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlGroup grp, int 
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc[q] = p.A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)];
     };
-    if (wv == 0) {
-        const int l = lane & 31, h = lane >> 5;
-        double r[16], prod;
+    // every wave issues its first tile's loads, then the kSweepNW sweeping waves sweep
+    // (pivot_block_sweep_nw) while they land; any other waves meet the sweep's barriers
+    load_tile();
+    if (wv < kSweepNW) {
+        constexpr int CW = 16 / kSweepNW;
+        const int l = lane & 31, h = lane >> 5, col0 = 16 * h + CW * wv;
+        double r[CW], prod;
         int bad;
         if (grp.stop == 23) {   // diagnostics only (MPO_FIT_DEBUG=23): the sweep skipped, timing of the rest
             prod = 1.0;
             bad = 0;
 #pragma unroll
-            for (int jj = 0; jj < 16; ++jj) r[jj] = Cc[(long long)(k0 + l) * kSwNb + 16 * h + jj];
+            for (int jj = 0; jj < CW; ++jj) r[jj] = Cc[(long long)(k0 + l) * kSwNb + col0 + jj];
         } else {
-            pivot_block_sweep2(Cc, k0, rowb, r, prod, bad);
+            pivot_block_sweep_nw<kSweepNW>(Cc, k0, rowb, colb, wv, r, prod, bad);
         }
 #pragma unroll
-        for (int jj = 0; jj < 16; ++jj) Pl[l * kSwNb + 16 * h + jj] = -r[jj];
-        if (blockIdx.x == 0 && lane == 0) {
+        for (int jj = 0; jj < CW; ++jj) Pl[l * kSwNb + col0 + jj] = -r[jj];
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
             p.acc[0] += log(prod);
             if (bad && p.acc[1] == 0.0) p.acc[1] = (double)(k0 + bad);
         }
-        load_tile();
-    } else {
-        load_tile();
+    } else if (grp.stop != 23) {
+        for (int i = 0; i < kSweepBarriers; ++i) __syncthreads();
     }
     __syncthreads();
     double* g = gl[wv];
