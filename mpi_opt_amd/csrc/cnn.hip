@@ -1389,7 +1389,7 @@ int env_int(const char* name, int dflt) {
 
 // Planner overrides for tuning sweeps, one variable: MPO_POP_PLAN="key=value,..."
 // (keys: dg_tiles, dg_kb, conv_mt, conv_kb1, conv_kb2, wg_spg1, wg_spg2, streams = 1 | 2 | 3,
-// occmerge = 0 | 1).  Every
+// occmerge = 0 | 1 | 2, occfill = quarter waves, see bucket_segs).  Every
 // value only changes how work is cut into items or ordered over streams, never the arithmetic.
 int plan_knob(const char* key, int dflt) {
     const char* v = getenv("MPO_POP_PLAN");
@@ -1474,9 +1474,13 @@ int choose_rows(int Ho, Fn lds_of, int kb1 = 52, int kb2 = 78, int mcap = 128) {
 // Workgroups per CU that `lds` bytes allow (LDS 160 KiB; 8 = the 32-wave cap).
 int lds_class(size_t lds) { return (int)std::min<size_t>(8, ((size_t)160 << 10) / std::max<size_t>(lds, 1)); }
 
+// mode 0: one segment per (NT, sub, occupancy class); 1: one per (NT, sub) at the
+// largest member's LDS; 2: adjacent occupancy classes of one (NT, sub) merge while
+// either of them is short of one full wave of workgroups at its own occupancy
 template <class T>
 void bucket_segs(std::vector<T>& items, Bucketed& bk, const std::vector<Member>& mem, const std::vector<size_t>& lds,
-                 bool by_occupancy = true) {
+                 int mode = 0) {
+    const bool by_occupancy = mode != 1;
     // by_occupancy = false: one segment per (NT, sub) at the largest member's LDS (fewer, fuller launches)
     auto key = [&](const T& x) {
         return (mem[x.member].nt * 8 + item_sub(x)) * 16 + (by_occupancy ? 8 - lds_class(lds[x.member]) : 0);
@@ -1491,6 +1495,17 @@ void bucket_segs(std::vector<T>& items, Bucketed& bk, const std::vector<Member>&
             ++i;
         }
         sg.end = i;
+        if (mode == 2 && !bk.segs.empty()) {
+            Seg& pv = bk.segs.back();
+            static const long long fill4 = std::max(1, plan_knob("occfill", 4));   // quarter waves
+            const long long full_pv = 64LL * fill4 * lds_class(pv.lds), full_sg = 64LL * fill4 * lds_class(sg.lds);
+            if (pv.nt == sg.nt && pv.sub == sg.sub &&
+                (pv.end - pv.begin < full_pv || sg.end - sg.begin < full_sg)) {
+                pv.end = sg.end;
+                pv.lds = std::max(pv.lds, sg.lds);
+                continue;
+            }
+        }
         bk.segs.push_back(sg);
     }
 }
@@ -1650,10 +1665,13 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
     for (auto& m : P.mem) wmax = std::max(wmax, (long long)m.k * m.k * m.F * m.F + m.F);
     P.wred_blocks = (int)((wmax + P.wred_per_block - 1) / P.wred_per_block);
     // Small populations (a distributed shard, configs[0]) launch too few workgroups per occupancy class
-    // to fill the chip, so their classes merge; measured on MI355X (profiles/r05/occmerge_o.log):
-    // 20 members 3.82 -> 3.52 ms, 40: 5.93 -> 5.70, 80: 10.94 -> 10.96, 160: 19.81 -> 20.30,
-    // 320: 36.92 -> 39.06 ms per train step. The segmenting changes no arithmetic.
-    const bool occ = plan_knob("occmerge", n <= 64 ? 1 : 0) == 0;
+    // to fill the chip.  Merging every class of an (NT, sub) bucket (mode 1) measured on MI355X
+    // (profiles/r05/occmerge_o.log): 20 members 3.82 -> 3.52 ms, 40: 5.93 -> 5.70, 80: 10.94 -> 10.96,
+    // 160: 19.81 -> 20.30, 320: 36.92 -> 39.06 ms per train step.  Merging only adjacent classes
+    // short of one full wave (mode 2, the default): 20: 3.53, 40: 5.56-5.59, 80: 10.63-10.67,
+    // 320: 36.81-36.95 (separate classes 36.87) -- profiles/r05/occmerge2_*.log.  The segmenting
+    // changes no arithmetic.
+    const int occ = plan_knob("occmerge", 2);
     bucket_segs(P.conv1, P.bc1, P.mem, L1, occ);
     bucket_segs(P.conv2, P.bc2, P.mem, L2, occ);
     bucket_segs(P.dgrad, P.bdg, P.mem, LD, occ);
