@@ -1057,6 +1057,58 @@ __global__ __launch_bounds__(256) void sw_alpha_kernel(LmlGroup grp) {
 // workspace's own end (mpo_gp_lml_ws_bytes adds them)
 constexpr int kPairGroups = 64;
 
+// The pairs i >= j of rows i = gw, gw + nw, ... (one wave per row): W_ij dK_ij/dtheta
+// (sklearn kernels.py:1747-1767) into g, each lane taking j = lane, lane + 64, ...
+// Two pairs' operands (alpha_j, A_ij, xs_j) are loaded before either is evaluated, so
+// one load latency covers two pairs; the lane still adds its pairs in j order
+// (bit-identical; sw_pairs_final 22.4 -> 19.2 us at n = 448, profiles/r05/lml_pair_prefetch_a.log).
+template <int DP>
+__device__ __forceinline__ void pair_rows(const SsPtrs& p, int n, int d, int np, double amp, double noise, int gw,
+                                          int nw, int lane, double (&g)[DP + 2]) {
+    for (int i = gw; i < n; i += nw) {
+        const double ai = p.alpha[i];
+        double xi[DP];
+#pragma unroll
+        for (int c = 0; c < DP; ++c) xi[c] = c < d ? p.xs[i * d + c] : 0.0;
+        for (int j0 = lane; j0 <= i; j0 += 128) {
+            double aj[2], aij[2], xj[2][DP];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int j = j0 + 64 * u <= i ? j0 + 64 * u : j0;
+                aj[u] = p.alpha[j];
+                aij[u] = p.A[(long long)i * np + j];
+#pragma unroll
+                for (int c = 0; c < DP; ++c) xj[u][c] = c < d ? p.xs[j * d + c] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int j = j0 + 64 * u;
+                if (j > i) break;
+                const double W = (ai * aj[u] + aij[u]) * (i == j ? 1.0 : 2.0);
+                double r2 = 0.0;
+#pragma unroll
+                for (int c = 0; c < DP; ++c)
+                    if (c < d) {
+                        const double t = xi[c] - xj[u][c];
+                        r2 += t * t;
+                    }
+                const double sq = sqrt(5.0 * r2);
+                const double e = exp(-sq);
+                const double Mij = i == j ? 1.0 : (1.0 + sq + sq * sq / 3.0) * e;
+                g[0] += W * (amp * Mij);
+                const double f = W * amp * (5.0 / 3.0) * (sq + 1.0) * e;
+#pragma unroll
+                for (int c = 0; c < DP; ++c)
+                    if (c < d) {
+                        const double t = xi[c] - xj[u][c];
+                        g[1 + c] += f * (t * t);
+                    }
+                if (i == j) g[DP + 1] += W * noise;
+            }
+        }
+    }
+}
+
 // grid (kPairGroups, B), 256 threads: pairs i >= j of rows i = gw (mod waves),
 // W_ij dK_ij/dtheta; one partial per workgroup
 template <int DP>
@@ -1074,37 +1126,7 @@ __global__ __launch_bounds__(256) void sw_pairs_kernel(LmlGroup grp) {
     double g[DP + 2];
 #pragma unroll
     for (int c = 0; c < DP + 2; ++c) g[c] = 0.0;
-    if (p.acc[1] == 0.0) {
-        for (int i = gw; i < n; i += nw) {
-            const double ai = p.alpha[i];
-            double xi[DP];
-#pragma unroll
-            for (int c = 0; c < DP; ++c) xi[c] = c < d ? p.xs[i * d + c] : 0.0;
-            for (int j = lane; j <= i; j += 64) {
-                const double W = (ai * p.alpha[j] + p.A[(long long)i * np + j]) * (i == j ? 1.0 : 2.0);
-                const double* xj = p.xs + j * d;
-                double r2 = 0.0;
-#pragma unroll
-                for (int c = 0; c < DP; ++c)
-                    if (c < d) {
-                        const double t = xi[c] - xj[c];
-                        r2 += t * t;
-                    }
-                const double sq = sqrt(5.0 * r2);
-                const double e = exp(-sq);
-                const double Mij = i == j ? 1.0 : (1.0 + sq + sq * sq / 3.0) * e;
-                g[0] += W * (amp * Mij);
-                const double f = W * amp * (5.0 / 3.0) * (sq + 1.0) * e;
-#pragma unroll
-                for (int c = 0; c < DP; ++c)
-                    if (c < d) {
-                        const double t = xi[c] - xj[c];
-                        g[1 + c] += f * (t * t);
-                    }
-                if (i == j) g[DP + 1] += W * noise;
-            }
-        }
-    }
+    if (p.acc[1] == 0.0) pair_rows<DP>(p, n, d, np, amp, noise, gw, nw, lane, g);
 #pragma unroll
     for (int c = 0; c < DP + 2; ++c) {
         const double v = wave_sum_bcast(g[c]);
@@ -1169,37 +1191,7 @@ __global__ __launch_bounds__(256) void sw_pairs_final_kernel(LmlGroup grp) {
     double g[DP + 2];
 #pragma unroll
     for (int c = 0; c < DP + 2; ++c) g[c] = 0.0;
-    if (!failed) {
-        for (int i = gw; i < n; i += nw) {
-            const double ai = p.alpha[i];
-            double xi[DP];
-#pragma unroll
-            for (int c = 0; c < DP; ++c) xi[c] = c < d ? p.xs[i * d + c] : 0.0;
-            for (int j = lane; j <= i; j += 64) {
-                const double W = (ai * p.alpha[j] + p.A[(long long)i * np + j]) * (i == j ? 1.0 : 2.0);
-                const double* xj = p.xs + j * d;
-                double r2 = 0.0;
-#pragma unroll
-                for (int c = 0; c < DP; ++c)
-                    if (c < d) {
-                        const double t = xi[c] - xj[c];
-                        r2 += t * t;
-                    }
-                const double sq = sqrt(5.0 * r2);
-                const double e = exp(-sq);
-                const double Mij = i == j ? 1.0 : (1.0 + sq + sq * sq / 3.0) * e;
-                g[0] += W * (amp * Mij);
-                const double f = W * amp * (5.0 / 3.0) * (sq + 1.0) * e;
-#pragma unroll
-                for (int c = 0; c < DP; ++c)
-                    if (c < d) {
-                        const double t = xi[c] - xj[c];
-                        g[1 + c] += f * (t * t);
-                    }
-                if (i == j) g[DP + 1] += W * noise;
-            }
-        }
-    }
+    if (!failed) pair_rows<DP>(p, n, d, np, amp, noise, gw, nw, lane, g);
 #pragma unroll
     for (int c = 0; c < DP + 2; ++c) {
         const double v = wave_sum_bcast(g[c]);
