@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import argparse
 import collections
+import gc
 import math
 import json
 import os
@@ -447,33 +448,38 @@ def cpu_baseline_train(trials, n_sample=32, concurrent=4):
                       f"extrapolated to 24000 train steps + 6000 validation batches per trial ({wall:.1f} s)"}
 
 
-def shard_step_ratio(eng, members, folds, x, yl, otr, torch, dev, gpus=8, steps=10):
+def _timed_train_steps(e, x, yl, order, torch, dev, steps=10):
+    """ms per train step of engine ``e`` (2 untimed steps first)."""
+    for s_ in range(2):
+        e.train_step(x, yl, order, s_ * e.batch)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for s_ in range(steps):
+        e.train_step(x, yl, order, (s_ + 2) * e.batch)
+    torch.cuda.synchronize(dev)
+    return (time.perf_counter() - t0) / steps * 1e3
+
+
+def shard_step_ratio(full_ms, members, folds, x, yl, otr, torch, dev, gpus=8, steps=10, batch=100):
     """ms per train step of one GPU's LPT share (by FLOPs, as DistributedEvaluator
     deals (trial, fold) units) of this population over ``gpus`` GPUs, against the
-    whole population's, same process: how much of a population's training one of
-    ``gpus`` GPUs still pays (small populations run at a higher per-member cost)."""
+    whole population's ``full_ms``: how much of a population's training one of
+    ``gpus`` GPUs still pays (small populations run at a higher per-member cost).
+    The caller has dropped the whole population's engine first, as a rank of the
+    8-GPU search holds only its own share: with the 320-member engine's buffers
+    still resident the share measured 6.53 instead of 5.69 ms
+    (scripts/shard_ratio_probe.py, profiles/r05/shard_ratio_probe.log)."""
     from mpi_opt_amd.blocks import lpt_assign
     from mpi_opt_amd.population import PopulationEngine
 
     owner = lpt_assign([m.flops_per_sample_train() for m in members], gpus)
     mine = [i for i, o in enumerate(owner) if o == 0]
-    sub = PopulationEngine([members[i] for i in mine], batch=eng.batch, device=dev)
+    sub = PopulationEngine([members[i] for i in mine], batch=batch, device=dev)
     osub = otr[mine].contiguous()
-
-    def timed(e, order):
-        for s_ in range(2):
-            e.train_step(x, yl, order, s_ * e.batch)
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for s_ in range(steps):
-            e.train_step(x, yl, order, (s_ + 2) * e.batch)
-        torch.cuda.synchronize(dev)
-        return (time.perf_counter() - t0) / steps * 1e3
-
-    full_ms, shard_ms = timed(eng, otr), timed(sub, osub)
+    shard_ms = _timed_train_steps(sub, x, yl, osub, torch, dev, steps)
     del sub
     return {"gpus": gpus, "members": len(mine), "shard_ms_per_step": shard_ms, "full_ms_per_step": full_ms,
-            "factor": shard_ms / full_ms}
+            "factor": shard_ms / full_ms, "note": "share timed alone (the whole population's engine freed first)"}
 
 
 def bench_train(args, torch, dist, ws, rank, dev):
@@ -544,7 +550,14 @@ def bench_train(args, torch, dist, ws, rank, dev):
             by_kernel[k] += v
     algo_bytes = sum(by_kernel.values())
     pmc = (args.pmc or {}).get("train") if n_trials == 64 else None
-    shard = shard_step_ratio(eng, members, folds, x, yl, otr, torch, dev) if (n_trials == 64 and ws == 1) else None
+    shard = None
+    if n_trials == 64 and ws == 1:
+        full_ms = _timed_train_steps(eng, x, yl, otr, torch, dev)
+        eng = None   # a rank of the 8-GPU search holds only its share: time it with the whole population freed
+        gc.collect()
+        torch.cuda.synchronize(dev)
+        torch.cuda.empty_cache()
+        shard = shard_step_ratio(full_ms, members, folds, x, yl, otr, torch, dev, batch=B)
     if pmc and pmc.get("per_family_hbm_bytes"):
         fam = pmc["per_family_hbm_bytes"]
         pmc["per_family_vs_model"] = {k: {"measured": fam.get(k, 0.0), "model": v,

@@ -17,9 +17,14 @@ from mpi_opt_amd.population import PopulationEngine, TrialSpec, kfold_split, syn
 from scripts.train_probe import sample_trials  # noqa: E402
 
 
-def members_of(trials, folds, shard):
+def members_of(trials, folds, shard, bench_set=False):
     members, fl = [], []
-    for t in sample_trials(trials):
+    if bench_set:   # bench.py's own draw (lr and dropout drawn between the shapes): its train leg's population
+        from bench import sample_trials as bench_sample_trials
+        drawn = bench_sample_trials(trials, seed=13579)
+    else:
+        drawn = sample_trials(trials)
+    for t in drawn:
         for f in range(folds):
             members.append(TrialSpec(t.nb_filters, t.kernel_size, t.pool_size, t.dense, t.lr, t.dropout,
                                      seed=len(members)))
@@ -50,6 +55,7 @@ def main():
     ap.add_argument("--shard", default="0/8")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--labels-ab", action="store_true")
+    ap.add_argument("--bench-set", action="store_true", help="bench.py's train-leg trials instead of train_probe's")
     args = ap.parse_args()
     if args.labels_ab:
         members, fl = members_of(args.trials, args.folds, None)
@@ -64,7 +70,7 @@ def main():
                   "loss", float(eng.loss.mean()), flush=True)
             del eng
         return
-    members, fl = members_of(args.trials, args.folds, args.shard)
+    members, fl = members_of(args.trials, args.folds, args.shard, args.bench_set)
     x, y = synthetic_mnist(60000, seed=0)
     order = torch.from_numpy(np.stack([kfold_split(60000, args.folds, f)[0] for f in fl])).cuda()
     eng = PopulationEngine(members, batch=100)
