@@ -30,6 +30,10 @@ def main():
     osub = otr[mine].contiguous()
     order = os.environ.get("ORDER", "full_first")
     if order == "sub_only":
+        ballast = None
+        if os.environ.get("BALLAST_GB"):   # untouched device memory held beside the share
+            ballast = torch.empty(int(float(os.environ["BALLAST_GB"]) * 2**30), dtype=torch.uint8, device=dev)
+            print(f"ballast {ballast.numel() / 2**30:.0f} GB", flush=True)
         sub = PopulationEngine([members[i] for i in mine], batch=100, device=dev)
         full = None
     elif order == "sub_first":
@@ -52,13 +56,20 @@ def main():
         torch.cuda.synchronize(dev)
         return (time.perf_counter() - t0) / steps * 1e3
 
-    print(f"engines created: {order}", flush=True)
+    print(f"engines created: {order}; device memory allocated {torch.cuda.memory_allocated(dev) / 2**30:.1f} GB",
+          flush=True)
     if order == "full_then_free":   # time the whole population, free it, then time the share alone
         f0 = timed(full, otr)
         del full
         torch.cuda.synchronize(dev)
-        torch.cuda.empty_cache()
+        if not os.environ.get("KEEP_CACHE"):   # KEEP_CACHE=1: the share reuses the freed engine's cached blocks
+            torch.cuda.empty_cache()
         sub = PopulationEngine([members[i] for i in mine], batch=100, device=dev)
+        for name in ("params", "grads", "act", "adam_m", "adam_v", "tables"):
+            t = getattr(sub, name, None)
+            if torch.is_tensor(t):
+                print(f"  {name}: {t.numel() * t.element_size() / 2**20:.1f} MiB at 0x{t.data_ptr():x} "
+                      f"(mod 2 MiB 0x{t.data_ptr() % (2 << 20):x})", flush=True)
         s0 = timed(sub, osub, 30)
         print(f"full, freed, then share: {s0:.2f} / {f0:.2f} ms = {s0 / f0:.4f}", flush=True)
         return
