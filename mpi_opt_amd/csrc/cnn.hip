@@ -1601,6 +1601,7 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         if (i == 0) P.conv_mt = plan_knob("conv_mt", 4) == 2 ? 2 : 4;
         if (i == 0) P.side.enabled = plan_knob("streams", 3) >= 2;
         if (i == 0) P.side2.enabled = plan_knob("streams", 3) >= 3;
+        if (i == 0) P.side2.slot = 1;
         const int mcap = P.conv_mt * 64;   // 4 waves x conv_mt m-tiles of 16 pixels
         const int R1 = choose_rows(m.H1, [&](int R) { return conv_lds_bytes(R + k - 1, kImg, 1, m.H1, k * k, nt); }, kc1, kc2, mcap);
         const int R2 = choose_rows(m.H2, [&](int R) { return conv_lds_bytes(R + k - 1, m.H1, F, m.H2, k * k * F, nt); }, kc1, kc2, mcap);
