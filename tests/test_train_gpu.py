@@ -248,3 +248,26 @@ def test_side_stream_schedule_is_bit_identical(monkeypatch):
     for k in (1, 2):
         np.testing.assert_array_equal(out[0][0], out[k][0])
         np.testing.assert_array_equal(out[0][1], out[k][1])
+
+
+def test_engines_sharing_side_streams_are_bit_identical():
+    """Population engines of one process share the pooled side streams
+    (mpo::pooled_side_stream): two engines alive and stepped alternately give the
+    bits of one engine stepped alone."""
+    x, y = dataset(6)
+    xd, yd = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    tr, _ = orders(MEMBERS, x)
+    otr = torch.from_numpy(tr).cuda()
+    alone, _, _ = make_engine()
+    ref = [alone.train_step(xd, yd, otr, st * BATCH).cpu().numpy().copy() for st in range(3)]
+    ref_p = alone.params.cpu().numpy().copy()
+    del alone
+    a, _, _ = make_engine()
+    b, _, _ = make_engine()
+    for st in range(3):
+        la = a.train_step(xd, yd, otr, st * BATCH).cpu().numpy()
+        lb = b.train_step(xd, yd, otr, st * BATCH).cpu().numpy()
+        np.testing.assert_array_equal(la, ref[st])
+        np.testing.assert_array_equal(lb, ref[st])
+    np.testing.assert_array_equal(a.params.cpu().numpy(), ref_p)
+    np.testing.assert_array_equal(b.params.cpu().numpy(), ref_p)
