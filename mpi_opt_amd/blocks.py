@@ -387,39 +387,105 @@ def merge_topk(parts, k):
     return vals[order], idx[order]
 
 
+KIND_EXIT, KIND_TRAIN, KIND_CHAINS, KIND_SCORE = 0, 1, 2, 3
+ACQ_ORDER = ("EI", "LCB", "PI")
+STATS_SCALARS = ("refits", "n_sum", "n_max", "refit_s", "propose_s", "prepare_s", "score_s", "polish_s")
+
+
+def encode_histories(res):
+    """{(trial, fold): history or None} -> f64 rows [t, f, n_vl, n_va, dropped_train,
+    dropped_val, E, val_loss (E), val_acc (E)] (-1: absent)."""
+    keys = sorted(res)
+    E = 0
+    for k in keys:
+        h = res[k]
+        if h is not None:
+            extra = set(h) - {"val_loss", "val_acc", "dropped_train_samples", "dropped_val_samples"}
+            if extra:
+                raise TypeError(f"encode_histories: unsupported history keys {sorted(extra)}")
+            E = max(E, len(h.get("val_loss", [])), len(h.get("val_acc", [])))
+    rows = np.full((len(keys), 7 + 2 * E), np.nan)
+    for r, (t, f) in enumerate(keys):
+        h = res[(t, f)]
+        rows[r, :7] = [t, f, -1, -1, -1, -1, E]
+        if h is None:
+            continue
+        vl, va = list(h.get("val_loss", [])), list(h.get("val_acc", []))
+        rows[r, 2], rows[r, 3] = len(vl), len(va)
+        rows[r, 4] = h.get("dropped_train_samples", -1)
+        rows[r, 5] = h.get("dropped_val_samples", -1)
+        rows[r, 7:7 + len(vl)] = vl
+        rows[r, 7 + E:7 + E + len(va)] = va
+    return rows
+
+
+def decode_histories(parts):
+    out = {}
+    for rows in parts:
+        for row in rows:
+            t, f, nvl, nva, dtr, dva, E = (int(v) for v in row[:7])
+            if nvl < 0:
+                out[(t, f)] = None
+                continue
+            h = {"val_loss": [float(v) for v in row[7:7 + nvl]], "val_acc": [float(v) for v in row[7 + E:7 + E + nva]]}
+            if dtr >= 0:
+                h["dropped_train_samples"] = dtr
+            if dva >= 0:
+                h["dropped_val_samples"] = dva
+            out[(t, f)] = h
+    return out
+
+
 class DistributedEvaluator:
     """Shards work over torch.distributed ranks (one process per GPU); rank 0 drives.
 
-    Two kinds of rounds, announced by a broadcast from rank 0:
-    * ``("train", params)`` -- (trial, fold) units LPT-sharded by FLOPs, histories
+    Every round is fixed-layout tensor collectives (``collectives.TensorChannel``:
+    RCCL device tensors on ``nccl``, CPU tensors on gloo), announced by an int64
+    header broadcast from rank 0 (the reference's tag-4 parameter sends and tag-2
+    FOM receives, coordinator.py:140-150):
+    * train -- the n x D suggestion table (values, type codes, trial ids)
+      broadcast; (trial, fold) units LPT-sharded by FLOPs; per-unit history rows
       all-gathered (SURVEY §8e);
-    * ``("score", request)`` -- the acquisition's candidates split M/W per rank,
-      each rank's (value, index) top-k all-gathered and merged lowest-index-first
-      (SURVEY §8e "EI"), used by :class:`ShardedScorer`.
+    * chains -- the population's ask batches (``ChainJob.encode`` tables)
+      broadcast, LPT-dealt by refit cost, each rank's batches (point tables),
+      refit accounts and error text all-gathered;
+    * score -- the fitted GP (observations, theta, y_opt, xi, kappa) broadcast,
+      the candidates scattered M/W per rank, each rank's (value, index) top-k
+      all-gathered and merged lowest-index-first (SURVEY §8e "EI"), used by
+      :class:`ShardedScorer`.
+    The only object broadcast is the optimizer configuration of the ask batches,
+    once per search (and again only if it changes) -- never per round.
     """
 
     def __init__(self, local, group=None, chain_runner=None):
         import torch.distributed as dist
+
+        from .collectives import TensorChannel
 
         self.local = local
         self.dist = dist
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
+        self.ch = TensorChannel(dist, group)
         self.n_evaluated = 0
         self.chain_runner = chain_runner    # this rank's chains.ThreadChainExecutor (set by DistributedChainExecutor)
+        self._job_config = None             # the ask batches' optimizer configuration (sent once)
+        self.config_broadcasts = 0
 
-    def _announce(self, msg):
-        box = [msg]
-        self.dist.broadcast_object_list(box, src=0, group=self.group)
-        return box[0]
+    # ---- train ------------------------------------------------------------------
+    def _train(self, n, d, has_ids, params_list=None, trial_ids=None):
+        from .collectives import decode_points, encode_points
 
-    def _gather(self, obj):
-        out = [None] * self.world
-        self.dist.all_gather_object(out, obj, group=self.group)
-        return out
-
-    def _train(self, params_list, trial_ids=None):
+        table = None
+        if self.rank == 0:
+            vals, codes = encode_points(params_list) if n else (np.zeros((0, d)), np.zeros((0, d)))
+            ids = np.asarray(trial_ids if has_ids else np.zeros(n), dtype=np.float64).reshape(n, 1)
+            table = np.concatenate([vals.reshape(n, d), codes.reshape(n, d), ids], axis=1)
+        t = self.ch.bcast(table, (n, 2 * d + 1))
+        if self.rank != 0:
+            params_list = decode_points(t[:, :d], t[:, d:2 * d])
+            trial_ids = [int(v) for v in t[:, 2 * d]] if has_ids else None
         units = self.local.units(params_list)
         owner = lpt_assign([u[3] for u in units], self.world)
         mine = [u for u, o in zip(units, owner) if o == self.rank]
@@ -428,22 +494,68 @@ class DistributedEvaluator:
         else:
             res = self.local.train_units(mine, seed_base=self.n_evaluated, trial_ids=trial_ids)
         self.n_evaluated += len(params_list)
-        merged = {}
-        for g in self._gather({k: v for k, v in res.items()}):
-            merged.update(g)
-        return merged
+        return decode_histories(self.ch.gather_rows(encode_histories(res)))
 
-    def _score(self, req):
-        m = len(req["cand"])
-        s0, s1 = self.rank * m // self.world, (self.rank + 1) * m // self.world
-        part = local_topk(req, s0, s1, device=self.local.device) if s1 > s0 else {}
-        parts = self._gather(part)
-        return {a: merge_topk([p[a] for p in parts if a in p], int(req["k"])) for a in req["acqs"]}
+    # ---- score ------------------------------------------------------------------
+    def _score(self, m, d, n, k, mask, dm, req=None):
+        acqs = [a for i, a in enumerate(ACQ_ORDER) if mask >> i & 1]
+        head = None
+        if self.rank == 0:
+            head = [float(req.get("y_opt", 0.0)), float(req.get("xi", 0.01)), float(req.get("kappa", 1.96))]
+            if dm:
+                head += [float(req["amp"]), float(req["noise"])] + list(np.ravel(req["ls"]).astype(float)) + \
+                    list(np.ravel(req["Xt"]).astype(float)) + list(np.ravel(req["y"]).astype(float))
+        g = self.ch.bcast(head, (3 + (2 + dm + n * dm + n if dm else 0),))
+        cand, s0, s1 = self.ch.scatter_rows(req["cand"] if self.rank == 0 else None, m, d)
+        payload = {"y_opt": float(g[0]), "xi": float(g[1]), "kappa": float(g[2]), "acqs": acqs, "k": int(k),
+                   "cand": cand}
+        if dm:
+            payload.update(amp=float(g[3]), noise=float(g[4]), ls=np.array(g[5:5 + dm]),
+                           Xt=np.array(g[5 + dm:5 + dm + n * dm]).reshape(n, dm),
+                           y=np.array(g[5 + dm + n * dm:5 + dm + n * dm + n]))
+        part = local_topk(payload, 0, s1 - s0, device=self.local.device) if s1 > s0 else {}
+        rows = np.full((len(acqs), 2 * k), np.nan)
+        for r, a in enumerate(acqs):
+            rows[r, k:] = -1.0
+            if a in part:
+                v, i = part[a]
+                rows[r, :len(v)] = v
+                rows[r, k:k + len(i)] = np.asarray(i, dtype=np.float64) + s0
+        out = {}
+        parts = self.ch.gather_rows(rows)
+        for r, a in enumerate(acqs):
+            lists = []
+            for pr in parts:
+                if len(pr):
+                    idx = pr[r, k:].astype(np.int64)
+                    keep = idx >= 0
+                    lists.append((pr[r, :k][keep], idx[keep]))
+            out[a] = merge_topk(lists, int(k))
+        return out
 
-    def _chains(self, jobs):
+    # ---- chains -----------------------------------------------------------------
+    def _chains(self, J, cfg_new, blob_len, jobs=None, enc=None):
         """Every rank runs its LPT share of the ask batches; all ranks get all batches."""
         from . import optimizer as O
+        from .collectives import decode_points, encode_points
 
+        if cfg_new:
+            box = [jobs[0].config if self.rank == 0 else None]
+            self.dist.broadcast_object_list(box, src=0, group=self.group)   # setup, once per search
+            self._job_config = box[0]
+            self.config_broadcasts += 1
+        meta = blob = None
+        if self.rank == 0:
+            meta = np.stack([e[0] for e in enc]) if enc else np.zeros((0, O.ChainJob.META), dtype=np.int64)
+            blob = np.concatenate([e[1] for e in enc]) if enc else np.zeros(0)
+        meta = self.ch.bcast(meta, (J, O.ChainJob.META), dtype=np.int64)
+        blob = self.ch.bcast(blob, (blob_len,))
+        if self.rank != 0:
+            jobs, o = [], 0
+            for row in meta:
+                ln = int(row[-1])
+                jobs.append(O.ChainJob.decode(row, blob[o:o + ln], self._job_config))
+                o += ln
         owner = lpt_assign([j.cost for j in jobs], self.world)
         mine = [i for i, o in enumerate(owner) if o == self.rank]
         if self.chain_runner is None:
@@ -453,36 +565,61 @@ class DistributedEvaluator:
         # a failure on one rank is gathered like a result and raised on every rank,
         # so no rank is left blocked in the all-gather
         try:
-            res, err = (self.chain_runner.run_now([jobs[i] for i in mine]) if mine else []), None
+            res, err = (self.chain_runner.run_now([jobs[i] for i in mine]) if mine else []), ""
         except Exception as e:  # noqa: BLE001 -- re-raised below on every rank
             res, err = [], f"rank {self.rank}: {type(e).__name__}: {e}"
-        stats = dict(O.STATS) if self.rank != 0 else None
+        # batches: rows [job index, n points, D, values, codes]
+        enc = []
+        for i, (X, trace) in zip(mine, res):
+            if trace is not None:
+                raise NotImplementedError("refit traces (parity tests) do not cross ranks")
+            v, c = encode_points([list(x) for x in X])
+            enc.append(np.concatenate([[i, v.shape[0], v.shape[1] if v.size else 0], v.ravel(), c.ravel()]))
+        width = max([len(e) for e in enc], default=3)
+        rows = np.zeros((len(enc), width))
+        for r, e in enumerate(enc):
+            rows[r, :len(e)] = e
+        st = O.STATS
+        srow = np.array([[*(float(st[k_]) for k_ in STATS_SCALARS), float(len(st["samples"])),
+                          *np.ravel(np.asarray(st["samples"], dtype=np.float64))]]) if self.rank != 0 else \
+            np.zeros((0, 0))
         merged = [None] * len(jobs)
-        errors = []
-        for part, st, e in self._gather(({i: r for i, r in zip(mine, res)}, stats, err)):
-            if e is not None:
-                errors.append(e)
-            for i, r in part.items():
-                merged[i] = r
-            if st is not None and self.rank == 0:
-                O.merge_stats(st)
+        for part in self.ch.gather_rows(rows):
+            for row in part:
+                i, npts, dd = int(row[0]), int(row[1]), int(row[2])
+                v = row[3:3 + npts * dd].reshape(npts, dd)
+                c = row[3 + npts * dd:3 + 2 * npts * dd].reshape(npts, dd)
+                merged[i] = (decode_points(v, c), None)
+        for r, part in enumerate(self.ch.gather_rows(srow)):
+            if r == 0 or self.rank != 0 or not len(part):
+                continue
+            row = part[0]
+            ns = int(row[len(STATS_SCALARS)])
+            d_ = {k_: row[j] for j, k_ in enumerate(STATS_SCALARS)}
+            for k_ in ("refits", "n_sum", "n_max"):
+                d_[k_] = int(d_[k_])
+            smp = row[len(STATS_SCALARS) + 1:len(STATS_SCALARS) + 1 + 2 * ns].reshape(ns, 2)
+            d_["samples"] = [(int(a), float(b)) for a, b in smp]
+            O.merge_stats(d_)
+        errors = [e for e in self.ch.gather_text(err) if e]
         if errors:
             raise RuntimeError("ask batches failed: " + "; ".join(errors))
         return merged
 
+    # ---- the round loop ------------------------------------------------------
     def _serve_one(self):
-        msg = self._announce(None)
-        if msg is None:
+        h = self.ch.header()
+        kind = h[0]
+        if kind == KIND_EXIT:
             return False
-        kind, body = msg
-        if kind == "train":
-            self._train(*body)
-        elif kind == "chains":
-            self._chains(body)
-        elif kind == "score":
-            self._score(body)
+        if kind == KIND_TRAIN:
+            self._train(h[1], h[2], h[3])
+        elif kind == KIND_CHAINS:
+            self._chains(h[1], h[2], h[3])
+        elif kind == KIND_SCORE:
+            self._score(*h[1:7])
         else:
-            raise ValueError(f"unknown round {kind!r}")
+            raise ValueError(f"unknown round {kind}")
         return True
 
     accepts_trial_ids = True
@@ -491,27 +628,45 @@ class DistributedEvaluator:
         """Rank 0: evaluate a batch over all ranks."""
         params_list = [list(p) for p in params_list]
         ids = None if trial_ids is None else [int(i) for i in trial_ids]
-        self._announce(("train", (params_list, ids)))
-        return self.local.foms(params_list, self._train(params_list, ids))
+        n, d = len(params_list), (len(params_list[0]) if params_list else 0)
+        self.ch.header([KIND_TRAIN, n, d, int(ids is not None)])
+        return self.local.foms(params_list, self._train(n, d, ids is not None, params_list, ids))
 
     def chains(self, jobs):
         """Rank 0: run ask batches (optimizer.ChainJob) over all ranks -> [(X, trace)]."""
-        self._announce(("chains", list(jobs)))
-        return self._chains(list(jobs))
+        jobs = list(jobs)
+        cfg_new = bool(jobs) and (self._job_config is None or jobs[0].config != self._job_config)
+        for j in jobs[1:]:
+            if j.config != jobs[0].config:
+                raise ValueError("chains: the batches of one round must share one optimizer configuration")
+        enc = [j.encode() for j in jobs]
+        blob_len = int(sum(len(b) for _, b in enc))
+        self.ch.header([KIND_CHAINS, len(jobs), int(cfg_new), blob_len])
+        return self._chains(len(jobs), cfg_new, blob_len, jobs, enc)
 
     def score(self, req):
         """Rank 0: a sharded acquisition request -> {acq: (values, indices)} top-k."""
-        self._announce(("score", req))
-        return self._score(req)
+        acqs = list(req["acqs"])
+        bad = [a for a in acqs if a not in ACQ_ORDER]
+        if bad:
+            raise ValueError(f"score: unknown acquisitions {bad}")
+        mask = sum(1 << ACQ_ORDER.index(a) for a in acqs)
+        cand = np.asarray(req["cand"], dtype=np.float64)
+        m, d = cand.shape
+        dm = int(np.asarray(req["Xt"]).shape[1]) if "Xt" in req else 0
+        n = int(np.asarray(req["Xt"]).shape[0]) if "Xt" in req else 0
+        self.ch.header([KIND_SCORE, m, d, n, int(req["k"]), mask, dm])
+        got = self._score(m, d, n, int(req["k"]), mask, dm, req)
+        return {a: got[a] for a in acqs}
 
     def serve(self):
-        """Ranks > 0: serve rounds until rank 0 sends None."""
+        """Ranks > 0: serve rounds until rank 0 sends the exit header."""
         while self._serve_one():
             pass
 
     def shutdown(self):
         if self.rank == 0:
-            self._announce(None)
+            self.ch.header([KIND_EXIT])
 
 
 class ShardedScorer:

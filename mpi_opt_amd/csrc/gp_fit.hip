@@ -592,6 +592,9 @@ struct LmlGroup {
     int d, count, stop, pad_;
     LmlTheta th[kMaxGroup];
 };
+// passed by value: the whole table must fit the 4 KiB kernel-argument segment (with the
+// launches' other arguments); raising kMaxGroup or growing LmlTheta must keep this
+static_assert(sizeof(LmlGroup) + 64 <= 4096, "LmlGroup exceeds the kernel-argument segment");
 
 __device__ __forceinline__ SsPtrs ss_ptrs_t(const LmlTheta& t, int d) {
     auto al = [](long long x) { return (x + 31) & ~31LL; };

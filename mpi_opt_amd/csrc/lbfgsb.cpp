@@ -26,6 +26,35 @@
 // rather than updated incrementally; in exact arithmetic that is the same
 // matrix, so iterates agree with scipy's to rounding (tests/test_lbfgsb.py
 // compares them on the GP objective and on bound-constrained test functions).
+//
+// Provenance and licence.  The routines below are a C++ translation of two
+// BSD-licensed Fortran packages, following their structure and variable names:
+//   * L-BFGS-B 3.0 (cauchy, subsm, formk/bmv, the heap sort of the breakpoints,
+//     and the LINPACK dpofa / dtrsl factor-and-solve it calls), distributed under
+//     the "New BSD License":
+//       Copyright (c) 2011 Ciyou Zhu, Richard Byrd, Jorge Nocedal and Jose Luis
+//       Morales.  All rights reserved.
+//   * the line search dcsrch / dcstep (Jorge J. More and David J. Thuente,
+//     MINPACK-1 Project, Argonne National Laboratory; MINPACK-2 Project,
+//     Argonne National Laboratory and University of Minnesota: Brett M.
+//     Averick, Richard G. Carter and Jorge J. More), shipped inside the
+//     L-BFGS-B 3.0 distribution and covered by the notice below.
+//   Redistribution and use in source and binary forms, with or without
+//   modification, are permitted provided that the following conditions are met:
+//   (1) redistributions of source code must retain the above copyright notice,
+//   this list of conditions and the following disclaimer; (2) redistributions in
+//   binary form must reproduce the above copyright notice, this list of
+//   conditions and the following disclaimer in the documentation and/or other
+//   materials provided with the distribution; (3) neither the name of the
+//   copyright holders nor the names of its contributors may be used to endorse
+//   or promote products derived from this software without specific prior
+//   written permission.  THIS SOFTWARE IS PROVIDED BY THE COPYRIGHT HOLDERS AND
+//   CONTRIBUTORS "AS IS" AND ANY EXPRESS OR IMPLIED WARRANTIES, INCLUDING, BUT
+//   NOT LIMITED TO, THE IMPLIED WARRANTIES OF MERCHANTABILITY AND FITNESS FOR A
+//   PARTICULAR PURPOSE ARE DISCLAIMED.  IN NO EVENT SHALL THE COPYRIGHT HOLDERS
+//   OR CONTRIBUTORS BE LIABLE FOR ANY DIRECT, INDIRECT, INCIDENTAL, SPECIAL,
+//   EXEMPLARY, OR CONSEQUENTIAL DAMAGES ARISING IN ANY WAY OUT OF THE USE OF
+//   THIS SOFTWARE, EVEN IF ADVISED OF THE POSSIBILITY OF SUCH DAMAGE.
 #pragma clang fp contract(off)
 // max / min of doubles are fmax / fmin throughout: a NaN operand yields the other one, as
 // the scipy build's L-BFGS-B does -- an infinite objective value (sklearn's LinAlgError
@@ -1122,6 +1151,7 @@ struct LmlBatcher {
                 rs.reserve(mine.size());
                 std::vector<bool> used(mine.size(), false);
                 int rc = MPO_OK;
+                long long sets = 0;
                 for (size_t i = 0; i < mine.size() && rc == MPO_OK; ++i) {
                     if (used[i]) continue;
                     rs.clear();
@@ -1131,6 +1161,7 @@ struct LmlBatcher {
                             used[j] = true;
                         }
                     rc = mpo::lml_launch_rounds(rs.data(), (int)rs.size(), s);
+                    ++sets;   // one launch set per distinct d
                 }
                 if (rc == MPO_OK) {
                     const hipError_t e = hipStreamSynchronize(s);
@@ -1142,7 +1173,7 @@ struct LmlBatcher {
                 const std::string err = rc != MPO_OK ? std::string(mpo_last_error()) : std::string();
                 lk.lock();
                 inflight -= (int)mine.size();
-                ++launches;
+                launches += sets;
                 rounds += (long long)mine.size();
                 for (Req* m : mine) {
                     m->rc = rc;

@@ -7,6 +7,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <map>
+#include <tuple>
 #include <mutex>
 #include <string>
 #include <utility>
@@ -64,18 +65,22 @@ struct StreamDeviceScope {
 // re-created if the caller moves to another device).  get() returns nullptr when
 // disabled or when the stream / events cannot be created (the step then runs
 // serially on the caller's stream).
-// The side streams themselves come from one process-wide pool per (device, slot):
-// every population engine of a process shares them, so a process that holds several
-// engines (a search: one per population, DenseNet and MNIST) keeps the same few
-// streams -- with one pair of streams per engine, a 40-member engine stepped 15%
-// slower while a second, idle engine was alive (6.53 vs 5.69 ms; 5.69 with pooled
-// streams: profiles/r05/shard_ratio_probe.log).  The fork / join events stay per
-// engine; a join waits for all work queued on the shared stream so far.
-inline hipStream_t pooled_side_stream(int dev, int slot) {
+// The side streams themselves come from one process-wide pool per (device, caller
+// stream, slot): every population engine stepped from the same caller stream shares
+// them, so a process that holds several engines (a search: one per population,
+// DenseNet and MNIST) keeps the same few streams -- with one pair of streams per
+// engine, a 40-member engine stepped 15% slower while a second, idle engine was alive
+// (6.53 vs 5.69 ms; 5.69 with pooled streams: profiles/r05/shard_ratio_probe.log).
+// Engines stepped from DISTINCT caller streams get distinct side streams (r06), so a
+// join never waits for another caller's work: the ABI's "thread-safe across streams"
+// contract holds for them (tests/test_train_gpu.py::
+// test_engines_on_two_threads_and_streams_keep_their_bits).  Engines sharing a caller
+// stream are serialised by that stream anyway.  The fork / join events stay per engine.
+inline hipStream_t pooled_side_stream(int dev, hipStream_t caller, int slot) {
     static std::mutex mu;
-    static std::map<std::pair<int, int>, hipStream_t> pool;
+    static std::map<std::tuple<int, hipStream_t, int>, hipStream_t> pool;
     std::lock_guard<std::mutex> lk(mu);
-    auto it = pool.find({dev, slot});
+    auto it = pool.find({dev, caller, slot});
     if (it != pool.end()) return it->second;
     int cur = 0;
     (void)hipGetDevice(&cur);
@@ -84,7 +89,7 @@ inline hipStream_t pooled_side_stream(int dev, int slot) {
     const bool ok = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
     (void)hipSetDevice(cur);
     if (!ok) { (void)hipGetLastError(); return nullptr; }
-    pool[{dev, slot}] = st;   // lives for the process
+    pool[{dev, caller, slot}] = st;   // lives for the process
     return st;
 }
 
@@ -92,6 +97,7 @@ struct SideStream {
     bool enabled = true;
     int slot = 0;   // which pooled stream (0: the side stream, 1: a third stream)
     hipStream_t side = nullptr;
+    hipStream_t caller = nullptr;   // the caller stream `side` was pooled for
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int device = -1;
     SideStream() = default;
@@ -102,6 +108,7 @@ struct SideStream {
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         if (ev_join) (void)hipEventDestroy(ev_join);
         side = nullptr;   // pooled: not destroyed
+        caller = nullptr;
         ev_fork = ev_join = nullptr;
         device = -1;
     }
@@ -109,12 +116,19 @@ struct SideStream {
         if (!enabled) return nullptr;
         int dev = 0;
         if (hipStreamGetDevice(s, &dev) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
-        if (side && dev == device) return side;
+        if (side && dev == device) {
+            if (s == caller) return side;
+            side = pooled_side_stream(dev, s, slot);   // same device, another caller stream
+            if (!side) { release(); enabled = false; return nullptr; }
+            caller = s;
+            return side;
+        }
         release();
         int cur = 0;
         (void)hipGetDevice(&cur);
         (void)hipSetDevice(dev);
-        side = pooled_side_stream(dev, slot);
+        side = pooled_side_stream(dev, s, slot);
+        caller = s;
         const bool ok = side && hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) == hipSuccess &&
                         hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) == hipSuccess;
         (void)hipSetDevice(cur);

@@ -103,12 +103,14 @@ class DeviceLML:
         h = self._out_np
         return -h[:B], -(h[B:B + B * (self.d + 2)].reshape(B, self.d + 2))
 
-    def fit(self, starts, bounds, ftol=None, gtol=1e-5, maxiter=15000, maxfun=15000):
+    def fit(self, starts, bounds, ftol=None, gtol=1e-5, maxiter=15000, maxfun=15000, batcher=True):
         """L-BFGS-B from every start on -LML, all in ``mpo_gp_fit_lml_host`` (the
         host L-BFGS-B of csrc/lbfgsb.cpp; one device round per iteration of all
         live runs; ctypes releases the GIL for the whole fit).  The rounds go
         through the device's batcher (``_lib.lml_batcher``): concurrent fits on
         this GPU (the cl_min chains) share launches, with unchanged results.
+        ``batcher=False`` runs every round on this fit's own stream instead (the
+        plain per-round path; the tests' baseline).
         Returns ([(theta, -lml)] per start, rounds)."""
         starts = np.ascontiguousarray(np.asarray(starts, dtype=np.float64))
         B, k = starts.shape
@@ -125,7 +127,7 @@ class DeviceLML:
             _lib.ptr(self.X), _lib.ptr(self.y), self.n, self.d, starts.ctypes.data, B, b.ctypes.data,
             ctypes.byref(opts), self.theta_h.data_ptr(), self.out_h.data_ptr(), _lib.ptr(self.io), self.io_bytes,
             _lib.ptr(self.ws), self.ws_bytes, x.ctypes.data, f.ctypes.data, stats.ctypes.data, ctypes.byref(rounds),
-            _lib.lml_batcher(self.X.device.index), self._stream)
+            _lib.lml_batcher(self.X.device.index) if batcher else None, self._stream)
         _lib.check(rc, "mpo_gp_fit_lml_host")
         self.last_stats = stats
         return [(x[r], float(f[r])) for r in range(B)], rounds.value

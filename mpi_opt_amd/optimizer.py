@@ -41,11 +41,18 @@ from .space import Space, check_random_state
 # --------------------------------------------------------------------------
 # GP hyper-parameter fit (device LML objective, sklearn's restart/L-BFGS-B loop)
 # --------------------------------------------------------------------------
+#: L-BFGS-B driver of the refits and the acquisition polish: "native" (csrc/lbfgsb.cpp,
+#: the default: GIL-free, iterates equal to scipy's to rounding) or "scipy" (scipy's own
+#: setulb driven from Python: the exact-parity mode, bit for bit scipy's iterates).
+DRIVER = "native"
+
+
 def fit_gp_hyperparameters(Xt, y, random_state=None, n_restarts_optimizer=2, device=None):
     """skopt's GP fit: sklearn GaussianProcessRegressor with the cook_estimator
     kernel + WhiteKernel, normalize_y, L-BFGS-B restarts -- the objective
     (LML + gradient) evaluated by ``mpo_gp_lml_grad``.  Returns (amp, length_scale, noise)."""
-    return fit_lml(Xt, y, random_state=random_state, n_restarts_optimizer=n_restarts_optimizer, device=device)
+    return fit_lml(Xt, y, random_state=random_state, n_restarts_optimizer=n_restarts_optimizer, device=device,
+                   driver=DRIVER)
 
 
 class GPModel:
@@ -164,6 +171,9 @@ def _record_refit(n, t_refit, t_prepare, t_score, t_polish, t_propose, t_total):
         STATS["samples"].append((n, t_total))      # (n, seconds of refit + proposal)
 
 
+STRATEGIES = ("cl_min", "cl_mean", "cl_max")
+
+
 class ChainJob:
     """Everything one ``ask(n_points, strategy)`` batch depends on: the optimizer's
     state when ``ask`` was called (its told points, gp_hedge gains, initial-point
@@ -192,6 +202,63 @@ class ChainJob:
         # over n/16 workgroups); one refit per lie once the initial points are spent
         n0 = len(self.yi)
         self.cost = float(sum((n0 + i + 1) ** 2 for i in range(self.n_points)))
+
+    # ---- fixed-layout form for the tensor collectives (blocks.DistributedEvaluator) ----
+    META = 10   # int64 words per job: n, D, has_gains, n_initial_points, seed, n_points, strategy, trace, n_init, blob
+
+    def encode(self):
+        """(meta int64 [META], blob f64): the job without its config (sent once per
+        search).  Points cross as (value, type code) pairs (collectives.encode_points)."""
+        from .collectives import encode_points
+
+        if not isinstance(self.seed, (int, np.integer)):
+            raise TypeError("ChainJob.encode: the copy's seed must be an int")
+        if self.trace:
+            raise NotImplementedError("ChainJob.encode: refit traces (parity tests) do not cross ranks")
+        n = len(self.yi)
+        xv, xc = encode_points(self.Xi) if n else (np.zeros((0, 0)), np.zeros((0, 0)))
+        d = xv.shape[1] if n else 0
+        parts = [xv.ravel(), xc.ravel(), np.asarray(self.yi, dtype=np.float64)]
+        if self.gains is not None:
+            parts.append(np.asarray(self.gains, dtype=np.float64).ravel())
+        n_init = -1
+        if self.initial_samples is not None:
+            iv, ic = encode_points([list(x) for x in self.initial_samples])
+            n_init = len(iv)
+            d = d or iv.shape[1]
+            parts += [iv.ravel(), ic.ravel()]
+        blob = np.concatenate(parts) if parts else np.zeros(0)
+        meta = np.array([n, d, -1 if self.gains is None else len(np.ravel(self.gains)), int(self.n_initial_points),
+                         int(self.seed), self.n_points, STRATEGIES.index(self.strategy), 0, n_init, len(blob)],
+                        dtype=np.int64)
+        return meta, blob
+
+    @classmethod
+    def decode(cls, meta, blob, config):
+        """Inverse of :meth:`encode` with the search's ``config``."""
+        from .collectives import decode_points
+
+        n, d, ng, nip, seed, npts, strat, _trace, n_init, _ = (int(v) for v in meta)
+        job = cls.__new__(cls)
+        o = 0
+        xv = blob[o:o + n * d].reshape(n, d); o += n * d
+        xc = blob[o:o + n * d].reshape(n, d); o += n * d
+        job.Xi = decode_points(xv, xc)
+        job.yi = [float(v) for v in blob[o:o + n]]; o += n
+        job.gains = None
+        if ng >= 0:
+            job.gains = np.array(blob[o:o + ng], dtype=np.float64); o += ng
+        job.initial_samples = None
+        if n_init >= 0:
+            iv = blob[o:o + n_init * d].reshape(n_init, d); o += n_init * d
+            ic = blob[o:o + n_init * d].reshape(n_init, d); o += n_init * d
+            job.initial_samples = decode_points(iv, ic)
+        job.config = config
+        job.n_initial_points = nip
+        job.seed = seed
+        job.n_points, job.strategy, job.trace = npts, STRATEGIES[strat], False
+        job.cost = float(sum((n + i + 1) ** 2 for i in range(npts)))
+        return job
 
     def copy_optimizer(self, device=None, scorer=None):
         """``Optimizer.copy(random_state=seed)`` of the asking optimizer, on ``device``."""
@@ -392,7 +459,7 @@ class Optimizer:
         if self.acq_optimizer == "lbfgs":
             runs = [(a, i) for a in self.cand_acq_funcs_ for i in top[a]]
             polished = polish_lockstep(est, [X[i] for _, i in runs], [a for a, _ in runs], y_opt, xi, kappa,
-                                       self.space.transformed_bounds)
+                                       self.space.transformed_bounds, driver=DRIVER)
             t_polish = time.perf_counter() - t4
         for acq in self.cand_acq_funcs_:
             idx = top[acq]

@@ -170,6 +170,17 @@ def _dist_worker(rank, world, port, tmp, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     O.Optimizer._fit_and_propose = fake_fit_and_propose
+    # count the pickled object collectives: the rounds must be tensor collectives only
+    # (the optimizer configuration is broadcast once per search)
+    calls = {"object": 0}
+    for name in ("broadcast_object_list", "all_gather_object", "gather_object", "scatter_object_list"):
+        orig = getattr(dist, name)
+
+        def counted(*a, _orig=orig, **k):
+            calls["object"] += 1
+            return _orig(*a, **k)
+
+        setattr(dist, name, counted)
     ev = DistributedEvaluator(_Local())
     ex = DistributedChainExecutor(ev, ThreadChainExecutor(device=None, workers=2))
     if rank == 0:
@@ -183,7 +194,8 @@ def _dist_worker(rank, world, port, tmp, q):
         ev.shutdown()
         q.put({"told": [list(map(float, p)) for p in st.param_list], "foms": list(st.fom_list),
                "trained": [list(map(float, p)) for p in comm.trained_params], "batches": list(comm.batches),
-               "refits": O.STATS["refits"], "rounds": ex.rounds})
+               "refits": O.STATS["refits"], "rounds": ex.rounds, "object_calls": calls["object"],
+               "config_broadcasts": ev.config_broadcasts})
     else:
         ev.serve()
     ex.close()
@@ -207,6 +219,9 @@ def test_chains_dealt_over_gloo_ranks_equal_sequential(fake_gp, tmp_path):
         assert p.exitcode == 0
     rounds = got.pop("rounds")
     assert rounds == len(want["batches"])       # one dispatch of buffered batches per population
+    # every round was tensor collectives: the one object broadcast is the search's
+    # optimizer configuration, sent with the first batch round
+    assert got.pop("config_broadcasts") == 1 and got.pop("object_calls") == 1
     for k in ("told", "foms", "trained", "batches", "refits"):
         assert got[k] == want[k], k
 
@@ -317,7 +332,8 @@ def _err_worker(rank, world, port, q):
     ev = DistributedEvaluator(_Local(), chain_runner=_FailingRunner(rank))
     try:
         if rank == 0:
-            ev.chains([_SlowJob() for _ in range(4)])
+            base = O.Optimizer(mnist_space(), random_state=0)
+            ev.chains([O.ChainJob(base, 100 + i, 1, "cl_min") for i in range(4)])
         else:
             ev.serve()
         q.put((rank, "no error"))

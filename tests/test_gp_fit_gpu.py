@@ -161,7 +161,9 @@ def test_concurrent_fits_share_launches_with_identical_results():
     """Refits on several threads at once (the cl_min chains) go through the
     device's batcher: rounds of different problems (n = 60 ... 201, d = 5 and 3:
     one launch set per d) launch together, and every fit's optima, values and
-    counts equal its lone run."""
+    counts equal its lone run on the plain per-round path (no batcher).  The
+    threads start together (barrier), and fewer launch sets than rounds shows
+    that rounds were actually grouped."""
     import threading
 
     from mpi_opt_amd.gp_fit import DeviceLML, normalize_targets, theta_bounds
@@ -173,16 +175,20 @@ def test_concurrent_fits_share_launches_with_identical_results():
         bounds.append(theta_bounds(d))
     rng = np.random.RandomState(0)
     starts = [np.array([np.zeros(len(b))] + [rng.uniform(b[:, 0], b[:, 1]) for _ in range(2)]) for b in bounds]
-    seq = [DeviceLML(X, yn, device="cuda:0").fit(st, b) for (X, yn), st, b in zip(probs, starts, bounds)]
+    seq = [DeviceLML(X, yn, device="cuda:0").fit(st, b, batcher=False)
+           for (X, yn), st, b in zip(probs, starts, bounds)]
     l0, r0 = _batcher_stats()
     out = [None] * len(probs)
     errors = []
+    go = threading.Barrier(len(probs))
 
     def run(i):
         try:
             torch.cuda.set_device(0)
             with torch.cuda.stream(torch.cuda.Stream()):
-                out[i] = DeviceLML(*probs[i], device="cuda:0").fit(starts[i], bounds[i])
+                lml = DeviceLML(*probs[i], device="cuda:0")
+                go.wait()
+                out[i] = lml.fit(starts[i], bounds[i])
         except BaseException as e:  # noqa: BLE001
             errors.append(e)
 
@@ -198,7 +204,7 @@ def test_concurrent_fits_share_launches_with_identical_results():
         assert ra == rc
         for (x1, f1), (x2, f2) in zip(a, c):
             assert np.array_equal(x1, x2) and f1 == f2
-    assert r1 - r0 == sum(r for _, r in seq) and l1 - l0 <= r1 - r0
+    assert r1 - r0 == sum(r for _, r in seq) and l1 - l0 < r1 - r0
 
 
 def test_fused_split_sweep_reports_failure():

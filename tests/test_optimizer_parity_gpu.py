@@ -31,6 +31,13 @@ pytestmark = pytest.mark.gpu
 REAL_TOL = 1e-6
 THETA_TOL = 1e-3
 GAINS_RTOL = 1e-4
+# n ~ 200 (the configs[3] search's refit sizes): the LML surface is flat enough that
+# sklearn's fit and the device fit stop up to 4e-4 apart in log theta (both inside
+# the solver's ftol; measured 3.9e-4 with the native driver, 3.6e-4 with scipy's own
+# setulb -- so not the driver), and the acquisition polish (maxiter=20) moves the
+# real dimension of a proposal with theta: measured 4.8e-4 with either driver, while
+# integer dimensions, every top-5 and every gp_hedge pick stay identical
+REAL_TOL_LARGE_N = 1e-3
 
 
 def f_mnist(x):
@@ -39,13 +46,13 @@ def f_mnist(x):
                  + (drop - 0.3) ** 2 + 0.05 * np.sin(nb * dense / 300.0))
 
 
-def _same_point(a, b, where):
+def _same_point(a, b, where, real_tol=REAL_TOL):
     assert len(a) == len(b), where
     for j, (u, v) in enumerate(zip(a, b)):
         if isinstance(v, (int, np.integer)):
             assert int(u) == int(v), f"{where}: dim {j}: {a} vs oracle {b}"
         else:
-            assert abs(float(u) - float(v)) <= REAL_TOL, f"{where}: dim {j}: {a} vs oracle {b}"
+            assert abs(float(u) - float(v)) <= real_tol, f"{where}: dim {j}: {a} vs oracle {b}"
 
 
 def _compare_traces(td, to, where):
@@ -89,3 +96,56 @@ def test_ask_tell_sequence_and_cl_min_batch_match_skopt_oracle():
           f"{max(worst['theta'], w2['theta']):.2e}, max gains rel diff = {max(worst['gains'], w2['gains']):.2e}")
     # the cache: a second ask(5) returns the same batch, a tell clears it
     assert opt.ask(5) is bd
+
+
+def _space_points(n, seed):
+    """n points of option3's mnist space from their own RandomState (not the
+    optimizers' stream): integer dims as ints, the dropout as a float."""
+    rng = np.random.RandomState(seed)
+    return [[int(rng.randint(10, 51)), int(rng.randint(2, 11)), int(rng.randint(2, 11)), int(rng.randint(50, 201)),
+             float(rng.uniform(0.0, 1.0))] for _ in range(n)]
+
+
+@pytest.mark.parametrize("driver", ["native", "scipy"])
+@pytest.mark.parametrize("n_told", [200])
+def test_ask_tell_at_search_sizes_match_skopt_oracle(n_told, driver, monkeypatch):
+    """G2 where the configs[3] search runs (refits at n = 64 ... 447, mean 223, DESIGN
+    §3.1c): both optimizers are told the same ``n_told`` points at once (one refit at
+    n = n_told), then three ask/tell rounds (n_told + 1 ... + 3), then the reference's
+    ``ask(5)`` cl_min batch (copy() refit + 4 lie refits past it).  With either
+    L-BFGS-B driver (``optimizer.DRIVER``: the native csrc/lbfgsb.cpp default, or
+    scipy's own setulb), every refit's fitted theta, candidate top-5 per acquisition,
+    gp_hedge pick and gains must match the oracle (sklearn's own fit + scipy polish)
+    with the tolerances above; proposals: integer dimensions exact, the real one
+    within REAL_TOL_LARGE_N."""
+    from mpi_opt_amd import optimizer as OPT
+    from mpi_opt_amd.models import mnist_space
+    from mpi_opt_amd.optimizer import Optimizer
+
+    monkeypatch.setattr(OPT, "DRIVER", driver)
+    opt = Optimizer(mnist_space(), random_state=13579, device="cuda:0")
+    opt.trace = []
+    ora = SkoptOracle(mnist_space(), random_state=13579)
+    X = _space_points(n_told, 7)
+    Y = [f_mnist(x) for x in X]
+    opt.tell(X, Y)
+    ora.tell(X, Y)
+    asked = []
+    for i in range(3):
+        xd, xo = opt.ask(), ora.ask()
+        asked.append((xd, xo))
+        y = f_mnist(xo)
+        opt.tell(xo, y)
+        ora.tell(xo, y)
+    bd, bo = opt.ask(5), ora.ask(5)
+    # the refits first (theta, top-5, picks, gains): a proposal inherits their differences
+    worst = _compare_traces(opt.trace, ora.trace, f"{driver}: tells at n={n_told}..{n_told + 3}")
+    w2 = _compare_traces(opt.batch_trace, ora.batch_trace, f"{driver}: cl_min batch")
+    real = max(abs(float(a[4]) - float(b[4])) for a, b in asked + list(zip(bd, bo)))
+    print(f"G2 parity at n={n_told} ({driver}): {len(opt.trace) + len(opt.batch_trace)} refits; max |log theta - "
+          f"oracle| = {max(worst['theta'], w2['theta']):.2e}, max gains rel diff = "
+          f"{max(worst['gains'], w2['gains']):.2e}, max real-dim proposal diff = {real:.2e}")
+    for i, (xd, xo) in enumerate(asked):
+        _same_point(xd, xo, f"{driver} n={n_told + i}: ask {i}", REAL_TOL_LARGE_N)
+    for k, (a, b) in enumerate(zip(bd, bo)):
+        _same_point(a, b, f"{driver}: cl_min batch point {k} (n={n_told + 3 + k})", REAL_TOL_LARGE_N)

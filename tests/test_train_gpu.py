@@ -271,3 +271,83 @@ def test_engines_sharing_side_streams_are_bit_identical():
         np.testing.assert_array_equal(lb, ref[st])
     np.testing.assert_array_equal(a.params.cpu().numpy(), ref_p)
     np.testing.assert_array_equal(b.params.cpu().numpy(), ref_p)
+
+
+def test_engines_on_two_threads_and_streams_keep_their_bits():
+    """The ABI is thread-safe across streams (include/mpo.h): two engines stepped at
+    once from two threads, each on its own torch stream, get side streams pooled for
+    their own caller stream (mpo::pooled_side_stream keyed by caller stream, r06),
+    finish without waiting on each other, and keep the bits of an engine stepped
+    alone."""
+    import threading
+
+    x, y = dataset(6)
+    xd, yd = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    tr, _ = orders(MEMBERS, x)
+    otr = torch.from_numpy(tr).cuda()
+    alone, _, _ = make_engine()
+    ref = [alone.train_step(xd, yd, otr, st * BATCH).cpu().numpy().copy() for st in range(4)]
+    ref_p = alone.params.cpu().numpy().copy()
+    del alone
+    engines = [make_engine()[0] for _ in range(2)]
+    torch.cuda.synchronize()
+    losses = [[], []]
+    errors = []
+    go = threading.Barrier(2)
+
+    def run(i):
+        try:
+            torch.cuda.set_device(0)
+            st_ = torch.cuda.Stream()
+            with torch.cuda.stream(st_):
+                go.wait()
+                for st in range(4):
+                    losses[i].append(engines[i].train_step(xd, yd, otr, st * BATCH).clone())
+            st_.synchronize()
+        except BaseException as e:  # noqa: BLE001
+            errors.append(e)
+
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in ths), "engines on two streams deadlocked"
+    assert not errors, errors
+    for i in range(2):
+        for st in range(4):
+            np.testing.assert_array_equal(losses[i][st].cpu().numpy(), ref[st])
+        np.testing.assert_array_equal(engines[i].params.cpu().numpy(), ref_p)
+
+
+def test_band_input_gradient_matches_gather_form(monkeypatch):
+    """The conv2 input gradient in band form (csrc/cnn.hip conv_dgrad_band_kernel:
+    K = (ky, co) in registers, the kx shift scattered into an LDS band of dz1) against
+    the 4x4-tile gather form (MPO_POP_PLAN dgband=0), on one train step of the same
+    members, init and data: identical forward / dz2, so dz1 differs only by f32
+    summation order.  Members span every kernel size 2..10 and widths below and
+    above 16 (F < 16 pads each kx block of an n-tile to 16 channels)."""
+    members = [(F, k, 2, 64, 1e-3, 0.0, 0) for F, k in
+               [(10, 2), (12, 3), (15, 10), (16, 4), (17, 5), (24, 6), (31, 7), (33, 8), (47, 9), (50, 10), (50, 2),
+                (20, 10), (40, 3)]]
+    x, y = dataset(9)
+    xd, yd = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    tr, _ = orders(members, x)
+    otr = torch.from_numpy(tr).cuda()
+    out = []
+    for plan in ("dgband=0", "dgband=1"):
+        monkeypatch.setenv("MPO_POP_PLAN", plan)
+        eng, specs, _ = make_engine(members)
+        eng.train_step(xd, yd, otr, 0)
+        torch.cuda.synchronize()
+        dz1 = []
+        for i, s in enumerate(specs):
+            g = s.geometry()
+            dz1.append(eng.activation(i, "dz1", (BATCH, g["H1"], g["H1"], s.nb_filters)))
+        out.append(dz1)
+        del eng
+    for i, (a, b) in enumerate(zip(*out)):
+        scale = float(np.max(np.abs(a)))
+        assert scale > 0, i
+        err = float(np.max(np.abs(a - b))) / scale
+        assert err <= 2e-5, (members[i], err)
