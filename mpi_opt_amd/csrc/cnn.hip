@@ -93,12 +93,8 @@ struct StepArgs {
     int* correct;            // [n_members] running correct count (eval)
     long long zero_off;      // 64 zero floats in the activation arena (DMA source past row ends)
     int debug;               // diagnostics only (env MPO_POP_DEBUG / plan dbg): 1 skip conv MMA loops, 2 skip conv staging,
-                             // 8 skip the band input gradient's scatter adds,
                              // 4 conv fwd / dgrad weight fragments re-read from groups 0-1 (cache-resident; timing only)
     int conv_mt;             // forward conv m-tiles per wave at most (2: M <= 128 pixels per item; 4: <= 256)
-    int dgband;              // 1: conv2 input gradient in band form (conv_dgrad_band_kernel, w2t = Wt[ky][co][(kx, c)])
-    int dgpf;                // gather-form input gradient: 1 = unconditional next-group prefetch
-    int dgrmw;               // band input gradient: 1 = scatter by read-add-write per n-tile, 0 = ds_add_f32
 };
 
 
@@ -397,7 +393,7 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
 // One workgroup = (member, sample, output rows [y0, y0+R)), R = 4*floor(16/CT)
 // (<= 16 tiles of 4x4, at most 4 per wave); K loop = (tap, 16-channel block).
 // ============================================================================
-template <int NT, int PF>
+template <int NT>
 __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvItem* __restrict__ items) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const ConvItem it = items[blockIdx.x];
@@ -523,13 +519,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
         advance(nky, nkx, ncb);
     }
     for (int g = 0; g < ngroups; g += 2) {
-        if (PF) {
-            // r06: unconditional prefetch (past the last group: the current group again),
-            // so the waitcnt pass keeps the next group's loads in flight over the MFMAs
-            const bool more = g + 1 < ngroups;
-            load_group(more ? nky : cky, more ? nkx : ckx, more ? ncb : ccb, b1);
-            readA(more ? nky : cky, more ? nkx : ckx, more ? ncb : ccb, a1);
-        } else if (g + 1 < ngroups) {
+        if (g + 1 < ngroups) {
             load_group(nky, nkx, ncb, b1);
             readA(nky, nkx, ncb, a1);
         }
@@ -539,11 +529,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
         if (g + 1 >= ngroups) break;
         cky = nky; ckx = nkx; ccb = ncb;
         advance(nky, nkx, ncb);
-        if (PF) {
-            const bool more = g + 2 < ngroups;
-            load_group(more ? nky : cky, more ? nkx : ckx, more ? ncb : ccb, b0);
-            readA(more ? nky : cky, more ? nkx : ckx, more ? ncb : ccb, a0);
-        } else if (g + 2 < ngroups) {
+        if (g + 2 < ngroups) {
             load_group(nky, nkx, ncb, b0);
             readA(nky, nkx, ncb, a0);
         }
@@ -578,232 +564,6 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(StepArgs a, const ConvI
     }
 }
 
-
-// ============================================================================
-// Input gradient of conv2, band form (r06):
-//   dz1[b][ty][tx][c] = (a1 > 0) * sum_{ky,kx,co} dz2[b][ty-ky][tx-kx][co] * w2[ky][kx][c][co]
-// The work of a band of target rows [y0, y0+R) is indexed by q = (ty - y0)*H2 + sx (the
-// target ROW, the SOURCE column) and n = (kx, c):
-//   C[q][n] = sum_{ky, co} dz2[ty - ky][sx][co] * Wt[ky][co][n],   dz1[ty][sx + kx][c] += C[q][(kx, c)].
-// sx + kx always lands inside the H1-wide target row, so every (q, n) product is a real one:
-// M = R*H2 and N = k*F carry no halo padding (the gather form multiplies the zero halo for
-// up to (H1/H2)^2 of its work; its 4x4 tiles cut that to ~1.4x, this form to the ky rows
-// that fall outside dz2 -- skipped per 16-q tile, wave-uniform -- and the 16-padding of M
-// and N).  K = (ky, co) accumulates in registers; only the kx shift is a scatter: once per
-// n-chunk, the accumulators are added into an LDS band of dz1 (ds_add_f32).
-// Determinism: a 16-q tile's scatter targets overlap only those of its two neighbour tiles
-// (16 >= k - 1 columns apart), and inside one wave-instruction all 64 targets differ (the
-// 16 columns of an n-tile carry 16 distinct channels: n = kx*F + c with F >= 16, or one kx
-// per tile with c padded to 16 when F < 16).  The waves own contiguous tile runs and
-// scatter the even tiles, barrier, then the odd tiles: every dz1 element receives its
-// additions in one fixed order (tile parity, the wave's program order), whatever the
-// population or the schedule -- the member-isolation tests hold bit for bit.
-// One workgroup = (member, sample, band); the planner keeps T = ceil(R*H2/16) <= 16 tiles
-// (<= 4 per wave) and the LDS (dz2 rows + halo, and the dz1 band) within the dg_kb budget.
-// ============================================================================
-constexpr int kDgNC = 4;   // n-tiles per chunk (accumulators: 4 q-tiles x 4 n-tiles)
-constexpr int kDgG = 4;    // k-steps per pipeline group
-__host__ __device__ constexpr inline int dgb_fq(int F) { return F >= 16 ? F : 16; }
-__host__ __device__ constexpr inline int dgb_npad(int k, int F) { return (k * dgb_fq(F) + 15) & ~15; }
-
-__global__ __launch_bounds__(256) void conv_dgrad_band_kernel(StepArgs a, const ConvItem* __restrict__ items) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const ConvItem it = items[blockIdx.x];
-    const Member& mb = a.mem[it.member];
-    const int k = mb.k, F = mb.F, H2 = mb.H2, H1 = mb.H1;
-    const int F4 = (F + 3) & ~3, Fs = dgrad_fp(F), S = F4 >> 2;
-    const int Fq = dgb_fq(F), Ncols = k * Fq, Npad = dgb_npad(k, F);
-    const int R = it.R, y0 = it.y0;
-    const int gy_lo = max(0, y0 - (k - 1)), gy_hi = min(H2, y0 + R);
-    const int rows = gy_hi - gy_lo;
-    const int RSs = H2 * Fs;                 // no row padding: pixel q of the band sits at q * Fs
-    const int zoff = align4(rows * RSs);     // 64 zero floats (A reads of rows outside dz2)
-    float* src = smem;                       // [rows][H2][Fs] dz2 rows gy_lo .. gy_hi - 1
-    float* tgt = smem + zoff + 64;           // [R][H1][F] the dz1 band (accumulated)
-    const int tgt_n = R * H1 * F;
-    const float* in = a.act + mb.dz2 + (long long)it.b * H2 * H2 * F;
-    const float* W = a.act + mb.w2t;         // Wt [k][F4][Npad]
-    float* out = a.act + mb.dz1 + ((long long)it.b * H1 + y0) * H1 * F;
-    const float* relu_mask = a.act + mb.a1 + ((long long)it.b * H1 + y0) * H1 * F;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int krow = lane >> 4, kcol = lane & 15;
-
-    // zero the zero block, the dz1 band and, when F % 4 != 0, the channels [F, F4) the
-    // k-steps read past F (their weights are zero; the values must be finite); the
-    // staging writes the other channels -- disjoint locations, one barrier below
-    {
-        float4* z4 = reinterpret_cast<float4*>(smem + zoff);   // zoff % 4 == 0; the LDS plan rounds up
-        for (int e = tid; e < (64 + tgt_n + 3) >> 2; e += 256) z4[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    if (F4 != F)
-        for (int px = tid; px < rows * H2; px += 256)
-            for (int c = F; c < F4; ++c) src[px * Fs + c] = 0.f;
-    if (a.debug != 2) stage_rows(in + (long long)gy_lo * H2 * F, src, rows, H2, F, Fs, RSs, tid);
-
-    // ---- this wave's contiguous run of q-tiles
-    const int M = R * H2;
-    const int T = (M + 15) >> 4;
-    const int t0 = (T * wave) >> 2, mt = ((T * (wave + 1)) >> 2) - t0;   // <= 4 (plan)
-    int qrow[4], base0[4], khi[4], klo[4];
-    int uky0 = k, uky1 = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int q = 16 * (t0 + i) + (lane & 15);
-        const int qr = q / H2, qc = q - qr * H2;
-        const bool ok = i < mt && q < M;
-        qrow[i] = ok ? y0 + qr : -(1 << 20);                 // source row = qrow - ky
-        base0[i] = (y0 + qr - gy_lo) * RSs + qc * Fs;
-        // tile i is live for ky iff some row ty of it has 0 <= ty - ky < H2 (scalar)
-        const int qa = 16 * (t0 + i), qb = min(M, qa + 16) - 1;
-        khi[i] = y0 + qb / H2;                                // ky <= khi
-        klo[i] = y0 + qa / H2 - H2;                           // ky > klo
-        if (i < mt) { uky0 = min(uky0, max(0, klo[i] + 1)); uky1 = max(uky1, min(k, khi[i] + 1)); }
-    }
-    __syncthreads();   // dz2 rows staged, the dz1 band and the padding zeroed
-
-    const int ntiles = Npad >> 4, nchunks = (ntiles + kDgNC - 1) / kDgNC;
-    const int nsteps = (mt > 0 && uky1 > uky0 && a.debug != 1) ? (uky1 - uky0) * S : 0;
-    for (int jc = 0; jc < nchunks; ++jc) {
-        const int nj = min(kDgNC, ntiles - jc * kDgNC);
-        f32x4 acc[4][kDgNC];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < kDgNC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const float* wcol = W + jc * (16 * kDgNC) + kcol;
-        // K = (ky, co) in groups of kDgG k-steps (4 channels each), one group ahead:
-        // a group carries up to kDgG x 4 x 4 MFMAs, enough to cover the next group's
-        // L2 weight loads.  Live bits (step u, tile i) are wave-uniform.
-        // Every load is unconditional (steps past the last one re-read the first step,
-        // n-tiles past nj re-read the last one; their MFMAs are skipped), so the
-        // compiler's vmcnt waits can count the next group's loads instead of draining
-        // them (a conditional load made it wait for vmcnt(0) before each group).
-        int lky = uky0, lst = 0, lidx = 0;   // the next k-step to load
-        const int njl = max(nj, 1) - 1;
-        auto load_group = [&](float (&av)[kDgG][4], float (&bv)[kDgG][kDgNC], unsigned& lm) {
-            lm = 0u;
-#pragma unroll
-            for (int u = 0; u < kDgG; ++u) {
-                const bool sv = lidx < nsteps;
-                const int ky = sv ? lky : uky0;
-                const int co = 4 * (sv ? lst : 0) + krow;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    lm |= (sv && i < mt && ky <= khi[i] && ky > klo[i]) ? 1u << (u * 4 + i) : 0u;
-                    const int sy = qrow[i] - ky;
-                    // rows outside dz2 (and tiles past mt) read the zero block: always finite
-                    av[u][i] = src[(unsigned)sy < (unsigned)H2 ? base0[i] - ky * RSs + co : zoff + co];
-                }
-                const float* wr = wcol + (long long)(ky * F4 + co) * Npad;
-#pragma unroll
-                for (int j = 0; j < kDgNC; ++j) bv[u][j] = wr[16 * min(j, njl)];
-                ++lst;
-                const bool wrap = lst == S;
-                lst = wrap ? 0 : lst;
-                lky += wrap ? 1 : 0;
-                ++lidx;
-            }
-        };
-        auto compute = [&](const float (&av)[kDgG][4], const float (&bv)[kDgG][kDgNC], unsigned lm) {
-#pragma unroll
-            for (int u = 0; u < kDgG; ++u)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if (!((lm >> (u * 4 + i)) & 1u)) continue;
-#pragma unroll
-                    for (int j = 0; j < kDgNC; ++j) {
-                        if (j >= nj) break;
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][i], bv[u][j], acc[i][j], 0, 0, 0);
-                    }
-                }
-        };
-        float a0[kDgG][4], a1[kDgG][4], b0[kDgG][kDgNC], b1[kDgG][kDgNC];
-        unsigned m0 = 0u, m1 = 0u;
-        const int ngroups = (nsteps + kDgG - 1) / kDgG;
-        // the next group is loaded unconditionally (past the last step the loads are
-        // clamped and the group's live bits are 0): a conditional prefetch makes the
-        // waitcnt pass merge the "no prefetch" path and drain to vmcnt(0) per MFMA
-        if (ngroups) load_group(a0, b0, m0);
-        for (int g = 0; g < ngroups; g += 2) {
-            load_group(a1, b1, m1);
-            __builtin_amdgcn_sched_barrier(0);
-            compute(a0, b0, m0);
-            __builtin_amdgcn_sched_barrier(0);
-            if (g + 1 >= ngroups) break;
-            load_group(a0, b0, m0);
-            __builtin_amdgcn_sched_barrier(0);
-            compute(a1, b1, m1);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        // ---- kx scatter of this chunk: even tiles, barrier, odd tiles, barrier
-#pragma unroll
-        for (int par = 0; par < 2; ++par) {
-            if (a.dgrmw) {
-                // plain read-add-write, one n-tile at a time: inside an n-tile every target
-                // of every tile of one parity differs, so its reads can all be in flight;
-                // the next n-tile's reads follow this one's writes in program order
-#pragma unroll
-                for (int j = 0; j < kDgNC; ++j) {
-                    if (j >= nj) break;
-                    const int n = jc * (16 * kDgNC) + 16 * j + kcol;
-                    const int cm = F >= 16 ? (n < Ncols ? n : -1) : ((n & 15) < F ? (n >> 4) * F + (n & 15) : -1);
-                    int ad[4][4];
-                    float v[4][4];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-#pragma unroll
-                        for (int rr = 0; rr < 4; ++rr) {
-                            const int q = 16 * (t0 + i) + krow * 4 + rr;
-                            const int qr = q / H2, qc = q - qr * H2;
-                            const bool ok = i < mt && ((t0 + i) & 1) == par && q < M && cm >= 0;
-                            ad[i][rr] = ok ? (qr * H1 + qc) * F + cm : -1;
-                            v[i][rr] = ok ? tgt[ad[i][rr]] : 0.f;
-                        }
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-#pragma unroll
-                        for (int rr = 0; rr < 4; ++rr)
-                            if (ad[i][rr] >= 0 && a.debug != 8) tgt[ad[i][rr]] = v[i][rr] + acc[i][j][rr];
-                }
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if (i >= mt || ((t0 + i) & 1) != par) continue;
-#pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) {
-                        const int q = 16 * (t0 + i) + krow * 4 + rr;
-                        if (q >= M) continue;
-                        const int qr = q / H2, qc = q - qr * H2;
-                        const int tb = (qr * H1 + qc) * F;
-#pragma unroll
-                        for (int j = 0; j < kDgNC; ++j) {
-                            if (j >= nj) break;
-                            const int n = jc * (16 * kDgNC) + 16 * j + kcol;
-                            const int cm = F >= 16 ? (n < Ncols ? n : -1) : ((n & 15) < F ? (n >> 4) * F + (n & 15) : -1);
-                            if (cm >= 0 && a.debug != 8) atomicAdd(tgt + tb + cm, acc[i][j][rr]);
-                        }
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    }
-    // ---- dz1 rows y0 .. y0 + R (contiguous), masked by the forward ReLU; 8 mask loads
-    // in flight per thread (one dependent load per element measured ~3x the whole
-    // gather kernel's epilogue)
-    constexpr int kEp = 8;
-    for (int e0 = tid; e0 < tgt_n; e0 += kEp * 256) {
-        float mv[kEp];
-#pragma unroll
-        for (int u = 0; u < kEp; ++u) mv[u] = relu_mask[min(e0 + u * 256, tgt_n - 1)];
-#pragma unroll
-        for (int u = 0; u < kEp; ++u) {
-            const int e = e0 + u * 256;
-            if (e < tgt_n) out[e] = mv[u] > 0.f ? tgt[e] : 0.f;
-        }
-    }
-}
 
 // ============================================================================
 // Weight gradient: dW[(ky,kx,c)][n] = sum_{b,y,x} in[b][y+ky][x+kx][c] * dout[b][y][x][n]
@@ -1180,19 +940,7 @@ __global__ void flip_w2_kernel(StepArgs a, const MItem* __restrict__ items) {
     const long long S = (long long)k * k * F4 * N16;
     const float* w2 = a.params + mb.w2;
     float* w2t = a.act + mb.w2t;
-    if (a.dgband) {
-        // band-form input gradient: Wt[ky][co][n], n = kx * Fq + c (conv_dgrad_band_kernel)
-        const int Fq = dgb_fq(F), Npad = dgb_npad(k, F);
-        const long long Sb = (long long)k * F4 * Npad;
-        for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < Sb; i += (long long)gridDim.x * blockDim.x) {
-            const int n = i % Npad;
-            const long long r = i / Npad;
-            const int co = r % F4, ky = r / F4;
-            const int kx = n / Fq, c = n - kx * Fq;
-            w2t[i] = (co < F && c < F && kx < k) ? w2[((long long)(ky * k + kx) * F + c) * F + co] : 0.f;
-        }
-    }
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < S && !a.dgband; i += (long long)gridDim.x * blockDim.x) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < S; i += (long long)gridDim.x * blockDim.x) {
         const int c = i % N16;
         const long long r = i / N16;
         const int f = r % F4;
@@ -1641,7 +1389,7 @@ int env_int(const char* name, int dflt) {
 }
 
 // Planner overrides for tuning sweeps, one variable: MPO_POP_PLAN="key=value,..."
-// (keys: dgband = 0 | 1, dgpf = 0 | 1, dgrmw = 0 | 1, dbg = MPO_POP_DEBUG, xcd = items per XCD run (0: plain order), dg_tiles, dg_kb, conv_mt, conv_kb1, conv_kb2, wg_spg1, wg_spg2, streams = 1 | 2 | 3,
+// (keys: dbg = MPO_POP_DEBUG, xcd = items per XCD run (0: plain order), dg_tiles, dg_kb, conv_mt, conv_kb1, conv_kb2, wg_spg1, wg_spg2, streams = 1 | 2 | 3,
 // occmerge = 0 | 1 | 2, occfill = quarter waves, see bucket_segs).  Every
 // value only changes how work is cut into items or ordered over streams, never the arithmetic.
 int plan_knob(const char* key, int dflt) {
@@ -1684,9 +1432,6 @@ struct Plan {
     size_t lds_conv_max = 0, lds_wg_max = 0;
     int conv_mt = 4;        // forward conv m-tiles per wave at most: items of up to 256 pixels (MPO_POP_PLAN conv_mt=2: 128)
     int dg_tiles = 12;      // 4x4 tiles per conv2 input-gradient work item at most (MPO_POP_PLAN dg_tiles)
-    int dgband = 0;         // conv2 input gradient in band form (MPO_POP_PLAN dgband=1; 0: the 4x4-tile gather kernel)
-    int dgpf = 0;           // gather kernel: unconditional next-group prefetch (MPO_POP_PLAN dgpf)
-    int dgrmw = 0;          // band kernel: read-add-write scatter instead of LDS atomics (MPO_POP_PLAN dgrmw)
     // Second stream for independent launches (MPO_POP_PLAN streams=1 keeps one): the
     // forward conv2 buckets alternate between the two, and the conv2 weight gradient
     // runs beside the input gradient + conv1 weight gradient, so one launch's tail
@@ -1705,27 +1450,6 @@ size_t conv_lds_bytes(int rows, int Wp, int Cin, int Ho, int K, int nt) {
 size_t dgrad_lds_bytes(int R, int k, int F, int H2) {
     const int rows = std::min(H2, R + k - 1);   // dz2 rows of the widest chunk (unpadded)
     return (size_t)(align4(rows * dgrad_rs(H2, F)) + 64) * sizeof(float);
-}
-
-// band-form input gradient: dz2 rows of the band + halo, the zero block, the dz1 band
-size_t dgb_lds_bytes(int R, int k, int F, int H1, int H2) {
-    const int rows = std::min(H2, R + k - 1);
-    return (size_t)(align4(rows * H2 * dgrad_fp(F)) + 64 + align4(R * H1 * F)) * sizeof(float);
-}
-
-// Band height of the band-form input gradient: the tallest band with T = ceil(R*H2/16)
-// <= 16 q-tiles (<= 4 per wave) inside the LDS budget.  r06 measured: a planner that
-// minimised the MFMA tiles (small bands) left ~21 MFMAs per 4-step group of a wave's
-// 64 slots, and the per-group loads and address math then set the pace; the tallest
-// band issues as few MFMAs (1.16x vs 1.16x the exact count) at ~33 per group.
-int dgb_rows(int k, int F, int H1, int H2, size_t budget) {
-    int best_r = 1;
-    for (int R = 1; R <= H1; ++R) {
-        if ((R * H2 + 15) / 16 > 16) break;
-        if (R > 1 && dgb_lds_bytes(R, k, F, H1, H2) > budget) break;
-        best_r = R;
-    }
-    return best_r;
 }
 
 size_t wg_lds_bytes(int k, int Hin, int Cin, int Ho, int F) {
@@ -1798,6 +1522,11 @@ void bucket_segs(std::vector<T>& items, Bucketed& bk, const std::vector<Member>&
 // groups, so every XCD still gets an even share of every member size (one contiguous
 // eighth per XCD -- c = n / 8 -- measured 21% SLOWER on the 320-member step despite
 // 16% less HBM traffic: the eighths' costs differ).  The table is stored permuted.
+// r06, MI355X, 320 members (profiles/r06/xcd_*.log): runs of c = 4 items cut the
+// measured HBM traffic per train batch 37.9 -> 33.8 GB (conv_wgrad 11.9 -> 8.7 GB, its
+// m-groups' row re-reads now meet in one L2) for +0.3% step time (37.05 -> 37.16 ms;
+// the kernels are issue-bound, not HBM-bound); c = 2 / 8 / 16 / 32: 37.2-37.4 ms.
+// MPO_POP_PLAN xcd=0 restores the plain order.
 template <class T>
 void xcd_deal(std::vector<T>& items, const Bucketed& bk, int c) {
     if (c <= 1) return;
@@ -1925,15 +1654,11 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         // r03: at most 12 tiles (3 per wave): conv2 dgrad 15.40 -> 15.15 ms per 320-member batch
         // (profiles/r03/train_sweep_dgtiles_ap.log; 16 was r01-r02's, 8 measured 16.96)
         if (i == 0) P.dg_tiles = std::max(1, std::min(16, plan_knob("dg_tiles", 12)));
-        if (i == 0) P.dgband = plan_knob("dgband", 0) ? 1 : 0;
-        if (i == 0) P.dgpf = plan_knob("dgpf", 0) ? 1 : 0;
-        if (i == 0) P.dgrmw = plan_knob("dgrmw", 0) ? 1 : 0;
         int Rd = 4 * std::max(1, P.dg_tiles / ((m.H1 + 3) / 4));
         while (Rd > 4 && dgrad_lds_bytes(Rd, k, F, m.H2) > dgb) Rd -= 4;
-        if (P.dgband) Rd = dgb_rows(k, F, m.H1, m.H2, dgb);
         const size_t l1 = conv_lds_bytes(R1 + k - 1, kImg, 1, m.H1, k * k, nt);
         const size_t l2 = conv_lds_bytes(R2 + k - 1, m.H1, F, m.H2, k * k * F, nt);
-        const size_t ld = P.dgband ? dgb_lds_bytes(Rd, k, F, m.H1, m.H2) : dgrad_lds_bytes(Rd, k, F, m.H2);
+        const size_t ld = dgrad_lds_bytes(Rd, k, F, m.H2);
         L1[i] = l1; L2[i] = l2; LD[i] = ld;
         for (int b = 0; b < B; ++b) {
             for (int y = 0; y < m.H1; y += R1) P.conv1.push_back({i, b, y, std::min(R1, m.H1 - y)});
@@ -1996,7 +1721,7 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
     bucket_segs(P.dgrad, P.bdg, P.mem, LD, occ);
     bucket_segs(P.wg1, P.bw1, P.mem, LW1, occ);
     bucket_segs(P.wg2, P.bw2, P.mem, LW2, occ);
-    const int xc = plan_knob("xcd", 0);
+    const int xc = plan_knob("xcd", 4);
     xcd_deal(P.conv1, P.bc1, xc);
     xcd_deal(P.conv2, P.bc2, xc);
     xcd_deal(P.dgrad, P.bdg, xc);
@@ -2052,7 +1777,7 @@ hipError_t launch_conv_nt(const StepArgs& a, const ConvItem* items, int count, s
 template <int NT>
 hipError_t launch_dgrad_nt(const StepArgs& a, const ConvItem* items, int count, size_t lds, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    auto kern = a.dgpf ? conv_dgrad_kernel<NT, 1> : conv_dgrad_kernel<NT, 0>;
+    auto kern = conv_dgrad_kernel<NT>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(count), dim3(256), lds, s, a, items);
     return hipGetLastError();
@@ -2116,15 +1841,6 @@ hipError_t launch_conv(Plan& P, const StepArgs& a, size_t table_off, const Bucke
 
 hipError_t launch_dgrad(Plan& P, const StepArgs& a, hipStream_t s, hipStream_t s2 = nullptr) {
     const ConvItem* base = dev_table<ConvItem>(P, P.off_dgrad);
-    if (P.dgband)
-        return launch_segs(P, P.bdg, "conv2_dgrad", s, [&](const Seg& sg, hipStream_t st) {
-            const int count = sg.end - sg.begin;
-            if (count <= 0) return hipSuccess;
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv_dgrad_band_kernel),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sg.lds);
-            hipLaunchKernelGGL(conv_dgrad_band_kernel, dim3(count), dim3(256), sg.lds, st, a, base + sg.begin);
-            return hipGetLastError();
-        }, s2);
     return launch_segs(P, P.bdg, "conv2_dgrad", s, [&](const Seg& sg, hipStream_t st) {
         return MPO_NT_SWITCH(launch_dgrad_nt, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, st);
     }, s2);
@@ -2176,9 +1892,6 @@ StepArgs make_args(const Plan& P, const float* x, const int* labels, const int* 
     a.correct = nullptr;
     a.debug = P.debug;
     a.conv_mt = P.conv_mt;
-    a.dgband = P.dgband;
-    a.dgpf = P.dgpf;
-    a.dgrmw = P.dgrmw;
     a.zero_off = P.zero_off;
     return a;
 }

@@ -318,36 +318,3 @@ def test_engines_on_two_threads_and_streams_keep_their_bits():
         for st in range(4):
             np.testing.assert_array_equal(losses[i][st].cpu().numpy(), ref[st])
         np.testing.assert_array_equal(engines[i].params.cpu().numpy(), ref_p)
-
-
-def test_band_input_gradient_matches_gather_form(monkeypatch):
-    """The conv2 input gradient in band form (csrc/cnn.hip conv_dgrad_band_kernel:
-    K = (ky, co) in registers, the kx shift scattered into an LDS band of dz1) against
-    the 4x4-tile gather form (MPO_POP_PLAN dgband=0), on one train step of the same
-    members, init and data: identical forward / dz2, so dz1 differs only by f32
-    summation order.  Members span every kernel size 2..10 and widths below and
-    above 16 (F < 16 pads each kx block of an n-tile to 16 channels)."""
-    members = [(F, k, 2, 64, 1e-3, 0.0, 0) for F, k in
-               [(10, 2), (12, 3), (15, 10), (16, 4), (17, 5), (24, 6), (31, 7), (33, 8), (47, 9), (50, 10), (50, 2),
-                (20, 10), (40, 3)]]
-    x, y = dataset(9)
-    xd, yd = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
-    tr, _ = orders(members, x)
-    otr = torch.from_numpy(tr).cuda()
-    out = []
-    for plan in ("dgband=0", "dgband=1"):
-        monkeypatch.setenv("MPO_POP_PLAN", plan)
-        eng, specs, _ = make_engine(members)
-        eng.train_step(xd, yd, otr, 0)
-        torch.cuda.synchronize()
-        dz1 = []
-        for i, s in enumerate(specs):
-            g = s.geometry()
-            dz1.append(eng.activation(i, "dz1", (BATCH, g["H1"], g["H1"], s.nb_filters)))
-        out.append(dz1)
-        del eng
-    for i, (a, b) in enumerate(zip(*out)):
-        scale = float(np.max(np.abs(a)))
-        assert scale > 0, i
-        err = float(np.max(np.abs(a - b))) / scale
-        assert err <= 2e-5, (members[i], err)
