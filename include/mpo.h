@@ -12,7 +12,10 @@
  *   - every launching call takes an explicit hipStream_t (passed as void*) and
  *     only enqueues work: no host synchronisation, no allocation, so callers
  *     may capture any sequence of calls into a hipGraph;
- *   - not re-entrant per stream; thread-safe across streams/devices.
+ *   - not re-entrant per stream; thread-safe across streams/devices.  The
+ *     population engines (mpo_pop_*, mpo_dn_*) fork part of a step onto side
+ *     streams pooled per (device, caller stream): engines stepped from distinct
+ *     caller streams never wait for each other's work.
  *
  * Row-major layouts throughout: matrix A(i,j) lives at A[i*ld + j].
  *

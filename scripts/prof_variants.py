@@ -20,6 +20,10 @@ def main():
     tag = sys.argv[1]
     args = sys.argv[2:]
     extra = []
+    script = "plan_ab.py"
+    if "--dn" in args:            # DenseNet population (scripts/dn_ab.py, MPO_DN_PLAN variants)
+        args.remove("--dn")
+        script = "dn_ab.py"
     if "--shard" in args:
         i = args.index("--shard")
         extra = ["--shard", args[i + 1]]
@@ -30,7 +34,7 @@ def main():
     for i, v in enumerate(args):
         d = tempfile.mkdtemp(prefix="mpo_pv_", dir="/tmp")
         cmd = ["rocprofv3", "--kernel-trace", "--stats", "-d", d, "-o", "run", "--output-format", "csv", "--",
-               sys.executable, os.path.join(ROOT, "scripts", "plan_ab.py"), "--variants", v, "--rounds", "1",
+               sys.executable, os.path.join(ROOT, "scripts", script), "--variants", v, "--rounds", "1",
                "--steps", str(steps), *extra]
         r = subprocess.run(cmd, cwd="/tmp", env={**os.environ, "TMPDIR": "/tmp"}, stdout=subprocess.PIPE,
                            stderr=subprocess.STDOUT, timeout=300)
