@@ -186,8 +186,11 @@ def live_pmc(train_trials):
         out["ei"] = {"hbm_bytes_per_launch": 2.0 * fetch + write, "fetch_size_bytes_raw": fetch,
                      "write_size_bytes": write, "launches": passes, "dispatches": len(f)}
         # the dominant kernel's average duration as rocprofv3 reports it (kernel-trace
-        # stats; the roofline's HIP-event time is measured in this process beside it)
-        calls, avg_ns = kernel_trace_pass(ei_prog, lambda k: "gp_score_kernel" in k)
+        # stats) over the bench's own EI leg in a child process (the same sustained
+        # launches: a short probe runs at a higher clock -- 0.96 vs 1.31 ms measured);
+        # the roofline's HIP-event time is measured in this process beside it
+        calls, avg_ns = kernel_trace_pass([os.path.join(ROOT, "bench.py"), "--workload", "ei", "--no-pmc",
+                                           "--no-cpu-baseline"], lambda k: "gp_score_kernel" in k, timeout=300)
         out["ei"]["rocprof_calls"], out["ei"]["rocprof_avg_ns"] = calls, avg_ns
     except Exception as e:  # noqa: BLE001 -- reported, the bench line carries traffic null
         out["errors"].append(f"ei: {e}")

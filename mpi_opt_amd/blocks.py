@@ -494,7 +494,8 @@ class DistributedEvaluator:
         else:
             res = self.local.train_units(mine, seed_base=self.n_evaluated, trial_ids=trial_ids)
         self.n_evaluated += len(params_list)
-        return decode_histories(self.ch.gather_rows(encode_histories(res)))
+        parts = self.ch.gather_rows(encode_histories(res))
+        return decode_histories(parts) if self.rank == 0 else None   # only rank 0 tells
 
     # ---- score ------------------------------------------------------------------
     def _score(self, m, d, n, k, mask, dm, req=None):
@@ -585,6 +586,8 @@ class DistributedEvaluator:
             np.zeros((0, 0))
         merged = [None] * len(jobs)
         for part in self.ch.gather_rows(rows):
+            if self.rank != 0:
+                continue                     # only rank 0 hands the batches to the optimizer
             for row in part:
                 i, npts, dd = int(row[0]), int(row[1]), int(row[2])
                 v = row[3:3 + npts * dd].reshape(npts, dd)

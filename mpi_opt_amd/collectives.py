@@ -28,33 +28,54 @@ HEADER = 16            # int64 words of a round header
 CODE_FLOAT, CODE_INT = 0, 1
 
 
+_INT_T = (int, np.integer)
+_NUM_T = (int, float, np.integer, np.floating)
+
+
+def _is_int(v):
+    return isinstance(v, _INT_T) and not isinstance(v, (bool, np.bool_))
+
+
 def encode_points(points):
-    """[[v, ...], ...] -> (values f64 [n, D], codes f64 [n, D]); ints -> CODE_INT."""
+    """[[v, ...], ...] -> (values f64 [n, D], codes f64 [n, D]); ints -> CODE_INT.
+    Columns are typed at once when uniform (a search space's points are: Integer
+    dimensions give ints, Real ones floats), value by value otherwise."""
     n = len(points)
     d = len(points[0]) if n else 0
-    vals = np.zeros((n, d), dtype=np.float64)
+    if any(len(p) != d for p in points):
+        raise ValueError("encode_points: points of different lengths")
     codes = np.zeros((n, d), dtype=np.float64)
-    for i, p in enumerate(points):
-        if len(p) != d:
-            raise ValueError("encode_points: points of different lengths")
-        for j, v in enumerate(p):
-            if isinstance(v, (bool, np.bool_)):
-                raise TypeError(f"encode_points: boolean parameter {v!r} is not supported")
-            if isinstance(v, (int, np.integer)):
-                vals[i, j] = float(int(v))
-                codes[i, j] = CODE_INT
-                if int(vals[i, j]) != int(v):
-                    raise ValueError(f"encode_points: integer {v} does not fit an f64 exactly")
-            elif isinstance(v, (float, np.floating)):
-                vals[i, j] = float(v)
-            else:
-                raise TypeError(f"encode_points: only numeric parameters cross ranks (got {type(v).__name__})")
+    for j in range(d):
+        col = [p[j] for p in points]
+        types = set(map(type, col))
+        if any(issubclass(t, (bool, np.bool_)) or not issubclass(t, _NUM_T) for t in types):
+            bad = next(t for t in types if issubclass(t, (bool, np.bool_)) or not issubclass(t, _NUM_T))
+            raise TypeError(f"encode_points: only int / float parameters cross ranks (got {bad.__name__})")
+        ints = [issubclass(t, _INT_T) for t in types]
+        if all(ints):
+            codes[:, j] = CODE_INT
+        elif any(ints):
+            codes[:, j] = [CODE_INT if _is_int(v) else CODE_FLOAT for v in col]
+    vals = np.array(points, dtype=np.float64).reshape(n, d)
+    if (codes == CODE_INT).any() and np.abs(vals[codes == CODE_INT]).max(initial=0.0) >= 2.0 ** 53:
+        raise ValueError("encode_points: an integer does not fit an f64 exactly")
     return vals, codes
 
 
 def decode_points(vals, codes):
-    return [[int(v) if c == CODE_INT else float(v) for v, c in zip(vr, cr)]
-            for vr, cr in zip(np.asarray(vals), np.asarray(codes))]
+    vals, codes = np.asarray(vals, dtype=np.float64), np.asarray(codes)
+    rows = vals.tolist()
+    if not len(rows):
+        return rows
+    for j in range(vals.shape[1]):
+        c = codes[:, j] == CODE_INT
+        if c.all():
+            for r, v in zip(rows, vals[:, j].astype(np.int64).tolist()):
+                r[j] = v
+        elif c.any():
+            for i in np.nonzero(c)[0]:
+                rows[i][j] = int(vals[i, j])
+    return rows
 
 
 class TensorChannel:

@@ -95,6 +95,7 @@ struct StepArgs {
     int debug;               // diagnostics only (env MPO_POP_DEBUG / plan dbg): 1 skip conv MMA loops, 2 skip conv staging,
                              // 4 conv fwd / dgrad weight fragments re-read from groups 0-1 (cache-resident; timing only)
     int conv_mt;             // forward conv m-tiles per wave at most (2: M <= 128 pixels per item; 4: <= 256)
+    int wgrpb;               // conv2 weight gradient: output rows per barrier (1 | 2)
 };
 
 
@@ -631,7 +632,14 @@ __device__ __forceinline__ void wgrad_row(const float* __restrict__ img, const f
 // ceil(tiles / 8)): a single loop body keeps the kernel at <= 128 VGPRs, i.e. two
 // 8-wave workgroups per CU.  A wave with fewer real tiles multiplies the constant
 // zero row for the rest (never written back).
-template <int OP, int NT, int MT>
+// RPB = output rows per barrier.  1: the r03 schedule (input row y+k+1 and dout row
+// y+2 issued at row y, a counted vmcnt keeps them in flight over the barrier).  2 (r06):
+// rows y, y+1 between barriers, the next pair's two input rows and two dout rows
+// issued before them and retired (vmcnt(0)) after them -- half the barriers, one
+// more ring slot and dout buffer.  The same MFMAs per row in the same order: the
+// same bits either way.  Measured (profiles/r06/wgrpb_sweep_*.log): 320 members
+// 37.17 -> 37.06 ms per step, 40 members 5.58 -> 5.52 ms; the default is 2.
+template <int OP, int NT, int MT, int RPB>
 __global__ __launch_bounds__(kWgThreads) void conv_wgrad_kernel(StepArgs a, const WgItem* __restrict__ items) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const WgItem it = items[blockIdx.x];
@@ -646,7 +654,7 @@ __global__ __launch_bounds__(kWgThreads) void conv_wgrad_kernel(StepArgs a, cons
     }
     const int N = F;
     const int Kw = k * k * Cin;
-    const int RS = k + 2;                       // ring slots
+    const int RS = k + 1 + RPB;                 // ring slots
     const int rowf = Hin * Cin;                 // floats per input row
     const int rowS = round64(rowf);             // slot stride (a DMA chunk never crosses a slot)
     const int dcnt = Ho * N;                    // floats per dout row (pixel stride N)
@@ -654,8 +662,9 @@ __global__ __launch_bounds__(kWgThreads) void conv_wgrad_kernel(StepArgs a, cons
     const int dS = round64((4 * nk4 + 4) * N + 64);   // dout buffer stride: zero padding past Ho*N
     float* ring = smem;                                              // [RS][rowS] (+ slack)
     const int ring_elems = RS * rowS + 8 * Cin + 64;                 // k-step padding reads stay in bounds
-    float* dl = smem + round64(ring_elems);                          // [3][dS]
-    const int lds_floats = round64(ring_elems) + 3 * dS;             // + kWgWaves*64 scratch, + {0, 1}
+    constexpr int ND = 2 + RPB;                                      // dout row buffers
+    float* dl = smem + round64(ring_elems);                          // [ND][dS]
+    const int lds_floats = round64(ring_elems) + ND * dS;            // + kWgWaves*64 scratch, + {0, 1}
     const int kZero = lds_floats + kWgWaves * 64, kOne = kZero + 1;  // constant A rows (padding / bias)
     const float* zero_src = a.act + a.zero_off;                      // 64 zero floats in global memory
     const float* in_base = OP == WG_CONV1 ? a.x : a.act + mb.a1;
@@ -721,6 +730,41 @@ __global__ __launch_bounds__(kWgThreads) void conv_wgrad_kernel(StepArgs a, cons
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         int slot0 = 0;   // ring slot of input row y
+        if constexpr (RPB == 2) {
+            for (int y = 0; y < Ho; y += 2) {
+                // the next pair's rows: input rows y+k+1, y+k+2 -> the slots rows y-2, y-1
+                // used; dout rows y+2, y+3 -> the buffers of dout rows y-2, y-1
+                if (y + 2 < Ho) {
+                    int sl = slot0 + k + 1;
+                    sl = sl >= RS ? sl - RS : sl;
+                    dma(inb + (y + k + 1) * rowf, rowf, ring + sl * rowS);
+                    dma(dob + (y + 2) * dcnt, dcnt, dl + ((y + 2) & 3) * dS);
+                    if (y + 3 < Ho) {
+                        sl = sl + 1 == RS ? 0 : sl + 1;
+                        dma(inb + (y + k + 2) * rowf, rowf, ring + sl * rowS);
+                        dma(dob + (y + 3) * dcnt, dcnt, dl + ((y + 3) & 3) * dS);
+                    }
+                }
+#pragma unroll
+                for (int dy = 0; dy < 2; ++dy) {
+                    if (y + dy >= Ho) break;
+                    int abase[MT];
+#pragma unroll
+                    for (int i = 0; i < MT; ++i) {
+                        int sl = slot0 + dy + tky[i];
+                        sl = sl >= RS ? sl - RS : sl;
+                        abase[i] = astep[i] ? sl * rowS + tcol[i] : tcol[i];
+                    }
+                    const float* dcur = dl + ((y + dy) & 3) * dS;
+                    if (a.debug != 1 && mine > 0) wgrad_row<MT, NT>(ring, dcur, abase, astep, N, nk4, krow, kcol, acc);
+                }
+                slot0 += 2;
+                slot0 = slot0 >= RS ? slot0 - RS : slot0;
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+            }
+            continue;
+        }
         for (int y = 0; y < Ho; ++y) {
             // two rows ahead: input row y+k+1 -> the slot row y-1 used; dout row y+2
             const bool ahead = y + 2 < Ho;   // then input row y + k + 1 = (y + 2) + k - 1 < Hin too
@@ -1389,7 +1433,7 @@ int env_int(const char* name, int dflt) {
 }
 
 // Planner overrides for tuning sweeps, one variable: MPO_POP_PLAN="key=value,..."
-// (keys: dbg = MPO_POP_DEBUG, xcd = items per XCD run (0: plain order), dg_tiles, dg_kb, conv_mt, conv_kb1, conv_kb2, wg_spg1, wg_spg2, streams = 1 | 2 | 3,
+// (keys: wgrpb = 1 | 2, dbg = MPO_POP_DEBUG, xcd = items per XCD run (0: plain order), dg_tiles, dg_kb, conv_mt, conv_kb1, conv_kb2, wg_spg1, wg_spg2, streams = 1 | 2 | 3,
 // occmerge = 0 | 1 | 2, occfill = quarter waves, see bucket_segs).  Every
 // value only changes how work is cut into items or ordered over streams, never the arithmetic.
 int plan_knob(const char* key, int dflt) {
@@ -1432,6 +1476,7 @@ struct Plan {
     size_t lds_conv_max = 0, lds_wg_max = 0;
     int conv_mt = 4;        // forward conv m-tiles per wave at most: items of up to 256 pixels (MPO_POP_PLAN conv_mt=2: 128)
     int dg_tiles = 12;      // 4x4 tiles per conv2 input-gradient work item at most (MPO_POP_PLAN dg_tiles)
+    int wgrpb = 2;          // conv2 weight gradient output rows per barrier (MPO_POP_PLAN wgrpb = 1 | 2)
     // Second stream for independent launches (MPO_POP_PLAN streams=1 keeps one): the
     // forward conv2 buckets alternate between the two, and the conv2 weight gradient
     // runs beside the input gradient + conv1 weight gradient, so one launch's tail
@@ -1452,10 +1497,10 @@ size_t dgrad_lds_bytes(int R, int k, int F, int H2) {
     return (size_t)(align4(rows * dgrad_rs(H2, F)) + 64) * sizeof(float);
 }
 
-size_t wg_lds_bytes(int k, int Hin, int Cin, int Ho, int F) {
-    const int ring = round64((k + 2) * round64(Hin * Cin) + 8 * Cin + 64);
+size_t wg_lds_bytes(int k, int Hin, int Cin, int Ho, int F, int rpb = 1) {
+    const int ring = round64((k + 1 + rpb) * round64(Hin * Cin) + 8 * Cin + 64);
     const int dS = round64((4 * ((Ho + 3) >> 2) + 4) * F + 64);
-    return (size_t)(ring + 3 * dS + kWgWaves * 64 + 4) * sizeof(float);
+    return (size_t)(ring + (2 + rpb) * dS + kWgWaves * 64 + 4) * sizeof(float);
 }
 
 // Row-chunk height: as many output rows as fit M = R*Ho <= mcap pixels, shrunk
@@ -1668,7 +1713,8 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         }
         P.lds_conv_max = std::max({P.lds_conv_max, l1, l2, ld});
         // wgrad items: (member, 512-row m-group, sample group)
-        const size_t lw2 = wg_lds_bytes(k, m.H1, F, m.H2, F);
+        if (i == 0) P.wgrpb = plan_knob("wgrpb", 2) == 1 ? 1 : 2;
+        const size_t lw2 = wg_lds_bytes(k, m.H1, F, m.H2, F, P.wgrpb);
         const size_t lw1 = wg_lds_bytes(k, kImg, 1, m.H1, F);
         LW2[i] = lw2; LW1[i] = lw1;
         const int K2 = k * k * F, K1w = k * k;
@@ -1783,11 +1829,16 @@ hipError_t launch_dgrad_nt(const StepArgs& a, const ConvItem* items, int count, 
     return hipGetLastError();
 }
 
+template <int OP, int NT, int RPB>
+auto wg_kernel(int mt) {
+    return mt == 1 ? conv_wgrad_kernel<OP, NT, 1, RPB> : mt == 2 ? conv_wgrad_kernel<OP, NT, 2, RPB>
+         : mt == 3 ? conv_wgrad_kernel<OP, NT, 3, RPB> : conv_wgrad_kernel<OP, NT, 4, RPB>;
+}
+
 template <int OP, int NT>
 hipError_t launch_wg_nt(const StepArgs& a, const WgItem* items, int count, size_t lds, int mt, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    auto kern = mt == 1 ? conv_wgrad_kernel<OP, NT, 1> : mt == 2 ? conv_wgrad_kernel<OP, NT, 2>
-              : mt == 3 ? conv_wgrad_kernel<OP, NT, 3> : conv_wgrad_kernel<OP, NT, 4>;
+    auto kern = a.wgrpb == 2 ? wg_kernel<OP, NT, 2>(mt) : wg_kernel<OP, NT, 1>(mt);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(count), dim3(kWgThreads), lds, s, a, items);
     return hipGetLastError();
@@ -1892,6 +1943,7 @@ StepArgs make_args(const Plan& P, const float* x, const int* labels, const int* 
     a.correct = nullptr;
     a.debug = P.debug;
     a.conv_mt = P.conv_mt;
+    a.wgrpb = P.wgrpb;
     a.zero_off = P.zero_off;
     return a;
 }
