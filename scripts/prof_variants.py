@@ -24,10 +24,11 @@ def main():
     if "--dn" in args:            # DenseNet population (scripts/dn_ab.py, MPO_DN_PLAN variants)
         args.remove("--dn")
         script = "dn_ab.py"
-    if "--shard" in args:
-        i = args.index("--shard")
-        extra = ["--shard", args[i + 1]]
-        args = args[:i] + args[i + 2:]
+    for flag in ("--shard", "--trials", "--members"):
+        if flag in args:
+            i = args.index(flag)
+            extra += [flag, args[i + 1]]
+            args = args[:i] + args[i + 2:]
     steps = 3
     out_dir = os.path.join(ROOT, "gpurun_out")
     os.makedirs(out_dir, exist_ok=True)

@@ -65,6 +65,11 @@ def main():
     flops = sum(m.flops_per_sample_train() for m in members) * 100
     print("train step %.2f ms  %.1f TFLOP/s  (%.1f%% of 157.3)" % (dt * 1e3, flops / dt / 1e12, flops / dt / 157.3e12 * 100))
     print("loss", eng.loss[:5].cpu().numpy())
+    if __import__("os").environ.get("MPO_POP_PROFILE"):
+        ph = eng.profile()   # ms summed over the 12 steps (serial: profiled steps stay on one stream)
+        tot = sum(ph.values())
+        for k_, v_ in sorted(ph.items(), key=lambda kv: -kv[1]):
+            print(f"  {k_:28s} {v_ / 12:8.3f} ms/step  {100 * v_ / tot:5.1f}%")
     if args.no_eval:
         return
     va = np.stack([kfold_split(60000, args.folds, f)[1] for f in folds])
