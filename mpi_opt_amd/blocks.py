@@ -34,6 +34,7 @@ import hashlib
 import json
 import math
 import os
+import types
 
 import numpy as np
 
@@ -498,8 +499,10 @@ class DistributedEvaluator:
         return decode_histories(parts) if self.rank == 0 else None   # only rank 0 tells
 
     # ---- score ------------------------------------------------------------------
-    def _score(self, m, d, n, k, mask, dm, req=None):
+    def _score(self, m, d, n, k, mask, dm, fac=0, req=None):
         acqs = [a for i, a in enumerate(ACQ_ORDER) if mask >> i & 1]
+        if fac:
+            return self._score_factor(m, d, k, acqs, fac, req)
         head = None
         if self.rank == 0:
             head = [float(req.get("y_opt", 0.0)), float(req.get("xi", 0.01)), float(req.get("kappa", 1.96))]
@@ -520,6 +523,63 @@ class DistributedEvaluator:
             rows[r, k:] = -1.0
             if a in part:
                 v, i = part[a]
+                rows[r, :len(v)] = v
+                rows[r, k:k + len(i)] = np.asarray(i, dtype=np.float64) + s0
+        out = {}
+        parts = self.ch.gather_rows(rows)
+        for r, a in enumerate(acqs):
+            lists = []
+            for pr in parts:
+                if len(pr):
+                    idx = pr[r, k:].astype(np.int64)
+                    keep = idx >= 0
+                    lists.append((pr[r, :k][keep], idx[keep]))
+            out[a] = merge_topk(lists, int(k))
+        return out
+
+    def _score_factor(self, m, d, k, acqs, wsb, req=None):
+        """Sharded scoring of a fitted model: rank 0's prepared factor --
+        the workspace ``mpo_gp_prepare`` wrote, ``DeviceGP.export_factor`` -- is
+        broadcast as raw words, so no rank factorises again; the candidates are
+        scattered, each rank scores its slice, the top-k rows are all-gathered."""
+        import torch
+
+        from .gp import DeviceGP
+
+        dev = self.local.device if self.local.device is not None else torch.device("cuda", torch.cuda.current_device())
+        lay_n = 4 + len(DeviceGP._PTRS)
+        meta = layout = None
+        if self.rank == 0:
+            gp = req["est"].dev
+            meta, layout, ws0 = gp.export_factor()
+            meta = np.concatenate([meta, [float(req["y_opt"]), float(req.get("xi", 0.01)), float(req.get("kappa", 1.96))]])
+        meta = self.ch.bcast(meta, (6,))
+        layout = self.ch.bcast(layout, (lay_n,), dtype=np.int64)
+        words = (wsb + 7) // 8
+        # the workspace as int64 words: on RCCL straight between the GPUs' buffers
+        if self.rank == 0 and self.ch.device.type == "cuda":
+            buf = torch.zeros(words * 8, dtype=torch.uint8, device=self.ch.device)
+            buf[:wsb].copy_(ws0[:wsb])
+        elif self.rank == 0:
+            buf = torch.zeros(words * 8, dtype=torch.uint8)
+            buf[:wsb].copy_(ws0[:wsb].cpu())
+        else:
+            buf = torch.empty(words * 8, dtype=torch.uint8, device=self.ch.device)
+        wv = buf.view(torch.int64)
+        self.dist.broadcast(wv, src=0, group=self.group)
+        if self.rank == 0:
+            gp_local = gp
+        else:
+            ws = buf.to(dev) if buf.device != dev else buf
+            gp_local = DeviceGP.from_factor(meta, layout, ws, device=dev)
+        cand, s0, s1 = self.ch.scatter_rows(req["cand"] if self.rank == 0 else None, m, d, as_tensor=True)
+        rows = np.full((len(acqs), 2 * k), np.nan)
+        rows[:, k:] = -1.0
+        if s1 > s0:
+            top = _device_topk(types.SimpleNamespace(dev=gp_local), cand, float(meta[3]), tuple(acqs),
+                               float(meta[4]), float(meta[5]), min(k, s1 - s0))
+            for r, a in enumerate(acqs):
+                v, i = top[a]
                 rows[r, :len(v)] = v
                 rows[r, k:k + len(i)] = np.asarray(i, dtype=np.float64) + s0
         out = {}
@@ -620,7 +680,7 @@ class DistributedEvaluator:
         elif kind == KIND_CHAINS:
             self._chains(h[1], h[2], h[3])
         elif kind == KIND_SCORE:
-            self._score(*h[1:7])
+            self._score(*h[1:8])
         else:
             raise ValueError(f"unknown round {kind}")
         return True
@@ -658,8 +718,11 @@ class DistributedEvaluator:
         m, d = cand.shape
         dm = int(np.asarray(req["Xt"]).shape[1]) if "Xt" in req else 0
         n = int(np.asarray(req["Xt"]).shape[0]) if "Xt" in req else 0
-        self.ch.header([KIND_SCORE, m, d, n, int(req["k"]), mask, dm])
-        got = self._score(m, d, n, int(req["k"]), mask, dm, req)
+        # a fitted model (ShardedScorer): its prepared factor is broadcast; a bare
+        # (Xt, y, theta) request: every rank factorises it (local_topk)
+        fac = int(req["est"].dev.export_factor()[2].numel()) if req.get("est") is not None else 0
+        self.ch.header([KIND_SCORE, m, d, n, int(req["k"]), mask, dm, fac])
+        got = self._score(m, d, n, int(req["k"]), mask, dm, fac, req)
         return {a: got[a] for a in acqs}
 
     def serve(self):
@@ -677,9 +740,10 @@ class ShardedScorer:
     :class:`DistributedEvaluator` (the candidate batch M/W per GPU, then a global
     lowest-index top-k); plugs into ``Optimizer(scorer=...)``.  Not pickled.
 
-    Sharding costs a broadcast of the candidates and the observations, a device
-    GP factorisation on every rank and an all-gather; scoring costs ~1.3 ms per
-    million candidates on one GPU.  Below ``min_shard`` candidates (skopt's
+    Sharding costs a broadcast of rank 0's prepared GP factor (the workspace
+    ``mpo_gp_prepare`` filled -- no rank factorises again), a scatter of the
+    candidates and an all-gather of the per-rank top-k rows; scoring costs ~1.3 ms
+    per million candidates on one GPU.  Below ``min_shard`` candidates (skopt's
     ``n_points`` is 10 000) the request is scored on rank 0 alone, where the
     fitted model is already resident -- the split pays only for large batches."""
 
@@ -694,7 +758,6 @@ class ShardedScorer:
             self.local_requests += 1
             return {a: idx for a, (vals, idx) in _device_topk(est, X, y_opt, acqs, xi, kappa, k).items()}
         self.sharded_requests += 1
-        req = {"Xt": est.Xt, "y": est.y, "amp": est.amp, "ls": est.length_scale, "noise": est.noise,
-               "cand": np.ascontiguousarray(X, dtype=np.float64), "y_opt": float(y_opt), "acqs": list(acqs),
-               "xi": float(xi), "kappa": float(kappa), "k": int(k)}
+        req = {"est": est, "cand": np.ascontiguousarray(X, dtype=np.float64), "y_opt": float(y_opt),
+               "acqs": list(acqs), "xi": float(xi), "kappa": float(kappa), "k": int(k)}
         return {a: idx for a, (vals, idx) in self.dist_eval.score(req).items()}

@@ -153,8 +153,9 @@ class TensorChannel:
         return out
 
     # ---- candidate slices ------------------------------------------------------
-    def scatter_rows(self, full, m, d):
-        """Rank 0's [m, d] f64 rows split as rank r's [r*m//W, (r+1)*m//W) -> this rank's block."""
+    def scatter_rows(self, full, m, d, as_tensor=False):
+        """Rank 0's [m, d] f64 rows split as rank r's [r*m//W, (r+1)*m//W) -> this rank's
+        block (numpy, or the received tensor -- on the GPU under RCCL -- with ``as_tensor``)."""
         torch = self.torch
         h = max((r + 1) * m // self.world - r * m // self.world for r in range(self.world))
         out = torch.empty((h, d), dtype=torch.float64, device=self.device)
@@ -173,4 +174,6 @@ class TensorChannel:
         else:
             self.dist.scatter(out, parts, src=0, group=self.group)
         s0, s1 = self.rank * m // self.world, (self.rank + 1) * m // self.world
+        if as_tensor:
+            return out[:s1 - s0], s0, s1
         return out.cpu().numpy()[:s1 - s0], s0, s1

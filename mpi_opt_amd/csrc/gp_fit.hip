@@ -782,7 +782,6 @@ __device__ __forceinline__ double pivot_rcp(double x) {
 // shuffle), so the bits are the same.  One barrier per two sweep steps (the LDS rounds
 // alternate between two buffers); waves of the workgroup that do not sweep must meet
 // the kSweepBarriers barriers too.  rowb: [2][64] doubles, colb: [2][64].
-constexpr int kSweepBarriers = kSwNb / 2;
 template <int CW>
 __device__ __forceinline__ void zero_cols(double (&r)[CW]) {
 #pragma unroll
@@ -860,6 +859,90 @@ __device__ __forceinline__ void pivot_block_sweep_nw(const double* __restrict__ 
     }
 }
 
+// The same sweep with FOUR steps per LDS round (r06): the pivot rows c .. c + 3 and
+// every row's columns c .. c + 3 are broadcast together, and every lane carries the
+// rows still to be pivoted through the round's earlier steps itself -- at its own CW
+// columns (Q) and at the block columns (B) -- with exactly the operations their
+// owning lanes perform (the argument of the two-step form, applied by induction over
+// the round's steps), so the bits are the one-step sweep's.  A quarter of the LDS
+// rounds and barriers of the one-step form, ~2x the FMAs of the two-step one (off the
+// pivot chain).  rowb: [2][4][32] doubles, colb: [2][32][4].
+template <int NW>
+__device__ __forceinline__ void pivot_block_sweep4_nw(const double* __restrict__ C, int k0, double* rowb,
+                                                      double* colb, int w, double (&r)[16 / NW], double& prod,
+                                                      int& bad) {
+    constexpr int CW = 16 / NW;
+    static_assert(CW % 4 == 0, "the round's four block columns must be one lane's");
+    const int lane = threadIdx.x & 63;
+    const int l = lane & 31, h = lane >> 5;
+    const int col0 = 16 * h + CW * w;
+#pragma unroll
+    for (int jj = 0; jj < CW; ++jj) r[jj] = C[(long long)(k0 + l) * kSwNb + col0 + jj];
+    prod = 1.0;
+    bad = 0;
+#pragma unroll
+    for (int c = 0; c < kSwNb; c += 4) {
+        double* rb = rowb + ((c >> 2) & 1) * (4 * kSwNb);
+        double* cl = colb + ((c >> 2) & 1) * (4 * kSwNb);
+        const int hc = c >> 4, wc = (c & 15) / CW, jc = c % CW;
+        if (h == hc && w == wc) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) cl[4 * l + s] = r[jc + s];   // A[l][c + s], before step c
+        }
+        const int ps = l - c;
+        if (ps >= 0 && ps < 4) {
+#pragma unroll
+            for (int jj = 0; jj < CW; ++jj) rb[kSwNb * ps + col0 + jj] = r[jj];
+        }
+        __syncthreads();
+        double colv[4], Q[4][CW], B[4][4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            colv[s] = cl[4 * l + s];
+#pragma unroll
+            for (int jj = 0; jj < CW; ++jj) Q[s][jj] = rb[kSwNb * s + col0 + jj];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) B[s][j] = rb[kSwNb * s + c + j];
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const bool piv = l == c + s;
+            const double pv = B[s][s];
+            if (!(pv > 0.0) || !isfinite(pv)) bad = bad ? bad : c + s + 1;
+            prod *= pv;
+            const double ip = pivot_rcp(pv);
+            const double t = colv[s] * ip;
+            const double f = piv ? ip : -t;
+            // the block's rows still to be pivoted, through step c + s as their owners
+#pragma unroll
+            for (int i = s + 1; i < 4; ++i) {
+                const double ti = B[i][s] * ip;
+#pragma unroll
+                for (int jj = 0; jj < CW; ++jj) {
+                    const double u = fma(-ti, Q[s][jj], Q[i][jj]);
+                    Q[i][jj] = col0 + jj == c + s ? ti : u;
+                }
+#pragma unroll
+                for (int j = s + 1; j < 4; ++j) B[i][j] = fma(-ti, B[s][j], B[i][j]);
+            }
+            // the lane's own row
+            if (piv) zero_cols<CW>(r);
+#pragma unroll
+            for (int j = s + 1; j < 4; ++j) colv[j] = fma(f, B[s][j], piv ? 0.0 : colv[j]);
+#pragma unroll
+            for (int jj = 0; jj < CW; ++jj) {
+                const double upd = fma(f, Q[s][jj], r[jj]);
+                r[jj] = col0 + jj == c + s ? (piv ? -ip : t) : upd;
+            }
+        }
+        asm volatile("" ::: "memory");
+    }
+}
+
+#ifndef MPO_SWEEP_STEPS
+#define MPO_SWEEP_STEPS 2
+#endif
+
 // grid (nwg, B), kUpdThreads, nwg * 4 * tpw >= the lower tile count: the whole sweep
 // step k in one launch.  Every workgroup sweeps the 32x32 pivot block of C_k itself
 // (pivot_block_sweep_nw on kSweepNW waves: the same instructions on the same data, so
@@ -889,6 +972,7 @@ __device__ __forceinline__ void step_tile_of(int t, int nt_low, int k, int& I, i
     kind = __builtin_amdgcn_readfirstlane(kind);
 }
 
+template <int SPR>   // sweep steps per LDS round: 2 (pivot_block_sweep_nw) or 4 (pivot_block_sweep4_nw)
 __global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlGroup grp, int k) {
     const int b = blockIdx.y;
     const LmlTheta& T = grp.th[b];
@@ -898,8 +982,8 @@ __global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlGroup grp, int 
     const double* Cc = p.C(k);
     __shared__ double gl[kUpdThreads / 64][16 * kSwNb];   // per wave: G_I, A-operand order
     __shared__ double Pl[kSwNb * kSwNb];                  // P^-1 of this step
-    __shared__ double rowb[2 * 2 * kSwNb];
-    __shared__ double colb[2 * 2 * kSwNb];
+    __shared__ double rowb[2 * SPR * kSwNb];
+    __shared__ double colb[2 * SPR * kSwNb];
     const int k1 = k0 + kSwNb;
     double* Cn = k1 < np ? p.C(k + 1) : nullptr;
     const int lane = threadIdx.x & 63;
@@ -939,7 +1023,10 @@ __global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlGroup grp, int 
 #pragma unroll
             for (int jj = 0; jj < CW; ++jj) r[jj] = Cc[(long long)(k0 + l) * kSwNb + col0 + jj];
         } else {
-            pivot_block_sweep_nw<kSweepNW>(Cc, k0, rowb, colb, wv, r, prod, bad);
+            if constexpr (SPR == 4)
+                pivot_block_sweep4_nw<kSweepNW>(Cc, k0, rowb, colb, wv, r, prod, bad);
+            else
+                pivot_block_sweep_nw<kSweepNW>(Cc, k0, rowb, colb, wv, r, prod, bad);
         }
 #pragma unroll
         for (int jj = 0; jj < CW; ++jj) Pl[l * kSwNb + col0 + jj] = -r[jj];
@@ -948,7 +1035,7 @@ __global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlGroup grp, int 
             if (bad && p.acc[1] == 0.0) p.acc[1] = (double)(k0 + bad);
         }
     } else if (grp.stop != 23) {
-        for (int i = 0; i < kSweepBarriers; ++i) __syncthreads();
+        for (int i = 0; i < kSwNb / SPR; ++i) __syncthreads();
     }
     __syncthreads();
     double* g = gl[wv];
@@ -1274,6 +1361,11 @@ int launch_split_group(const LmlTheta* th, int count, int d, int stop, hipStream
             const char* e = getenv("MPO_FIT_STEP_WG");
             return e && *e ? std::max(1LL, atoll(e)) : kStepWgTarget;
         }();
+        // MPO_FIT_SWEEP_STEPS (2 | 4): the pivot sweep's steps per LDS round (the same bits)
+        static const int sweep_steps = [] {
+            const char* e = getenv("MPO_FIT_SWEEP_STEPS");
+            return e && *e ? atoi(e) : MPO_SWEEP_STEPS;
+        }();
         int tpw = kUpdTilesPerWave;
         while (tpw < 16 && (long long)B * nt_low / (4LL * tpw) > wg_target) tpw *= 2;
         const int nwg = std::max(1, (nt_low + 4 * tpw - 1) / (4 * tpw));
@@ -1297,7 +1389,10 @@ int launch_split_group(const LmlTheta* th, int count, int d, int stop, hipStream
             MPO_LAUNCH_CHECK();
         }
         for (int k = 0; k < nbk; ++k) {
-            hipLaunchKernelGGL(sw_step_kernel, dim3(nwg, B), dim3(kUpdThreads), 0, s, g, k);
+            if (sweep_steps == 4)
+                hipLaunchKernelGGL(sw_step_kernel<4>, dim3(nwg, B), dim3(kUpdThreads), 0, s, g, k);
+            else
+                hipLaunchKernelGGL(sw_step_kernel<2>, dim3(nwg, B), dim3(kUpdThreads), 0, s, g, k);
             MPO_LAUNCH_CHECK();
         }
         hipLaunchKernelGGL(sw_alpha_kernel, dim3(ntile, B), dim3(256), 0, s, g);

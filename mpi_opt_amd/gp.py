@@ -78,6 +78,40 @@ class DeviceGP:
                 f"device Cholesky failed at column {self.chol_info - 1} (K not positive definite)")
         self._score_ws = None
 
+    # -- the prepared factor as plain arrays (the sharded scorer's broadcast) ----
+    _PTRS = ("xs", "ls", "alpha", "wfrag", "L", "W", "info", "wmeta", "xb")
+
+    def export_factor(self):
+        """(meta f64 [3], layout i64 [4 + len(_PTRS)], ws uint8 tensor): everything the
+        scoring kernels read, as the prepared workspace plus the offsets of the model's
+        pointers into it (-1: NULL).  ``from_factor`` on another GPU rebuilds the
+        identical model from a copy of these bytes -- no second factorisation."""
+        base = self._ws.data_ptr()
+        offs = [(-1 if not getattr(self.model, f) else getattr(self.model, f) - base) for f in self._PTRS]
+        layout = np.array([self.model.n, self.model.d, self.model.dp, self.model.np16] + offs, dtype=np.int64)
+        meta = np.array([self.model.amp, self.model.y_mean, self.model.y_std], dtype=np.float64)
+        return meta, layout, self._ws
+
+    @classmethod
+    def from_factor(cls, meta, layout, ws, device=None):
+        """A scoring-only DeviceGP over a copy of another rank's prepared workspace
+        (``export_factor``): the same model bits, addresses rebased to ``ws``."""
+        g = cls.__new__(cls)
+        g.device = _dev(device)
+        g._ws = ws
+        g.model = _lib.MpoGpModel()
+        n, d, dp, np16 = (int(v) for v in layout[:4])
+        g.model.n, g.model.d, g.model.dp, g.model.np16 = n, d, dp, np16
+        g.model.amp, g.model.y_mean, g.model.y_std = (float(v) for v in meta[:3])
+        base = ws.data_ptr()
+        for f, off in zip(cls._PTRS, layout[4:]):
+            setattr(g.model, f, None if int(off) < 0 else base + int(off))
+        g.n, g.d = n, d
+        g.amp, g.y_mean, g.y_std = float(meta[0]), float(meta[1]), float(meta[2])
+        g.chol_info = 0
+        g._score_ws = None
+        return g
+
     # -- views of device state (tests / diagnostics) --------------------------
     def _state_view(self, addr, count):
         base = self._ws.data_ptr()

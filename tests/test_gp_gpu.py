@@ -301,3 +301,28 @@ def test_acq_grad_host_requires_pinned_buffers():
     assert rc != 0 and "pinned" in _lib.lib().mpo_last_error().decode()
     fv, gv = g.acq_grad(f["C"][:3], np.ones(3, dtype=np.int32), float(f["y_opt"]))
     assert fv.shape == (3,) and gv.shape == (3, g.d) and np.all(np.isfinite(gv))
+
+
+def test_factor_copy_scores_bit_identical():
+    """The sharded scorer's broadcast (DeviceGP.export_factor -> from_factor, SURVEY
+    §8e): a GP rebuilt over a COPY of another model's prepared workspace -- at a
+    different address, no second factorisation -- scores every acquisition with the
+    same bits, top-k included."""
+    from mpi_opt_amd.gp import DeviceGP
+
+    f = load(os.path.join(GOLDEN, "gp_ei_n200_d10.npz"))
+    g = device_gp(f)
+    meta, layout, ws = g.export_factor()
+    copy = torch.empty(ws.numel() + 256, dtype=torch.uint8, device=ws.device)[256:]
+    copy.copy_(ws)
+    del g
+    h = DeviceGP.from_factor(meta, layout, copy)
+    g = device_gp(f)
+    assert h.model.xs != g.model.xs and bool(h.model.xb) == bool(g.model.xb)
+    C = torch.from_numpy(f["C"]).cuda()
+    a = g.score(C, float(f["y_opt"]), acqs=("EI", "PI", "LCB"), k=5)
+    b = h.score(C, float(f["y_opt"]), acqs=("EI", "PI", "LCB"), k=5)
+    assert torch.equal(a["mu"], b["mu"]) and torch.equal(a["sd"], b["sd"])
+    for acq in ("EI", "PI", "LCB"):
+        assert torch.equal(a["values"][acq], b["values"][acq])
+        assert torch.equal(a["topk"][acq][0], b["topk"][acq][0])

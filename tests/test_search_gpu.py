@@ -162,6 +162,13 @@ def _nccl_search3_worker(port, tmp, q):
         want = local_topk(req, 0, len(req["cand"]), device=torch.device("cuda", 0))
         score_ok = all(np.array_equal(got[a][1], want[a][1]) and np.array_equal(got[a][0], want[a][0])
                        for a in req["acqs"])
+        # a fitted model's round: its prepared factor crosses RCCL as raw words
+        from mpi_opt_amd.optimizer import GPModel
+
+        est = GPModel(req["Xt"], req["y"], req["amp"], req["ls"], req["noise"], device=torch.device("cuda", 0))
+        fac = ev.score({"est": est, **{k: req[k] for k in ("cand", "y_opt", "acqs", "xi", "kappa", "k")}})
+        score_ok = score_ok and all(np.array_equal(fac[a][1], want[a][1]) and np.array_equal(fac[a][0], want[a][0])
+                                    for a in req["acqs"])
         maps = open("/proc/self/maps").read()
         rccl = sorted({ln.split()[-1] for ln in maps.splitlines() if "librccl" in ln})
         q.put({k: rep[k] for k in ("told_params", "told_foms", "trained_params", "populations", "best_fom",
