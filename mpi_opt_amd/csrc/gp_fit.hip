@@ -539,12 +539,8 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 __host__ __device__ inline long long sw_np(int n) { return (n + kSwNb - 1) / kSwNb * kSwNb; }
 
-#ifndef MPO_SWEEP_NW
-#define MPO_SWEEP_NW 4
-#endif
 constexpr int kSplitMinN = 48;    // past it the split beats both single-workgroup kernels (0.09 vs 0.20 ms at n = 64)
-constexpr int kUpdThreads = 256;
-constexpr int kSweepNW = MPO_SWEEP_NW;   // waves that share the pivot sweep of a step (2 or 4)
+constexpr int kStepWaves = 4;   // waves per sw_step workgroup; all of them share the pivot sweep
 constexpr int kUpdTilesPerWave = 1;   // one lower tile per wave: latency-bound steps want many waves
 // sw_step workgroups per launch before waves take more tiles (one per CU).  Chains at
 // n = 448, 8 / 16 threads: 72 / 82 refits/s with one tile per wave, 93 / 120 at 256,
@@ -559,12 +555,16 @@ constexpr long long kStepWgTarget = 256;
 __host__ __device__ inline long long ss_ws_doubles(int n, int d) {
     auto al = [](long long x) { return (x + 31) & ~31LL; };
     const long long np = sw_np(n);
-    return al((long long)n * d) + al(np) + np * np + 2 * np * kSwNb + kSwNb * kSwNb + 32;
+    return al((long long)n * d) + al(np) + np * np + 2 * np * kSwNb + kSwNb * kSwNb + 32 + kSwNb * kSwNb;
 }
 
 struct SsPtrs {
-    double *xs, *alpha, *A, *C0, *C1, *P, *acc;   // acc[0] = log det, acc[1] = failure column (as double)
+    // acc[0] = log det, acc[1] = failure column (as double), acc[2] the pair kernel's
+    // arrival counter, acc[4] = y . alpha (sw_pairs_final), acc[8 ..] diagnostics, acc[16 + i] / acc[18 + i] the look-ahead's
+    // log det / failure slots; P, P2: the look-ahead's P^-1 buffers (Pg(k & 1))
+    double *xs, *alpha, *A, *C0, *C1, *P, *acc, *P2;
     __device__ double* C(int k) const { return (k & 1) ? C1 : C0; }
+    __device__ double* Pg(int i) const { return i ? P2 : P; }
 };
 
 // The split sweep's launches take a table of thetas (LmlGroup, by value in the
@@ -607,7 +607,16 @@ __device__ __forceinline__ SsPtrs ss_ptrs_t(const LmlTheta& t, int d) {
     p.C1 = p.C0 + np * kSwNb;
     p.P = p.C1 + np * kSwNb;
     p.acc = p.P + kSwNb * kSwNb;
+    p.P2 = p.acc + 32;
     return p;
+}
+
+template <int DP>
+__device__ __forceinline__ void ss_theta_p(const double* th, int d, double& amp, double& noise, double (&ls)[DP]) {
+    amp = exp(th[0]);
+    noise = exp(th[d + 1]);
+#pragma unroll
+    for (int c = 0; c < DP; ++c) ls[c] = c < d ? exp(th[1 + c]) : 1.0;
 }
 
 template <int DP>
@@ -698,18 +707,38 @@ __global__ __launch_bounds__(1024) void sw_xs_build_kernel(LmlGroup grp) {
     const int n = T.n, d = grp.d, np = (int)sw_np(n);
     if ((int)blockIdx.x >= np / 16) return;   // a larger problem of the group sized the grid
     const SsPtrs p = ss_ptrs_t(T, grp.d);
-    double amp, noise, ls[DP];
-    ss_theta_t<DP>(T, grp.d, amp, noise, ls, true);   // host-staged call: theta straight from pinned memory
-    if (T.theta_src && blockIdx.x == 0 && threadIdx.x < d + 2)   // ... and the device copy the later kernels read
-        const_cast<double*>(T.theta)[threadIdx.x] = T.theta_src[threadIdx.x];
+    // host-staged call: theta straight from pinned memory, read once per workgroup (one
+    // PCIe read per value, not one per wave) and shared through the LDS; workgroup 0
+    // writes the device copy the later kernels read
+    // The X rows are loaded first, so that their latency overlaps the theta read (the
+    // fused build runs only while rows * d <= np * DP <= 8192: at most 8 per thread).
+    __shared__ double thl[34];
     const int rows = min(n, 16 * (int)blockIdx.x + 16);
-    for (int e = threadIdx.x; e < rows * d; e += blockDim.x) {
+    constexpr int kXPer = 8;
+    double xv[kXPer];
+#pragma unroll
+    for (int u = 0; u < kXPer; ++u) {
+        const int e = threadIdx.x + u * 1024;
+        xv[u] = e < rows * d ? T.X[e] : 0.0;
+    }
+    if (threadIdx.x < d + 2) {
+        const double v = T.theta_src ? T.theta_src[threadIdx.x] : T.theta[threadIdx.x];
+        thl[threadIdx.x] = v;
+        if (T.theta_src && blockIdx.x == 0) const_cast<double*>(T.theta)[threadIdx.x] = v;
+    }
+    __syncthreads();
+    double amp, noise, ls[DP];
+    ss_theta_p<DP>(thl, grp.d, amp, noise, ls);
+#pragma unroll
+    for (int u = 0; u < kXPer; ++u) {
+        const int e = threadIdx.x + u * 1024;
+        if (e >= rows * d) break;
         const int i = e / d, c = e % d;
         double lc = 1.0;
 #pragma unroll
         for (int q = 0; q < DP; ++q)
             if (q == c) lc = ls[q];
-        const double v = T.X[e] / lc;
+        const double v = xv[u] / lc;
         xsl[i * DP + c] = v;
         if (i >= 16 * (int)blockIdx.x) p.xs[e] = v;
     }
@@ -717,6 +746,10 @@ __global__ __launch_bounds__(1024) void sw_xs_build_kernel(LmlGroup grp) {
         p.acc[0] = 0.0;
         p.acc[1] = 0.0;
         *reinterpret_cast<unsigned*>(p.acc + 2) = 0u;
+        if (grp.stop == 24) {   // diagnostics only: sw_step_kernel's timestamps (step_stamps)
+            unsigned long long* st = reinterpret_cast<unsigned long long*>(p.acc + 8);
+            st[0] = ~0ULL; st[1] = 0; st[2] = ~0ULL; st[3] = 0; st[6] = 0;
+        }
     }
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -775,13 +808,12 @@ __device__ __forceinline__ double pivot_rcp(double x) {
 // written as exec-masked v_mov_b64 (a branch): as plain stores the compiler
 // if-converts the branch into two v_cndmask_b32 per double.
 //
-// The sweep on NW waves (2 or 4): wave w's lane l + 32 h holds the CW =
+// The sweep on NW waves (2, 4 or 8): wave w's lane l + 32 h holds the CW =
 // 16 / NW columns [16 h + CW w, 16 h + CW w + CW) of row l, so each lane issues 1 / NW
 // of the FMAs.  Every element sees exactly the operations of the one-wave form (the
 // pivot rows and the pivot columns' entries go through the LDS instead of a cross-lane
 // shuffle), so the bits are the same.  One barrier per two sweep steps (the LDS rounds
-// alternate between two buffers); waves of the workgroup that do not sweep must meet
-// the kSweepBarriers barriers too.  rowb: [2][64] doubles, colb: [2][64].
+// alternate between two buffers).  rowb: [2][64] doubles, colb: [2][64].
 template <int CW>
 __device__ __forceinline__ void zero_cols(double (&r)[CW]) {
 #pragma unroll
@@ -859,97 +891,13 @@ __device__ __forceinline__ void pivot_block_sweep_nw(const double* __restrict__ 
     }
 }
 
-// The same sweep with FOUR steps per LDS round (r06): the pivot rows c .. c + 3 and
-// every row's columns c .. c + 3 are broadcast together, and every lane carries the
-// rows still to be pivoted through the round's earlier steps itself -- at its own CW
-// columns (Q) and at the block columns (B) -- with exactly the operations their
-// owning lanes perform (the argument of the two-step form, applied by induction over
-// the round's steps), so the bits are the one-step sweep's.  A quarter of the LDS
-// rounds and barriers of the one-step form, ~2x the FMAs of the two-step one (off the
-// pivot chain).  rowb: [2][4][32] doubles, colb: [2][32][4].
-template <int NW>
-__device__ __forceinline__ void pivot_block_sweep4_nw(const double* __restrict__ C, int k0, double* rowb,
-                                                      double* colb, int w, double (&r)[16 / NW], double& prod,
-                                                      int& bad) {
-    constexpr int CW = 16 / NW;
-    static_assert(CW % 4 == 0, "the round's four block columns must be one lane's");
-    const int lane = threadIdx.x & 63;
-    const int l = lane & 31, h = lane >> 5;
-    const int col0 = 16 * h + CW * w;
-#pragma unroll
-    for (int jj = 0; jj < CW; ++jj) r[jj] = C[(long long)(k0 + l) * kSwNb + col0 + jj];
-    prod = 1.0;
-    bad = 0;
-#pragma unroll
-    for (int c = 0; c < kSwNb; c += 4) {
-        double* rb = rowb + ((c >> 2) & 1) * (4 * kSwNb);
-        double* cl = colb + ((c >> 2) & 1) * (4 * kSwNb);
-        const int hc = c >> 4, wc = (c & 15) / CW, jc = c % CW;
-        if (h == hc && w == wc) {
-#pragma unroll
-            for (int s = 0; s < 4; ++s) cl[4 * l + s] = r[jc + s];   // A[l][c + s], before step c
-        }
-        const int ps = l - c;
-        if (ps >= 0 && ps < 4) {
-#pragma unroll
-            for (int jj = 0; jj < CW; ++jj) rb[kSwNb * ps + col0 + jj] = r[jj];
-        }
-        __syncthreads();
-        double colv[4], Q[4][CW], B[4][4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            colv[s] = cl[4 * l + s];
-#pragma unroll
-            for (int jj = 0; jj < CW; ++jj) Q[s][jj] = rb[kSwNb * s + col0 + jj];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) B[s][j] = rb[kSwNb * s + c + j];
-        }
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const bool piv = l == c + s;
-            const double pv = B[s][s];
-            if (!(pv > 0.0) || !isfinite(pv)) bad = bad ? bad : c + s + 1;
-            prod *= pv;
-            const double ip = pivot_rcp(pv);
-            const double t = colv[s] * ip;
-            const double f = piv ? ip : -t;
-            // the block's rows still to be pivoted, through step c + s as their owners
-#pragma unroll
-            for (int i = s + 1; i < 4; ++i) {
-                const double ti = B[i][s] * ip;
-#pragma unroll
-                for (int jj = 0; jj < CW; ++jj) {
-                    const double u = fma(-ti, Q[s][jj], Q[i][jj]);
-                    Q[i][jj] = col0 + jj == c + s ? ti : u;
-                }
-#pragma unroll
-                for (int j = s + 1; j < 4; ++j) B[i][j] = fma(-ti, B[s][j], B[i][j]);
-            }
-            // the lane's own row
-            if (piv) zero_cols<CW>(r);
-#pragma unroll
-            for (int j = s + 1; j < 4; ++j) colv[j] = fma(f, B[s][j], piv ? 0.0 : colv[j]);
-#pragma unroll
-            for (int jj = 0; jj < CW; ++jj) {
-                const double upd = fma(f, Q[s][jj], r[jj]);
-                r[jj] = col0 + jj == c + s ? (piv ? -ip : t) : upd;
-            }
-        }
-        asm volatile("" ::: "memory");
-    }
-}
-
-#ifndef MPO_SWEEP_STEPS
-#define MPO_SWEEP_STEPS 2
-#endif
-
-// grid (nwg, B), kUpdThreads, nwg * 4 * tpw >= the lower tile count: the whole sweep
+// grid (nwg, B), 64 NW threads, nwg * NW * tpw >= the lower tile count: the whole sweep
 // step k in one launch.  Every workgroup sweeps the 32x32 pivot block of C_k itself
-// (pivot_block_sweep_nw on kSweepNW waves: the same instructions on the same data, so
+// (pivot_block_sweep_nw on its NW waves: the same instructions on the same data, so
 // the same P^-1 bits in every workgroup) into its LDS while its waves' first tile
 // operands land; then each wave forms G_I = C_I P^-1 (16 MFMAs, turned into the
 // A-operand layout through its LDS slice) and updates its tile -- tpw tiles per wave,
-// tiles t, t + 4 nwg, ...; the diagonal tile (I, I) also writes G_I into block column
+// tiles t, t + NW nwg, ...; the diagonal tile (I, I) also writes G_I into block column
 // k of A (and row I's entries of C_{k+1}), tile (I, I) of block k writes -P^-1 there.
 // Workgroup 0 keeps the log det and the failure column.  A tile's arithmetic does not
 // depend on which wave computes it, so tpw changes no bits: it trades latency (one
@@ -972,29 +920,159 @@ __device__ __forceinline__ void step_tile_of(int t, int nt_low, int k, int& I, i
     kind = __builtin_amdgcn_readfirstlane(kind);
 }
 
-template <int SPR>   // sweep steps per LDS round: 2 (pivot_block_sweep_nw) or 4 (pivot_block_sweep4_nw)
-__global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlGroup grp, int k) {
+// MPO_FIT_DEBUG=24 (diagnostics only): step 2 of theta 0 records, in its acc[8 ..]
+// words, the first / last workgroup entry and exit (wall clock, 100 MHz), workgroup
+// 0's shader cycles to the end of the sweep and from there to its exit, and step 1's
+// last exit -- the launch gap, the dispatch spread and the sweep's share of a step
+__device__ __forceinline__ void step_stamp(const LmlGroup& grp, const SsPtrs& p, int k, int at) {
+    if (grp.stop != 24 || blockIdx.y != 0 || (threadIdx.x & 255) != 0) return;
+    unsigned long long* st = reinterpret_cast<unsigned long long*>(p.acc + 8);
+    const unsigned long long t = wall_clock64();
+    if (k == 1 && at == 2) atomicMax(st + 6, t);
+    if (k != 2) return;
+    if (at == 0) { atomicMin(st + 0, t); atomicMax(st + 1, t); }
+    if (at == 2) { atomicMin(st + 2, t); atomicMax(st + 3, t); }
+}
+
+// One lower 16x16 tile's update A_IJ -= G_I C_J^T with G_I = C_I P^-1 (16 MFMAs,
+// turned into the A-operand layout through the wave's LDS slice g, which keeps G_I
+// for the caller); av / cb: rows 16 I / 16 J of C_k in MFMA operand order.
+__device__ __forceinline__ void tile_update(const double (&av)[8], const double (&cb)[8], f64x4& acc,
+                                            const double* Pl, double* g, int lane) {
+    {
+        double b0[8], b1[8];
+        const double* br = Pl + (lane >> 4) * kSwNb + (lane & 15);
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            b0[ks] = br[4 * ks * kSwNb];
+            b1[ks] = br[4 * ks * kSwNb + 16];
+        }
+        f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ks], b0[ks], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ks], b1[ks], acc1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int rr = (lane >> 4) + 4 * q, c0 = lane & 15, c1 = 16 + c0;
+            g[(c0 >> 2) * 64 + rr + 16 * (c0 & 3)] = acc0[q];
+            g[(c1 >> 2) * 64 + rr + 16 * (c1 & 3)] = acc1[q];
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's G_I stores (LDS ops of one wave complete in order)
+    double ga[8];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) ga[ks] = g[ks * 64 + lane];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-ga[ks], cb[ks], acc, 0, 0, 0);
+}
+
+// The pivot sweep of rows row0 .. row0 + 31 of src (row-major [.][32]: C_k in global
+// memory, or the look-ahead's LDS copy of a diagonal block) on all NW waves of the
+// workgroup; -P^-1 lands in dst[32][32] (LDS or global), thread 0 returns the product
+// of the pivots and the first bad one.
+template <int NW>
+__device__ __forceinline__ void sweep_block(const LmlGroup& grp, const double* src, int row0, double* rowb,
+                                            double* colb, double* dst, double& prod, int& bad) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    constexpr int CW = 16 / NW;
+    const int l = lane & 31, h = lane >> 5, col0 = 16 * h + CW * wv;
+    double r[CW];
+    if (grp.stop == 23) {   // diagnostics only (MPO_FIT_DEBUG=23): the sweep skipped, timing of the rest
+        prod = 1.0;
+        bad = 0;
+#pragma unroll
+        for (int jj = 0; jj < CW; ++jj) r[jj] = src[(long long)(row0 + l) * kSwNb + col0 + jj];
+    } else {
+        pivot_block_sweep_nw<NW>(src, row0, rowb, colb, wv, r, prod, bad);
+    }
+#pragma unroll
+    for (int jj = 0; jj < CW; ++jj) dst[l * kSwNb + col0 + jj] = -r[jj];
+}
+
+// grid (nwg [+ 1], B), 64 NW threads: sweep step k.  LA (look-ahead, r06): the extra first
+// workgroup computes the three lower tiles of block k + 1's diagonal block with this
+// step's update (tile_update: the same instructions as the workgroups that write them,
+// so the same bits), sweeps that block from LDS and writes P_{k+1}^-1 (ws Pg[(k+1)&1])
+// and its log det / failure slot; the other workgroups of step k > 0 then load P_k^-1
+// instead of sweeping it.  The serial sweep leaves every other workgroup's path, and a
+// step ends with the look-ahead's sweep instead of (sweep + update + the slowest
+// workgroup's tail).  The first tile workgroup adds the slots to the log det in step
+// order (the same sum as before).  Step 0 still sweeps P_0 in every workgroup.
+template <bool LA, int NW>
+__global__ __launch_bounds__(64 * NW) void sw_step_kernel(LmlGroup grp, int k) {
     const int b = blockIdx.y;
     const LmlTheta& T = grp.th[b];
     const int np = (int)sw_np(T.n), ntile = np / 16, k0 = k * kSwNb;
     if (k0 >= np) return;                     // this problem has fewer pivot blocks
     const SsPtrs p = ss_ptrs_t(T, grp.d);
+    step_stamp(grp, p, k, 0);
+    const long long c_enter = grp.stop == 24 ? clock64() : 0;
     const double* Cc = p.C(k);
-    __shared__ double gl[kUpdThreads / 64][16 * kSwNb];   // per wave: G_I, A-operand order
+    __shared__ double gl[NW][16 * kSwNb];                 // per wave: G_I, A-operand order
     __shared__ double Pl[kSwNb * kSwNb];                  // P^-1 of this step
-    __shared__ double rowb[2 * SPR * kSwNb];
-    __shared__ double colb[2 * SPR * kSwNb];
+    __shared__ double rowb[2 * 2 * kSwNb];
+    __shared__ double colb[2 * 2 * kSwNb];
     const int k1 = k0 + kSwNb;
     double* Cn = k1 < np ? p.C(k + 1) : nullptr;
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
+    double* g = gl[wv];
+    if (LA && blockIdx.x == 0) {
+        // ---- the look-ahead workgroup (dispatched first): P_{k+1}^-1
+        __shared__ double Dl[LA ? kSwNb * kSwNb : 1];     // C_{k+1}'s diagonal block
+        if (k1 >= np) return;
+        double prod;
+        int bad;
+        const int I = 2 * k + 2 + (wv > 0), J = 2 * k + 2 + (wv == 2);
+        double av[8], cb[8];
+        f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+        if (wv < 3) {
+            const double* ar = Cc + (long long)(16 * I + (lane & 15)) * kSwNb + (lane >> 4);
+            const double* cr = Cc + (long long)(16 * J + (lane & 15)) * kSwNb + (lane >> 4);
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) {
+                av[ks] = ar[4 * ks];
+                cb[ks] = cr[4 * ks];
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] = p.A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)];
+        }
+        if (k == 0) {
+            sweep_block<NW>(grp, Cc, k0, rowb, colb, Pl, prod, bad);
+        } else {
+            const double* pg = p.Pg((k) & 1);
+            for (int e = threadIdx.x; e < kSwNb * kSwNb; e += 64 * NW) Pl[e] = pg[e];
+        }
+        __syncthreads();
+        if (wv < 3) {
+            tile_update(av, cb, acc, Pl, g, lane);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int i = 16 * I + (lane >> 4) + 4 * q - k1, j = 16 * J + (lane & 15) - k1;
+                if (i < j) continue;                                    // upper half of a diagonal tile
+                Dl[i * kSwNb + j] = acc[q];
+                Dl[j * kSwNb + i] = acc[q];
+            }
+        }
+        __syncthreads();
+        sweep_block<NW>(grp, Dl, 0, rowb, colb, p.Pg((k + 1) & 1), prod, bad);
+        if (threadIdx.x == 0) {
+            p.acc[16 + ((k + 1) & 1)] = log(prod);
+            p.acc[18 + ((k + 1) & 1)] = (double)bad;
+        }
+        return;
+    }
     const int nt_low = ntile * (ntile + 1) / 2;
-    const int stride = (int)gridDim.x * (kUpdThreads / 64);
-    int t = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kUpdThreads / 64) + wv));
+    const int wg = (int)blockIdx.x - (LA ? 1 : 0);       // this workgroup among the tile workgroups
+    const int stride = ((int)gridDim.x - (LA ? 1 : 0)) * NW;
+    int t = __builtin_amdgcn_readfirstlane(wg * NW + wv);
     int I, J, kind;
     step_tile_of(t, nt_low, k, I, J, kind);
-    // the tile's operands that do not depend on P^-1: waves 1-3 load their first tile's
-    // while wave 0 sweeps (if / else, so that they are not live across the sweep's registers)
+    // the tile's operands that do not depend on P^-1, loaded while the sweep runs
+    // (or P^-1 arrives)
     double av[8], cb[8];
     f64x4 acc = {0.0, 0.0, 0.0, 0.0};
     auto load_tile = [&]() {
@@ -1009,36 +1087,26 @@ __global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlGroup grp, int 
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc[q] = p.A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)];
     };
-    // every wave issues its first tile's loads, then the kSweepNW sweeping waves sweep
-    // (pivot_block_sweep_nw) while they land; any other waves meet the sweep's barriers
     load_tile();
-    if (wv < kSweepNW) {
-        constexpr int CW = 16 / kSweepNW;
-        const int l = lane & 31, h = lane >> 5, col0 = 16 * h + CW * wv;
-        double r[CW], prod;
+    if (!LA || k == 0) {
+        double prod;
         int bad;
-        if (grp.stop == 23) {   // diagnostics only (MPO_FIT_DEBUG=23): the sweep skipped, timing of the rest
-            prod = 1.0;
-            bad = 0;
-#pragma unroll
-            for (int jj = 0; jj < CW; ++jj) r[jj] = Cc[(long long)(k0 + l) * kSwNb + col0 + jj];
-        } else {
-            if constexpr (SPR == 4)
-                pivot_block_sweep4_nw<kSweepNW>(Cc, k0, rowb, colb, wv, r, prod, bad);
-            else
-                pivot_block_sweep_nw<kSweepNW>(Cc, k0, rowb, colb, wv, r, prod, bad);
-        }
-#pragma unroll
-        for (int jj = 0; jj < CW; ++jj) Pl[l * kSwNb + col0 + jj] = -r[jj];
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
+        sweep_block<NW>(grp, Cc, k0, rowb, colb, Pl, prod, bad);
+        if (wg == 0 && threadIdx.x == 0) {
             p.acc[0] += log(prod);
             if (bad && p.acc[1] == 0.0) p.acc[1] = (double)(k0 + bad);
         }
-    } else if (grp.stop != 23) {
-        for (int i = 0; i < kSwNb / SPR; ++i) __syncthreads();
+    } else {
+        const double* pg = p.Pg(k & 1);
+        for (int e = threadIdx.x; e < kSwNb * kSwNb; e += 64 * NW) Pl[e] = pg[e];
+        if (wg == 0 && threadIdx.x == 0) {
+            p.acc[0] += p.acc[16 + (k & 1)];
+            const int bad = (int)p.acc[18 + (k & 1)];
+            if (bad && p.acc[1] == 0.0) p.acc[1] = (double)(k0 + bad);
+        }
     }
     __syncthreads();
-    double* g = gl[wv];
+    const long long c_swept = grp.stop == 24 ? clock64() : 0;
     for (;;) {
         if (kind == 1) {
 #pragma unroll
@@ -1047,37 +1115,15 @@ __global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlGroup grp, int 
                 p.A[(long long)i * np + k0 + c] = -Pl[(i - k0) * kSwNb + c];
             }
         } else if (kind == 2) {
-            {
-                double b0[8], b1[8];
-                const double* br = Pl + (lane >> 4) * kSwNb + (lane & 15);
+            tile_update(av, cb, acc, Pl, g, lane);
+            // with the look-ahead, block k + 1's diagonal tiles are not stored to A: those
+            // stores are dead (step k + 1 overwrites the block with -P^-1) and the
+            // look-ahead workgroup of this step reads the block's step-k input there
+            if (!LA || (I >> 1) != k + 1 || (J >> 1) != k + 1) {
 #pragma unroll
-                for (int ks = 0; ks < 8; ++ks) {
-                    b0[ks] = br[4 * ks * kSwNb];
-                    b1[ks] = br[4 * ks * kSwNb + 16];
-                }
-                f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                for (int ks = 0; ks < 8; ++ks) {
-                    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ks], b0[ks], acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ks], b1[ks], acc1, 0, 0, 0);
-                }
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int rr = (lane >> 4) + 4 * q, c0 = lane & 15, c1 = 16 + c0;
-                    g[(c0 >> 2) * 64 + rr + 16 * (c0 & 3)] = acc0[q];
-                    g[(c1 >> 2) * 64 + rr + 16 * (c1 & 3)] = acc1[q];
-                }
+                for (int q = 0; q < 4; ++q)
+                    p.A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)] = acc[q];
             }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's G_I stores (LDS ops of one wave complete in order)
-            double ga[8];
-#pragma unroll
-            for (int ks = 0; ks < 8; ++ks) ga[ks] = g[ks * 64 + lane];
-#pragma unroll
-            for (int ks = 0; ks < 8; ++ks)
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-ga[ks], cb[ks], acc, 0, 0, 0);
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                p.A[(long long)(16 * I + (lane >> 4) + 4 * q) * np + 16 * J + (lane & 15)] = acc[q];
             if (Cn && ((J >> 1) == k + 1 || (I >> 1) == k + 1)) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -1107,6 +1153,14 @@ __global__ __launch_bounds__(kUpdThreads) void sw_step_kernel(LmlGroup grp, int 
         step_tile_of(t, nt_low, k, I, J, kind);
         acc = f64x4{0.0, 0.0, 0.0, 0.0};
         load_tile();
+    }
+    if (grp.stop == 24) {
+        step_stamp(grp, p, k, 2);
+        if (k == 2 && wg == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+            unsigned long long* st = reinterpret_cast<unsigned long long*>(p.acc + 8);
+            st[4] = (unsigned long long)(c_swept - c_enter);
+            st[5] = (unsigned long long)(clock64() - c_swept);
+        }
     }
 }
 
@@ -1284,6 +1338,14 @@ __global__ __launch_bounds__(256) void sw_pairs_final_kernel(LmlGroup grp) {
     double g[DP + 2];
 #pragma unroll
     for (int c = 0; c < DP + 2; ++c) g[c] = 0.0;
+    // y . alpha off the tail: workgroup 0's wave 0 forms it first (the same per-lane fma
+    // order and butterfly as the last workgroup once did) and leaves it in acc[4]
+    if (blockIdx.x == 0 && wave == 0 && !failed) {
+        double ya = 0.0;
+        for (int i = lane; i < n; i += 64) ya = fma(T.y[i], p.alpha[i], ya);
+        ya = wave_sum_bcast(ya);
+        if (lane == 0) p.acc[4] = ya;
+    }
     if (!failed) pair_rows<DP>(p, n, d, np, amp, noise, gw, nw, lane, g);
 #pragma unroll
     for (int c = 0; c < DP + 2; ++c) {
@@ -1317,10 +1379,8 @@ __global__ __launch_bounds__(256) void sw_pairs_final_kernel(LmlGroup grp) {
         pl[e] = T.partials[e];
     __syncthreads();
     if (wave != 0) return;
-    double ya = 0.0;
-    for (int i = lane; i < n; i += 64) ya = fma(T.y[i], p.alpha[i], ya);
-    ya = wave_sum_bcast(ya);
     if (lane == 0) {
+        const double ya = p.acc[4];
         T.lml[0] = -0.5 * ya - 0.5 * p.acc[0] - 0.5 * n * kLog2Pi;
         T.info[0] = 0;
     }
@@ -1361,16 +1421,23 @@ int launch_split_group(const LmlTheta* th, int count, int d, int stop, hipStream
             const char* e = getenv("MPO_FIT_STEP_WG");
             return e && *e ? std::max(1LL, atoll(e)) : kStepWgTarget;
         }();
-        // MPO_FIT_SWEEP_STEPS (2 | 4): the pivot sweep's steps per LDS round (the same bits)
-        static const int sweep_steps = [] {
-            const char* e = getenv("MPO_FIT_SWEEP_STEPS");
-            return e && *e ? atoi(e) : MPO_SWEEP_STEPS;
+        // MPO_FIT_LOOKAHEAD (0 | 1): P_{k+1}^-1 swept by one extra workgroup of step k;
+        // MPO_FIT_STEP_WAVES (2 | 4 | 8): waves per step workgroup, all of which share the
+        // pivot sweep (the same bits either way)
+        static const int lookahead = [] {
+            const char* e = getenv("MPO_FIT_LOOKAHEAD");
+            return e && *e ? atoi(e) : 1;
+        }();
+        static const int nw = [] {
+            const char* e = getenv("MPO_FIT_STEP_WAVES");
+            const int v = e && *e ? atoi(e) : kStepWaves;
+            return v == 2 || v == 8 ? v : 4;
         }();
         int tpw = kUpdTilesPerWave;
-        while (tpw < 16 && (long long)B * nt_low / (4LL * tpw) > wg_target) tpw *= 2;
-        const int nwg = std::max(1, (nt_low + 4 * tpw - 1) / (4 * tpw));
+        while (tpw < 16 && (long long)B * nt_low / ((long long)nw * tpw) > wg_target) tpw *= 2;
+        const int nwg = std::max(1, (nt_low + nw * tpw - 1) / (nw * tpw));
         const size_t xs_lds = (size_t)np * DP * sizeof(double);
-        const bool fuse_build = xs_lds <= 64 * 1024;
+        const bool fuse_build = xs_lds <= 64 * 1024;   // np * DP <= 8192: sw_xs_build_kernel's 8 X values per thread
         if (fuse_build) {
             auto kb = sw_xs_build_kernel<DP>;
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kb), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1389,10 +1456,16 @@ int launch_split_group(const LmlTheta* th, int count, int d, int stop, hipStream
             MPO_LAUNCH_CHECK();
         }
         for (int k = 0; k < nbk; ++k) {
-            if (sweep_steps == 4)
-                hipLaunchKernelGGL(sw_step_kernel<4>, dim3(nwg, B), dim3(kUpdThreads), 0, s, g, k);
-            else
-                hipLaunchKernelGGL(sw_step_kernel<2>, dim3(nwg, B), dim3(kUpdThreads), 0, s, g, k);
+            const dim3 grid(nwg + (lookahead ? 1 : 0), B), block(64 * nw);
+            if (lookahead) {
+                if (nw == 8) hipLaunchKernelGGL((sw_step_kernel<true, 8>), grid, block, 0, s, g, k);
+                else if (nw == 2) hipLaunchKernelGGL((sw_step_kernel<true, 2>), grid, block, 0, s, g, k);
+                else hipLaunchKernelGGL((sw_step_kernel<true, 4>), grid, block, 0, s, g, k);
+            } else {
+                if (nw == 8) hipLaunchKernelGGL((sw_step_kernel<false, 8>), grid, block, 0, s, g, k);
+                else if (nw == 2) hipLaunchKernelGGL((sw_step_kernel<false, 2>), grid, block, 0, s, g, k);
+                else hipLaunchKernelGGL((sw_step_kernel<false, 4>), grid, block, 0, s, g, k);
+            }
             MPO_LAUNCH_CHECK();
         }
         hipLaunchKernelGGL(sw_alpha_kernel, dim3(ntile, B), dim3(256), 0, s, g);
