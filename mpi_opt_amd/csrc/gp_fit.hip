@@ -783,6 +783,91 @@ __global__ __launch_bounds__(1024) void sw_xs_build_kernel(LmlGroup grp) {
     }
 }
 
+// grid (ntile (ntile + 1) / 2, B), 256 threads (r06): sw_xs_build_kernel's work as one
+// lower 16x16 tile (I, J) of K per workgroup -- every workgroup divides only its 32 X
+// rows by the length scales, and the row-tiled form's last workgroup no longer
+// evaluates a whole 16-row band on one CU.  Each element is formed by the same
+// expression from the same xs values (the same bits); the diagonal tiles write the xs
+// rows for the later kernels, tile (0, 0) the accumulators and the theta device copy.
+template <int DP>
+__global__ __launch_bounds__(256) void sw_xs_build_tile_kernel(LmlGroup grp) {
+    const int b = blockIdx.y;
+    const LmlTheta& T = grp.th[b];
+    const int n = T.n, d = grp.d, np = (int)sw_np(n), ntile = np / 16;
+    const int t = blockIdx.x;
+    if (t >= ntile * (ntile + 1) / 2) return;   // a larger problem of the group sized the grid
+    int I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+    while (I * (I + 1) / 2 > t) --I;
+    while ((I + 1) * (I + 2) / 2 <= t) ++I;
+    const int J = t - I * (I + 1) / 2;
+    const SsPtrs p = ss_ptrs_t(T, grp.d);
+    __shared__ double thl[34];
+    __shared__ double xsl[2][16][DP];   // xs rows 16 I .., 16 J ..
+    // the two row blocks' X first (their latency overlaps the theta read)
+    const int e0 = threadIdx.x, half = 16 * DP;   // 256 threads cover 2 x 16 x DP <= 1024 elements in 4 passes
+    double xv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int e = e0 + 256 * u, w = e / half, r = (e % half) / DP, c = e % DP;
+        const int row = 16 * (w ? J : I) + r;
+        xv[u] = (e < 2 * half && c < d && row < n) ? T.X[(long long)row * d + c] : 0.0;
+    }
+    if (threadIdx.x < d + 2) {
+        const double v = T.theta_src ? T.theta_src[threadIdx.x] : T.theta[threadIdx.x];
+        thl[threadIdx.x] = v;
+        if (T.theta_src && t == 0) const_cast<double*>(T.theta)[threadIdx.x] = v;
+    }
+    if (t == 0 && threadIdx.x == 0) {
+        p.acc[0] = 0.0;
+        p.acc[1] = 0.0;
+        *reinterpret_cast<unsigned*>(p.acc + 2) = 0u;
+        if (grp.stop == 24) {   // diagnostics only: sw_step_kernel's timestamps (step_stamps)
+            unsigned long long* st = reinterpret_cast<unsigned long long*>(p.acc + 8);
+            st[0] = ~0ULL; st[1] = 0; st[2] = ~0ULL; st[3] = 0; st[6] = 0;
+        }
+    }
+    __syncthreads();
+    double amp, noise, ls[DP];
+    ss_theta_p<DP>(thl, grp.d, amp, noise, ls);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int e = e0 + 256 * u, w = e / half, r = (e % half) / DP, c = e % DP;
+        if (e >= 2 * half) break;
+        double lc = 1.0;
+#pragma unroll
+        for (int q = 0; q < DP; ++q)
+            if (q == c) lc = ls[q];
+        const int row = 16 * (w ? J : I) + r;
+        const double v = (c < d && row < n) ? xv[u] / lc : 0.0;
+        xsl[w][r][c] = v;
+        if (w == 0 && I == J && c < d && row < n) p.xs[(long long)row * d + c] = v;
+    }
+    __syncthreads();
+    const int r = threadIdx.x >> 4, cc = threadIdx.x & 15;
+    const int i = 16 * I + r, j = 16 * J + cc;
+    double v;
+    if (i >= n || j >= n) {
+        v = i == j ? 1.0 : 0.0;
+    } else if (i == j) {
+        v = amp * 1.0 + noise + kFitJitter;
+    } else {
+        double r2 = 0.0;
+#pragma unroll
+        for (int c = 0; c < DP; ++c)
+            if (c < d) {
+                const double tt = xsl[0][r][c] - xsl[1][cc][c];
+                r2 += tt * tt;
+            }
+        const double k = sqrt(r2) * kSqrt5;
+        v = amp * ((1.0 + k + k * k / 3.0) * exp(-k));
+    }
+    p.A[(long long)i * np + j] = v;
+    if (j < kSwNb && j <= i) {
+        p.C0[(long long)i * kSwNb + j] = v;
+        if (i < kSwNb) p.C0[(long long)j * kSwNb + i] = v;
+    }
+}
+
 // 1 / x for the pivot sweep's serial chain: v_rcp_f64 and two Newton steps (a few
 // fp64 FMAs instead of the IEEE division's scale / fixup sequence; within an ulp).
 // LML launch 3-4% shorter at n = 128-512 (profiles/r05/fit_pivot_rcp_ab_ag.log)
@@ -1438,7 +1523,15 @@ int launch_split_group(const LmlTheta* th, int count, int d, int stop, hipStream
         const int nwg = std::max(1, (nt_low + nw * tpw - 1) / (nw * tpw));
         const size_t xs_lds = (size_t)np * DP * sizeof(double);
         const bool fuse_build = xs_lds <= 64 * 1024;   // np * DP <= 8192: sw_xs_build_kernel's 8 X values per thread
-        if (fuse_build) {
+        // MPO_FIT_BUILD=rows: the row-band build (one 16-row band per workgroup), for A/B
+        static const bool tile_build = [] {
+            const char* e = getenv("MPO_FIT_BUILD");
+            return !(e && std::string(e) == "rows");
+        }();
+        if (fuse_build && tile_build) {
+            hipLaunchKernelGGL(sw_xs_build_tile_kernel<DP>, dim3(nt_low, B), dim3(256), 0, s, g);
+            MPO_LAUNCH_CHECK();
+        } else if (fuse_build) {
             auto kb = sw_xs_build_kernel<DP>;
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kb), hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)xs_lds);
