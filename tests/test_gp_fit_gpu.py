@@ -233,3 +233,24 @@ def test_repeated_host_staged_calls_are_bit_identical(name):
     T2[1, 0] = np.nan
     l2, g2, i2 = dev.evaluate(T2)
     assert i2[0] == 0 and i2[1] >= 1 and l2[1] == -np.inf and np.all(g2[1] == 0.0) and l2[0] == l0[0]
+
+
+def test_lookahead_sweep_and_tile_build_keep_the_bits(tmp_path):
+    """r06: the look-ahead pivot sweep (MPO_FIT_LOOKAHEAD) and the K build as 16x16
+    tiles (MPO_FIT_BUILD) change the schedule, never an operation: the LML, gradient
+    and status of 5 problems x 6 thetas plus 40-theta groups (n = 57 ... 500, the
+    tiles-per-wave path included) are bit-identical to the r05 schedule.  The switches
+    are read once per process, so each variant runs in its own (sequential) process."""
+    import subprocess
+    import sys
+
+    probe = os.path.join(ROOT, "scripts", "lml_bits_probe.py")
+    ref = str(tmp_path / "r05_schedule.npz")
+    env0 = dict(os.environ, MPO_FIT_LOOKAHEAD="0", MPO_FIT_BUILD="rows")
+    subprocess.run([sys.executable, probe, ref], env=env0, check=True, timeout=240)
+    for name, extra in (("lookahead", {"MPO_FIT_BUILD": "rows"}), ("tiles", {"MPO_FIT_LOOKAHEAD": "0"}), ("both", {})):
+        env = {k: v for k, v in os.environ.items() if k not in ("MPO_FIT_LOOKAHEAD", "MPO_FIT_BUILD")}
+        env.update(extra)
+        out = subprocess.run([sys.executable, probe, str(tmp_path / f"{name}.npz"), ref], env=env, check=True,
+                             timeout=240, capture_output=True, text=True).stdout
+        assert "bit-identical: True" in out, (name, out)
