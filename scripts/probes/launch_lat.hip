@@ -53,5 +53,39 @@ int main() {
                        std::chrono::duration<double, std::micro>(t2 - t0).count() / N, call / R, rt / R);
         }
     }
+    // 100 dependent empty kernels: stream launches vs one hipGraph replay (device-side gap per kernel)
+    for (int pass = 0; pass < 2; ++pass) {
+        const int K = 100, R = 50;
+        hipGraph_t g;
+        hipGraphExec_t ge;
+        hipStreamBeginCapture(s, hipStreamCaptureModeGlobal);
+        for (int i = 0; i < K; ++i) hipLaunchKernelGGL(ksmall, dim3(64), dim3(256), 0, s, small, out);
+        hipStreamEndCapture(s, &g);
+        hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+        hipEvent_t e0, e1;
+        hipEventCreate(&e0);
+        hipEventCreate(&e1);
+        float ms_stream = 0, ms_graph = 0;
+        for (int r = 0; r < R; ++r) {
+            hipEventRecord(e0, s);
+            for (int i = 0; i < K; ++i) hipLaunchKernelGGL(ksmall, dim3(64), dim3(256), 0, s, small, out);
+            hipEventRecord(e1, s);
+            hipEventSynchronize(e1);
+            float t;
+            hipEventElapsedTime(&t, e0, e1);
+            ms_stream += t;
+            hipEventRecord(e0, s);
+            hipGraphLaunch(ge, s);
+            hipEventRecord(e1, s);
+            hipEventSynchronize(e1);
+            hipEventElapsedTime(&t, e0, e1);
+            ms_graph += t;
+        }
+        if (pass == 1)
+            printf("100 dependent empty kernels: stream %.2f us per kernel, hipGraph replay %.2f us per kernel\n",
+                   ms_stream * 1e3 / (R * K), ms_graph * 1e3 / (R * K));
+        hipGraphExecDestroy(ge);
+        hipGraphDestroy(g);
+    }
     return 0;
 }
