@@ -825,6 +825,10 @@ __global__ __launch_bounds__(256) void sw_xs_build_tile_kernel(LmlGroup grp) {
             unsigned long long* st = reinterpret_cast<unsigned long long*>(p.acc + 8);
             st[0] = ~0ULL; st[1] = 0; st[2] = ~0ULL; st[3] = 0; st[6] = 0;
         }
+        if (grp.stop == 25) {   // diagnostics only: sw_pairs_final_kernel's timestamps
+            unsigned long long* st = reinterpret_cast<unsigned long long*>(p.acc + 20);
+            st[0] = ~0ULL; st[1] = 0; st[2] = 0; st[3] = 0; st[4] = 0;
+        }
     }
     __syncthreads();
     double amp, noise, ls[DP];
@@ -1419,6 +1423,10 @@ __global__ __launch_bounds__(256) void sw_pairs_final_kernel(LmlGroup grp) {
     (void)ls;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int gw = blockIdx.x * 4 + wave, nw = gridDim.x * 4;
+    // MPO_FIT_DEBUG=25 (diagnostics only): theta 0's entry spread, pairs done, tail start / end
+    unsigned long long* pst = reinterpret_cast<unsigned long long*>(p.acc + 20);
+    const bool stamp = grp.stop == 25 && blockIdx.y == 0 && threadIdx.x == 0;
+    if (stamp) { const unsigned long long t = wall_clock64(); atomicMin(pst + 0, t); atomicMax(pst + 1, t); }
     const bool failed = p.acc[1] != 0.0;
     double g[DP + 2];
 #pragma unroll
@@ -1443,6 +1451,7 @@ __global__ __launch_bounds__(256) void sw_pairs_final_kernel(LmlGroup grp) {
         T.partials[(long long)blockIdx.x * (DP + 2) + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
     }
     __syncthreads();
+    if (stamp) atomicMax(pst + 2, wall_clock64());
     if (threadIdx.x == 0) {
         // one device-scope release per workgroup (after the barrier it covers the
         // partial rows written by threads 0 .. DP+1): each fence writes back this
@@ -1453,6 +1462,7 @@ __global__ __launch_bounds__(256) void sw_pairs_final_kernel(LmlGroup grp) {
     __syncthreads();
     if (!last) return;
     __threadfence();
+    if (stamp) pst[3] = wall_clock64();
     const int groups = gridDim.x;
     double* out = T.grad;
     if (failed) {
@@ -1475,6 +1485,7 @@ __global__ __launch_bounds__(256) void sw_pairs_final_kernel(LmlGroup grp) {
         for (int w = 0; w < groups; ++w) sum += pl[w * (DP + 2) + src];
         out[lane] = 0.5 * sum;
     }
+    if (stamp) pst[4] = wall_clock64();
 }
 
 // One evaluation of the thetas th[0 .. count) (any problems of dimension d, DP =
