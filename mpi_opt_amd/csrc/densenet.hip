@@ -1402,7 +1402,7 @@ struct DnPlan {
     // member strides of the activation buffers (floats)
     std::vector<long long> cat_ms;
     long long z_ms_max = 0;
-    long long dz_off = 0, dz_ms = 0, dt_off = 0, dt_ms = 0, part_off = 0, part_ms = 0;
+    long long dz_off = 0, dz_ms = 0, dt_off = 0, dt_ms = 0, part_off = 0, part_ms = 0, part2_off = 0, part2_ms = 0;
     long long head_off = 0, head_ms = 0, lr_off = 0;
     long long bnp_off = 0;
     long long bnt_off = 0;      // fp64 BN totals of the latest site [n][H][2]      // fp64 BN slice partials [n][S][H][2] (shared by all sites)
@@ -1413,6 +1413,11 @@ struct DnPlan {
     // stream beside the input-gradient convs and BN backward (MPO_DN_PLAN=streams=1:
     // one stream); see enqueue_backward for what they read and write
     mpo::SideStream side;
+    // r06: a second weight-gradient stream (pooled slot 1): the layers' weight gradients
+    // alternate between the two, each pair of streams with its own slab buffer
+    // (MPO_DN_PLAN=wg2=0: one weight-gradient stream)
+    mpo::SideStream side2;
+    bool wg2 = true;
     // the transitions' 1x1 convs streamed by dn_conv1x1_kernel (MPO_DN_PLAN=c1x1=0: dn_conv_kernel)
     bool conv1x1 = true;
 };
@@ -1589,6 +1594,7 @@ int build_plan(DnPlan& p) {
     p.dz_off = ar.take(dz_max, &p.dz_ms);
     p.dt_off = ar.take(std::max(dt_max, 1LL), &p.dt_ms);
     p.part_off = ar.take(part_max, &p.part_ms);
+    if (p.wg2) p.part2_off = ar.take(part_max, &p.part2_ms);
     const Layer& hd = ls.back();
     // head scratch: g [B][C] | dl [B][K] | ce [2B] | dg [B][C]
     p.head_off = ar.take((long long)B * hd.cin * 2 + (long long)B * hd.cout + 2LL * B, &p.head_ms);
@@ -1880,6 +1886,9 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
     // buffer dt is shared by the transitions, so s waits for s2 before each pool
     // backward refills it; s waits for everything at the end (Adam reads the gradients).
     hipStream_t s2 = p.side.get(s);
+    p.side2.slot = 1;
+    hipStream_t s3 = s2 && p.wg2 ? p.side2.get(s) : nullptr;
+    int wgi = 0;   // weight gradients issued: odd ones on s3 (when it exists)
     for (int i = (int)p.layers.size() - 1; i >= 0; --i) {
         Layer& ly = p.layers[i];
         const int st = ly.stage;
@@ -1894,12 +1903,15 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
         // dOut of this layer's conv and the input it saw
         WgArgs w{};
         w.H = ly.H; w.W = ly.W; w.Cin = ly.cin; w.N = ly.cout; w.R = ly.Rw; w.spg = ly.spg; w.B = B; w.kw = ly.kw;
-        w.part = p.act + p.part_off; w.part_ms = p.part_ms;
+        const bool on3 = s3 && (wgi & 1);
+        ++wgi;
+        w.part = p.act + (on3 ? p.part2_off : p.part_off); w.part_ms = on3 ? p.part2_ms : p.part_ms;
         const float* dout;
         long long dout_ms;
         int dout_ps;
         if (ly.kind == K_TRANS) {
             if (s2) MPO_HIP(p.side.join(s, s2));     // an earlier-issued transition wgrad may still read dt
+            if (s3) MPO_HIP(p.side2.join(s, s3));
             const bool v4 = pool_vec4(ly.cout, p.sC[st + 1], p.dt_ms, p.cat_ms[st + 1], p.act + p.dt_off,
                                       p.act + p.dcat_off[st + 1]);
             hipLaunchKernelGGL(v4 ? dn_pool_bwd_kernel<4> : dn_pool_bwd_kernel<1>, dim3((B * ly.H + 1) / 2, n),
@@ -1919,14 +1931,17 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
             w.bnc = bx.coef; w.bnc_ms = bx.coef_ms;
         }
         hipStream_t sw = s;
-        if (s2) {
+        if (on3) {
+            MPO_HIP(p.side2.fork(s, s3));
+            sw = s3;
+        } else if (s2) {
             MPO_HIP(p.side.fork(s, s2));
             sw = s2;
         }
         DN_TRY(launch_wgrad(w, ly.ks, n, ly.G, sw));
         const long long cnt = (long long)ly.ks * ly.ks * ly.cin * ly.cout;
-        hipLaunchKernelGGL(dn_wgrad_reduce_kernel, flat_grid(cnt, n), dim3(256), 0, sw, (const float*)(p.act + p.part_off),
-                           p.part_ms, ly.G, cnt, p.grads, p.n_params, ly.w_off);
+        hipLaunchKernelGGL(dn_wgrad_reduce_kernel, flat_grid(cnt, n), dim3(256), 0, sw, (const float*)w.part,
+                           w.part_ms, ly.G, cnt, p.grads, p.n_params, ly.w_off);
         if (ly.kind == K_CONV0) continue;
         // input gradient: 'same' conv of dOut with the rotated, transposed kernel -> dz
         BnArgs bn = bn_args(p, ly, true);
@@ -1944,6 +1959,7 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
         enqueue_bn_bwd(p, bn, i, s);
     }
     if (s2) MPO_HIP(p.side.join(s, s2));
+    if (s3) MPO_HIP(p.side2.join(s, s3));
     MPO_LAUNCH_CHECK();
     return MPO_OK;
 }
@@ -1970,6 +1986,7 @@ int mpo_dn_create(const MpoDnArch* arch, int n_members, int batch, void** handle
     if (const char* e = getenv("MPO_DN_PLAN")) {
         p->side.enabled = strstr(e, "streams=1") == nullptr;
         p->conv1x1 = strstr(e, "c1x1=0") == nullptr;
+        p->wg2 = strstr(e, "wg2=0") == nullptr;
     }
     const int rc = build_plan(*p);
     if (rc != MPO_OK) {
