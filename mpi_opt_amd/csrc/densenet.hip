@@ -1403,6 +1403,7 @@ struct DnPlan {
     std::vector<long long> cat_ms;
     long long z_ms_max = 0;
     long long dz_off = 0, dz_ms = 0, dt_off = 0, dt_ms = 0, part_off = 0, part_ms = 0, part2_off = 0, part2_ms = 0;
+    long long part3_off = 0, part3_ms = 0;
     long long head_off = 0, head_ms = 0, lr_off = 0;
     long long bnp_off = 0;
     long long bnt_off = 0;      // fp64 BN totals of the latest site [n][H][2]      // fp64 BN slice partials [n][S][H][2] (shared by all sites)
@@ -1416,8 +1417,9 @@ struct DnPlan {
     // r06: a second weight-gradient stream (pooled slot 1): the layers' weight gradients
     // alternate between the two, each pair of streams with its own slab buffer
     // (MPO_DN_PLAN=wg2=0: one weight-gradient stream)
-    mpo::SideStream side2;
+    mpo::SideStream side2, side3;
     bool wg2 = true;
+    int wgs = 2;   // weight-gradient streams (MPO_DN_PLAN=wgs=3: a third, pooled slot 2)
     // the transitions' 1x1 convs streamed by dn_conv1x1_kernel (MPO_DN_PLAN=c1x1=0: dn_conv_kernel)
     bool conv1x1 = true;
 };
@@ -1595,6 +1597,7 @@ int build_plan(DnPlan& p) {
     p.dt_off = ar.take(std::max(dt_max, 1LL), &p.dt_ms);
     p.part_off = ar.take(part_max, &p.part_ms);
     if (p.wg2) p.part2_off = ar.take(part_max, &p.part2_ms);
+    if (p.wg2 && p.wgs >= 3) p.part3_off = ar.take(part_max, &p.part3_ms);
     const Layer& hd = ls.back();
     // head scratch: g [B][C] | dl [B][K] | ce [2B] | dg [B][C]
     p.head_off = ar.take((long long)B * hd.cin * 2 + (long long)B * hd.cout + 2LL * B, &p.head_ms);
@@ -1888,7 +1891,9 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
     hipStream_t s2 = p.side.get(s);
     p.side2.slot = 1;
     hipStream_t s3 = s2 && p.wg2 ? p.side2.get(s) : nullptr;
-    int wgi = 0;   // weight gradients issued: odd ones on s3 (when it exists)
+    p.side3.slot = 2;
+    hipStream_t s4 = s3 && p.wgs >= 3 ? p.side3.get(s) : nullptr;
+    int wgi = 0;   // weight gradients issued, dealt round-robin over s2, s3 (, s4)
     for (int i = (int)p.layers.size() - 1; i >= 0; --i) {
         Layer& ly = p.layers[i];
         const int st = ly.stage;
@@ -1903,15 +1908,18 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
         // dOut of this layer's conv and the input it saw
         WgArgs w{};
         w.H = ly.H; w.W = ly.W; w.Cin = ly.cin; w.N = ly.cout; w.R = ly.Rw; w.spg = ly.spg; w.B = B; w.kw = ly.kw;
-        const bool on3 = s3 && (wgi & 1);
+        const int nws = s4 ? 3 : (s3 ? 2 : 1), ws_i = wgi % nws;
         ++wgi;
-        w.part = p.act + (on3 ? p.part2_off : p.part_off); w.part_ms = on3 ? p.part2_ms : p.part_ms;
+        const bool on3 = ws_i == 1, on4 = ws_i == 2;
+        w.part = p.act + (on4 ? p.part3_off : on3 ? p.part2_off : p.part_off);
+        w.part_ms = on4 ? p.part3_ms : on3 ? p.part2_ms : p.part_ms;
         const float* dout;
         long long dout_ms;
         int dout_ps;
         if (ly.kind == K_TRANS) {
             if (s2) MPO_HIP(p.side.join(s, s2));     // an earlier-issued transition wgrad may still read dt
             if (s3) MPO_HIP(p.side2.join(s, s3));
+            if (s4) MPO_HIP(p.side3.join(s, s4));
             const bool v4 = pool_vec4(ly.cout, p.sC[st + 1], p.dt_ms, p.cat_ms[st + 1], p.act + p.dt_off,
                                       p.act + p.dcat_off[st + 1]);
             hipLaunchKernelGGL(v4 ? dn_pool_bwd_kernel<4> : dn_pool_bwd_kernel<1>, dim3((B * ly.H + 1) / 2, n),
@@ -1931,7 +1939,10 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
             w.bnc = bx.coef; w.bnc_ms = bx.coef_ms;
         }
         hipStream_t sw = s;
-        if (on3) {
+        if (on4) {
+            MPO_HIP(p.side3.fork(s, s4));
+            sw = s4;
+        } else if (on3) {
             MPO_HIP(p.side2.fork(s, s3));
             sw = s3;
         } else if (s2) {
@@ -1960,6 +1971,7 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
     }
     if (s2) MPO_HIP(p.side.join(s, s2));
     if (s3) MPO_HIP(p.side2.join(s, s3));
+    if (s4) MPO_HIP(p.side3.join(s, s4));
     MPO_LAUNCH_CHECK();
     return MPO_OK;
 }
@@ -1987,6 +1999,7 @@ int mpo_dn_create(const MpoDnArch* arch, int n_members, int batch, void** handle
         p->side.enabled = strstr(e, "streams=1") == nullptr;
         p->conv1x1 = strstr(e, "c1x1=0") == nullptr;
         p->wg2 = strstr(e, "wg2=0") == nullptr;
+        if (strstr(e, "wgs=3")) p->wgs = 3;
     }
     const int rc = build_plan(*p);
     if (rc != MPO_OK) {
