@@ -1433,7 +1433,7 @@ int env_int(const char* name, int dflt) {
 }
 
 // Planner overrides for tuning sweeps, one variable: MPO_POP_PLAN="key=value,..."
-// (keys: wgrpb = 1 | 2, dbg = MPO_POP_DEBUG, xcd = items per XCD run (0: plain order), dg_tiles, dg_kb, conv_mt, conv_kb1, conv_kb2, wg_spg1, wg_spg2, streams = 1 | 2 | 3,
+// (keys: wgrpb = 1 | 2, wgs = 1 | 2, dbg = MPO_POP_DEBUG, xcd = items per XCD run (0: plain order), dg_tiles, dg_kb, conv_mt, conv_kb1, conv_kb2, wg_spg1, wg_spg2, streams = 1 | 2 | 3,
 // occmerge = 0 | 1 | 2, occfill = quarter waves, see bucket_segs).  Every
 // value only changes how work is cut into items or ordered over streams, never the arithmetic.
 int plan_knob(const char* key, int dflt) {
@@ -1482,6 +1482,7 @@ struct Plan {
     // runs beside the input gradient + conv1 weight gradient, so one launch's tail
     // overlaps the other's work.  No two concurrent kernels write the same buffer.
     mpo::SideStream side;
+    mpo::SideStream side3;   // r06: conv2 weight-gradient buckets alternate over side and side3 (plan knob wgs = 2, the default; 1: one stream)
     mpo::SideStream side2;   // a third stream: the input-gradient buckets alternate over s and it
 };
 
@@ -1690,6 +1691,8 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         if (i == 0) P.side.enabled = plan_knob("streams", 3) >= 2;
         if (i == 0) P.side2.enabled = plan_knob("streams", 3) >= 3;
         if (i == 0) P.side2.slot = 1;
+        if (i == 0) P.side3.enabled = P.side.enabled && plan_knob("wgs", 2) >= 2;
+        if (i == 0) P.side3.slot = 2;
         const int mcap = P.conv_mt * 64;   // 4 waves x conv_mt m-tiles of 16 pixels
         const int R1 = choose_rows(m.H1, [&](int R) { return conv_lds_bytes(R + k - 1, kImg, 1, m.H1, k * k, nt); }, kc1, kc2, mcap);
         const int R2 = choose_rows(m.H2, [&](int R) { return conv_lds_bytes(R + k - 1, m.H1, F, m.H2, k * k * F, nt); }, kc1, kc2, mcap);
@@ -1906,14 +1909,15 @@ struct WgLaunch {
 };
 
 template <int OP>
-hipError_t launch_wg(Plan& P, const StepArgs& a, size_t table_off, const Bucketed& bk, hipStream_t s) {
+hipError_t launch_wg(Plan& P, const StepArgs& a, size_t table_off, const Bucketed& bk, hipStream_t s,
+                     hipStream_t s_alt = nullptr) {
     const WgItem* base = dev_table<WgItem>(P, table_off);
     return launch_segs(P, bk, OP == WG_CONV1 ? "conv1_wgrad" : "conv2_wgrad", s, [&](const Seg& sg, hipStream_t st) {
         if constexpr (OP == WG_CONV1)
             return MPO_NT_SWITCH(launch_wg1_wave_nt, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, sg.sub, st);
         else
             return MPO_NT_SWITCH(WgLaunch<OP>::template go, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, sg.sub, st);
-    });
+    }, s_alt);
 }
 
 template <int OP>
@@ -2091,7 +2095,10 @@ int mpo_pop_train_step(void* handle, const float* x, const int32_t* labels, cons
         // conv2 weight gradient (a1, dz2 -> slabs -> dw2) beside the input gradient and
         // the conv1 weight gradient (dz2 -> dz1 -> slabs -> dw1): disjoint outputs
         MPO_HIP(P.side.fork(s, s2));                                        // dz2 ready
-        MPO_HIP(launch_wg<WG_CONV2>(P, a, P.off_wg2, P.bw2, s2));
+        hipStream_t s4 = P.side3.get(s);   // disjoint slab rows per bucket: alternating buckets may overlap
+        if (s4) MPO_HIP(P.side3.fork(s, s4));
+        MPO_HIP(launch_wg<WG_CONV2>(P, a, P.off_wg2, P.bw2, s2, s4));
+        if (s4) MPO_HIP(P.side3.join(s2, s4));                              // the slab reduction reads all of them
         hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)P.wred_blocks, nm), dim3(256), 0, s2, a, wred,
                            P.wred_per_block);
         MPO_LAUNCH_CHECK();
