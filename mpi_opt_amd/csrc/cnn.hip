@@ -1433,7 +1433,7 @@ int env_int(const char* name, int dflt) {
 }
 
 // Planner overrides for tuning sweeps, one variable: MPO_POP_PLAN="key=value,..."
-// (keys: wgrpb = 1 | 2, wgs = 1 | 2, dbg = MPO_POP_DEBUG, xcd = items per XCD run (0: plain order), dg_tiles, dg_kb, conv_mt, conv_kb1, conv_kb2, wg_spg1, wg_spg2, streams = 1 | 2 | 3,
+// (keys: wgrpb = 1 | 2, wgs = 1 | 2, dgs = 2 | 3, dbg = MPO_POP_DEBUG, xcd = items per XCD run (0: plain order), dg_tiles, dg_kb, conv_mt, conv_kb1, conv_kb2, wg_spg1, wg_spg2, streams = 1 | 2 | 3,
 // occmerge = 0 | 1 | 2, occfill = quarter waves, see bucket_segs).  Every
 // value only changes how work is cut into items or ordered over streams, never the arithmetic.
 int plan_knob(const char* key, int dflt) {
@@ -1482,6 +1482,7 @@ struct Plan {
     // runs beside the input gradient + conv1 weight gradient, so one launch's tail
     // overlaps the other's work.  No two concurrent kernels write the same buffer.
     mpo::SideStream side;
+    mpo::SideStream side4;   // r06: a third stream for the input-gradient buckets (plan knob dgs = 3, the default; 2: two)
     mpo::SideStream side3;   // r06: conv2 weight-gradient buckets alternate over side and side3 (plan knob wgs = 2, the default; 1: one stream)
     mpo::SideStream side2;   // a third stream: the input-gradient buckets alternate over s and it
 };
@@ -1693,6 +1694,8 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         if (i == 0) P.side2.slot = 1;
         if (i == 0) P.side3.enabled = P.side.enabled && plan_knob("wgs", 2) >= 2;
         if (i == 0) P.side3.slot = 2;
+        if (i == 0) P.side4.enabled = P.side2.enabled && plan_knob("dgs", 3) >= 3;
+        if (i == 0) P.side4.slot = 3;
         const int mcap = P.conv_mt * 64;   // 4 waves x conv_mt m-tiles of 16 pixels
         const int R1 = choose_rows(m.H1, [&](int R) { return conv_lds_bytes(R + k - 1, kImg, 1, m.H1, k * k, nt); }, kc1, kc2, mcap);
         const int R2 = choose_rows(m.H2, [&](int R) { return conv_lds_bytes(R + k - 1, m.H1, F, m.H2, k * k * F, nt); }, kc1, kc2, mcap);
@@ -1860,10 +1863,13 @@ hipError_t launch_wg1_wave_nt(const StepArgs& a, const WgItem* items, int count,
 // s2 (optional): segments alternate between s and s2 (independent launches)
 template <class Fn>
 hipError_t launch_segs(Plan& P, const Bucketed& bk, const char* name, hipStream_t s, Fn launch_nt,
-                       hipStream_t s2 = nullptr) {
+                       hipStream_t s2 = nullptr, hipStream_t s3 = nullptr) {
+    // segments dealt round-robin over s, s2 (, s3)
+    const hipStream_t st[3] = {s, s2, s3};
+    const int ns = s2 ? (s3 ? 3 : 2) : 1;
     int i = 0;
     for (const Seg& sg : bk.segs) {
-        if (hipError_t e = launch_nt(sg, (s2 && (i++ & 1)) ? s2 : s)) return e;
+        if (hipError_t e = launch_nt(sg, st[i++ % ns])) return e;
         P.timer.mark(std::string(name) + "/nt" + std::to_string(sg.nt) + (sg.sub ? "/mt" + std::to_string(sg.sub) : "") +
                          (P.timer_detail ? "/occ" + std::to_string(lds_class(sg.lds)) + "/n" + std::to_string(sg.end - sg.begin) : ""),
                      s);
@@ -1893,11 +1899,11 @@ hipError_t launch_conv(Plan& P, const StepArgs& a, size_t table_off, const Bucke
     }, s2);
 }
 
-hipError_t launch_dgrad(Plan& P, const StepArgs& a, hipStream_t s, hipStream_t s2 = nullptr) {
+hipError_t launch_dgrad(Plan& P, const StepArgs& a, hipStream_t s, hipStream_t s2 = nullptr, hipStream_t s3 = nullptr) {
     const ConvItem* base = dev_table<ConvItem>(P, P.off_dgrad);
     return launch_segs(P, P.bdg, "conv2_dgrad", s, [&](const Seg& sg, hipStream_t st) {
         return MPO_NT_SWITCH(launch_dgrad_nt, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, st);
-    }, s2);
+    }, s2, s3);
 }
 
 template <int OP>
@@ -2104,8 +2110,11 @@ int mpo_pop_train_step(void* handle, const float* x, const int32_t* labels, cons
         MPO_LAUNCH_CHECK();
         if (hipStream_t s3 = P.side2.get(s)) {   // input-gradient buckets over s and s3 (disjoint rows of dz1)
             MPO_HIP(P.side2.fork(s, s3));
-            MPO_HIP(launch_dgrad(P, a, s, s3));
+            hipStream_t s5 = P.side4.get(s);
+            if (s5) MPO_HIP(P.side4.fork(s, s5));
+            MPO_HIP(launch_dgrad(P, a, s, s3, s5));
             MPO_HIP(P.side2.join(s, s3));
+            if (s5) MPO_HIP(P.side4.join(s, s5));
         } else {
             MPO_HIP(launch_dgrad(P, a, s));
         }
