@@ -76,6 +76,13 @@ struct ConvArgs {
     int H, W, Cin, N, R;
     int pool;      // 1: out is AvgPool2D((2,2)) of the conv output, [B][H/2][W/2] (R, y0 even)
     int c1x1;      // 1x1 convs: dn_conv1x1_kernel where it applies (DnPlan::conv1x1)
+    // r06: the BN backward reduce of the input gradient's consumer, in the epilogue (rpart
+    // != nullptr): x = cat at the BN site (rx), its coef [4][H] (rcoef); per (sample,
+    // 16-pixel row segment, row) the (sum dy, sum dy xhat) pair into rpart as dn_bn_bwd
+    // slice partials (slice = b * SL + segment, SL = max(1, W / 16), rS slices)
+    const float* rx; long long rx_ms; int rx_ps;
+    const float* rcoef; long long rcoef_ms;
+    double* rpart; int rS;
 };
 
 struct WgArgs {
@@ -428,6 +435,57 @@ __global__ __launch_bounds__(256) void dn_conv_kernel(ConvArgs a) {
             for (int r = 0; r < 4; ++r) {
                 const int mm = mt * 16 + krow * 4 + r;
                 if (mm < Mc) dst[(long long)mm * a.out_ps + n] = acc[i][j][r];
+            }
+        }
+    }
+    if (a.rpart) {
+        // the consumer's dn_bn_bwd_reduce on the values just produced (dz = this output):
+        // dy = dz ELU'(x scale + shift), sums of dy and dy xhat per image row -- a lane's
+        // four pixels share a row (W % 4 == 0); a 16-pixel tile is one row segment for
+        // W >= 16, 16 / W whole rows below; one (b, segment, row) slot per tile and row
+        const float* xr = a.rx + m * a.rx_ms + ((long long)b * H + y0) * W * a.rx_ps;
+        const float* cf = a.rcoef + m * a.rcoef_ms;
+        const int SL = W >= 16 ? W / 16 : 1;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            if (i >= mine) break;
+            const int mt = wave + 4 * i;
+            const int mm0 = mt * 16 + krow * 4;
+            double sdy = 0.0, sdyx = 0.0;
+            if (mm0 < Mc) {
+                const int h = y0 + mm0 / W;
+                const float mean = cf[h], inv = cf[H + h], bs_ = cf[2 * H + h], bt_ = cf[3 * H + h];
+#pragma unroll
+                for (int j = 0; j < NT; ++j) {
+                    const int n = j * 16 + kcol;
+                    if (n >= a.N) continue;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float xv = xr[(long long)(mm0 + r) * a.rx_ps + n];
+                        const float y = xv * bs_ + bt_;
+                        const float dy = acc[i][j][r] * (y > 0.f ? 1.f : __expf(y));
+                        const float xh = (xv - mean) * inv;
+                        sdy += dy;
+                        sdyx += (double)dy * xh;
+                    }
+                }
+            }
+            const int tr = W >= 16 ? 1 : 16 / W;
+            for (int q = 0; q < tr; ++q) {
+                const bool row_q = W >= 16 || (krow * 4) / W == q;
+                double v0 = row_q ? sdy : 0.0, v1 = row_q ? sdyx : 0.0;
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) {
+                    v0 += __shfl_xor(v0, off);
+                    v1 += __shfl_xor(v1, off);
+                }
+                const int pix = mt * 16 + q * W;   // the row's first pixel in this tile
+                if (lane == 0 && pix < Mc) {
+                    const int slot = W >= 16 ? (pix % W) / 16 : 0;
+                    double* o = a.rpart + (((long long)m * a.rS + ((long long)b * SL + slot)) * H + (y0 + pix / W)) * 2;
+                    o[0] = v0;
+                    o[1] = v1;
+                }
             }
         }
     }
@@ -1143,6 +1201,33 @@ __global__ __launch_bounds__(64) void dn_bn_bwd_fold_kernel(BnArgs a, double* __
     }
 }
 
+// grid (H, member), one wave per image row: the fold for the epilogue-fused reduce's
+// many slices (sample x row segment): lane l sums slices l, l + 64, ... in order, then a
+// fixed butterfly; slot 0 and the gradients as dn_bn_bwd_fold
+__global__ __launch_bounds__(64) void dn_bn_bwd_fold_wide_kernel(BnArgs a, double* __restrict__ part, int S) {
+    const int h = blockIdx.x, m = blockIdx.y, H = a.H, lane = threadIdx.x;
+    double sdy = 0.0, sdyx = 0.0;
+    for (int sl = lane; sl < S; sl += 64) {
+        const double* o = part + (((long long)m * S + sl) * H + h) * 2;
+        sdy += o[0];
+        sdyx += o[1];
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        sdy += __shfl_xor(sdy, off);
+        sdyx += __shfl_xor(sdyx, off);
+    }
+    __syncthreads();   // every lane has read its slices before lane 0 overwrites slot 0 (slice 0)
+    if (lane == 0) {
+        double* o = part + ((long long)m * S * H + h) * 2;
+        o[0] = sdy;
+        o[1] = sdyx;
+        float* gm = a.grads + m * a.p_ms;
+        gm[a.g_off + h] = (float)sdyx;
+        gm[a.b_off + h] = (float)sdy;
+    }
+}
+
 template <int V>
 __global__ __launch_bounds__(256) void dn_bn_bwd_apply_kernel(BnArgs a, const double* __restrict__ part, int S) {
     const int tid = threadIdx.x & 127, m = blockIdx.y;
@@ -1408,6 +1493,8 @@ struct DnPlan {
     long long bnp_off = 0;
     long long bnt_off = 0;      // fp64 BN totals of the latest site [n][H][2]      // fp64 BN slice partials [n][S][H][2] (shared by all sites)
     std::vector<int> bn_S, bn_bs;   // per layer: batch slices and samples per slice
+    std::vector<int> bn_fS;         // per dense layer: the slices of its epilogue-fused BN backward reduce (0: none)
+    bool bnfuse = true;             // MPO_DN_PLAN=bnfuse=0: dn_bn_bwd_reduce as its own pass
     float *params = nullptr, *grads = nullptr, *m = nullptr, *v = nullptr, *state = nullptr, *act = nullptr;
     bool bound = false;
     // the weight gradients (+ their slab reduction) of the backward run on a second
@@ -1586,6 +1673,15 @@ int build_plan(DnPlan& p) {
         p.bn_bs[i] = bs;
         p.bn_S[i] = (B + bs - 1) / bs;
         bnp_max = std::max(bnp_max, (long long)p.bn_S[i] * ly.H * 2);
+    }
+    // the dense layers' BN backward reduce in their input-gradient conv's epilogue: one
+    // partial per (sample, 16-pixel row segment) slice
+    p.bn_fS.assign(ls.size(), 0);
+    for (size_t i = 0; i < ls.size(); ++i) {
+        const Layer& ly = ls[i];
+        if (!p.bnfuse || ly.kind != K_DENSE || ly.ks != 3 || ly.W % 4 != 0 || (ly.W < 16 && 16 % ly.W != 0)) continue;
+        p.bn_fS[i] = B * std::max(1, ly.W / 16);
+        bnp_max = std::max(bnp_max, (long long)p.bn_fS[i] * ly.H * 2);
     }
     long long bnp_ms;
     p.bnp_off = ar.take(bnp_max * 2, &bnp_ms);   // doubles = 2 floats (arena offsets are 64-float aligned)
@@ -1868,13 +1964,15 @@ int enqueue_forward(DnPlan& p, const float* x, const int* labels, const int* ord
     return MPO_OK;
 }
 
-void enqueue_bn_bwd(DnPlan& p, const BnArgs& bn, int li, hipStream_t s) {
+void enqueue_bn_bwd(DnPlan& p, const BnArgs& bn, int li, hipStream_t s, int fused_S = 0) {
     double* bnp = reinterpret_cast<double*>(p.act + p.bnp_off);
-    const int S = p.bn_S[li];
+    const int S = fused_S > 0 ? fused_S : p.bn_S[li];
     const bool v4 = bn_vec4(bn);
-    hipLaunchKernelGGL(v4 ? dn_bn_bwd_reduce_kernel<4> : dn_bn_bwd_reduce_kernel<1>, dim3(bn.H, S, p.n), dim3(256),
-                       0, s, bn, bnp, S, p.bn_bs[li]);
-    hipLaunchKernelGGL(dn_bn_bwd_fold_kernel, dim3(p.n), dim3(64), 0, s, bn, bnp, S);
+    if (fused_S <= 0)   // else the input-gradient conv's epilogue wrote the slice partials
+        hipLaunchKernelGGL(v4 ? dn_bn_bwd_reduce_kernel<4> : dn_bn_bwd_reduce_kernel<1>, dim3(bn.H, S, p.n),
+                           dim3(256), 0, s, bn, bnp, S, p.bn_bs[li]);
+    if (fused_S > 0) hipLaunchKernelGGL(dn_bn_bwd_fold_wide_kernel, dim3(bn.H, p.n), dim3(64), 0, s, bn, bnp, S);
+    else hipLaunchKernelGGL(dn_bn_bwd_fold_kernel, dim3(p.n), dim3(64), 0, s, bn, bnp, S);
     hipLaunchKernelGGL(v4 ? dn_bn_bwd_apply_kernel<4> : dn_bn_bwd_apply_kernel<1>, dim3((p.B * bn.H + 1) / 2, p.n),
                        dim3(256), 0, s, bn, (const double*)bnp, S);
 }
@@ -1962,12 +2060,18 @@ int enqueue_backward(DnPlan& p, const float* x, const int* order, long long ord_
         c.out = p.act + p.dz_off; c.out_ms = p.dz_ms; c.out_ps = ly.cin;
         c.H = ly.H; c.W = ly.W; c.Cin = ly.cout; c.N = ly.cin; c.R = ly.R;
         c.c1x1 = p.conv1x1 ? 1 : 0;
+        const int fS = p.bn_fS[i];
+        if (fS > 0) {
+            c.rx = bn.x; c.rx_ms = bn.x_ms; c.rx_ps = bn.x_ps;
+            c.rcoef = bn.coef; c.rcoef_ms = bn.coef_ms;
+            c.rpart = reinterpret_cast<double*>(p.act + p.bnp_off); c.rS = fS;
+        }
         if (ly.ks == 3) DN_TRY(launch_conv<3>(c, n, B, s));
         else DN_TRY(launch_conv<1>(c, n, B, s));
         bn.dz = p.act + p.dz_off; bn.dz_ms = p.dz_ms;
         bn.dx = p.act + p.dcat_off[st]; bn.dx_ms = p.cat_ms[st]; bn.dx_ps = p.sC[st];
         bn.accumulate = ly.kind == K_DENSE ? 1 : 0;
-        enqueue_bn_bwd(p, bn, i, s);
+        enqueue_bn_bwd(p, bn, i, s, fS);
     }
     if (s2) MPO_HIP(p.side.join(s, s2));
     if (s3) MPO_HIP(p.side2.join(s, s3));
@@ -1999,6 +2103,7 @@ int mpo_dn_create(const MpoDnArch* arch, int n_members, int batch, void** handle
         p->side.enabled = strstr(e, "streams=1") == nullptr;
         p->conv1x1 = strstr(e, "c1x1=0") == nullptr;
         p->wg2 = strstr(e, "wg2=0") == nullptr;
+        p->bnfuse = strstr(e, "bnfuse=0") == nullptr;
         if (strstr(e, "wgs=3")) p->wgs = 3;
     }
     const int rc = build_plan(*p);
