@@ -270,9 +270,21 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
     int Hin, Cin, Ho;
     const float* in;
     const float* W;
-    const float* bias;
+    const float* bias = nullptr;
     float* out;
-    if (OP == CONV1_FWD) {
+    const float* relu_mask = nullptr;
+    if (OP == CONV2_DGRAD) {
+        // r06: the conv2 input gradient as a forward conv over dz2 zero-bordered by k - 1
+        // (Hin = H2 + 2 (k - 1) = H1 + k - 1), the rotated weights w2t, Cin = F rounded to
+        // 4 (w2t's channel stride; channels >= F are zero in the image and in w2t).  Every
+        // MFMA step multiplies the same 4 (tap, channel) pairs as conv_dgrad_kernel's;
+        // the halo steps it does not skip only add exact zeros: the same bits.
+        Hin = mb.H1 + k - 1; Cin = (F + 3) & ~3; Ho = mb.H1;
+        in = a.act + mb.dz2 + (long long)it.b * mb.H2 * mb.H2 * F;
+        W = a.act + mb.w2t;
+        out = a.act + mb.dz1 + (long long)it.b * Ho * Ho * F;
+        relu_mask = a.act + mb.a1 + (long long)it.b * Ho * Ho * F;
+    } else if (OP == CONV1_FWD) {
         Hin = kImg; Cin = 1; Ho = mb.H1;
         const int sidx = a.order[(long long)it.member * a.order_stride + a.row0 + it.b];
         in = a.x + (long long)sidx * (kImg * kImg);
@@ -301,7 +313,17 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
     const int krow = lane >> 4, kcol = lane & 15;
 
     // ---- stage the input rows + the tap-offset table (the only barrier)
-    if (a.debug != 2) {
+    if (OP == CONV2_DGRAD) {
+        // zero image (halo rows / columns, channels >= F), then dz2's rows inside it:
+        // padded row y0 + r is dz2 row y0 + r - (k - 1)
+        const int pad = k - 1, H2 = mb.H2;
+        for (int e = tid; e < img_elems; e += 256) img[e] = 0.f;
+        __syncthreads();
+        const int gy_lo = max(0, it.y0 - pad), gy_hi = min(H2, it.y0 + it.R);
+        if (a.debug != 2 && gy_hi > gy_lo)
+            stage_rows(in + (long long)gy_lo * H2 * F, img + (gy_lo + pad - it.y0) * RS + pad * Fp, gy_hi - gy_lo, H2,
+                       F, Fp, RS, tid);
+    } else if (a.debug != 2) {
         const float* src = in + (long long)it.y0 * Hin * Cin;
         if (Cin == 1) {
             for (int e = tid; e < rows * Hin; e += 256) {
@@ -368,13 +390,14 @@ __global__ __launch_bounds__(256) void conv_img_kernel(StepArgs a, const ConvIte
         for (int j = 0; j < NT; ++j) {
             const int n = j * 16 + kcol;
             if (n >= N) continue;
-            const float bv = bias[n];
+            const float bv = OP == CONV2_DGRAD ? 0.f : bias[n];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int m = mt * 16 + krow * 4 + r;
                 if (m >= M) continue;
                 const long long o = (pix0 + m) * N + n;
-                out[o] = fmaxf(acc[i][j][r] + bv, 0.f);
+                if (OP == CONV2_DGRAD) out[o] = relu_mask[o] > 0.f ? acc[i][j][r] : 0.f;
+                else out[o] = fmaxf(acc[i][j][r] + bv, 0.f);
             }
         }
     }
@@ -1457,8 +1480,8 @@ struct Plan {
     int debug = 0;
     std::vector<Member> mem;
     long long n_params = 0, act_floats = 0;
-    std::vector<ConvItem> conv1, conv2, dgrad;
-    Bucketed bc1, bc2, bdg;
+    std::vector<ConvItem> conv1, conv2, dgrad, dgf;
+    Bucketed bc1, bc2, bdg, bdf;
     std::vector<WgItem> wg1, wg2;
     Bucketed bw1, bw2;
     std::vector<GemmItem> d1f, d2f, d2w, d2d, d1w, d1d;
@@ -1469,13 +1492,15 @@ struct Plan {
     char* table_base = nullptr;
     size_t table_bytes = 0;
     std::vector<char> host_tables;
-    size_t off_mem, off_conv1, off_conv2, off_dgrad, off_wg1, off_wg2, off_d1f, off_d2f, off_d2w, off_d2d,
+    size_t off_mem, off_conv1, off_conv2, off_dgrad, off_dgf, off_wg1, off_wg2, off_d1f, off_d2f, off_d2w, off_d2d,
         off_d1w, off_d1d, off_pm, off_ps, off_cs, off_wr, off_adam;
     float *params = nullptr, *grads = nullptr, *m = nullptr, *v = nullptr, *act = nullptr;
     bool bound = false;
     size_t lds_conv_max = 0, lds_wg_max = 0;
     int conv_mt = 4;        // forward conv m-tiles per wave at most: items of up to 256 pixels (MPO_POP_PLAN conv_mt=2: 128)
     int dg_tiles = 12;      // 4x4 tiles per conv2 input-gradient work item at most (MPO_POP_PLAN dg_tiles)
+    int dgfset = 0;         // ... and members whose bit k is set (MPO_POP_PLAN dgfset, a mask over k)
+    int dgfwd = 4;          // r06: members with k <= dgfwd take the zero-bordered forward conv for their input gradient (MPO_POP_PLAN dgfwd)
     int wgrpb = 2;          // conv2 weight gradient output rows per barrier (MPO_POP_PLAN wgrpb = 1 | 2)
     // Second stream for independent launches (MPO_POP_PLAN streams=1 keeps one): the
     // forward conv2 buckets alternate between the two, and the conv2 weight gradient
@@ -1668,7 +1693,7 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         m.dp = aalloc((long long)B * m.K1);
         m.dz2 = aalloc((long long)B * m.H2 * m.H2 * F);
         m.dz1 = aalloc((long long)B * m.H1 * m.H1 * F);
-        m.w2t = aalloc((long long)(k * k * ((F + 3) & ~3) + 16) * (m.nt * 16));
+        m.w2t = aalloc((long long)(((k * k * ((F + 3) & ~3) + 15) & ~15) + kWSlack) * (m.nt * 16));
         m.w1p = aalloc((long long)(((k * k + 15) & ~15) + kWSlack) * (m.nt * 16));
         m.w2p = aalloc((long long)(((k * k * F + 15) & ~15) + kWSlack) * (m.nt * 16));
         m.wp1 = aalloc((long long)m.g1 * (k * k + 1) * F);
@@ -1684,7 +1709,7 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
     // (profiles/r03/train_sweep_mt4_budget_am.log; 128-pixel items at 52/78 KiB were r01-r02's plan)
     const int kc1 = plan_knob("conv_kb1", 40), kc2 = plan_knob("conv_kb2", 100);
     const int kdg = plan_knob("dg_kb", 78);
-    std::vector<size_t> L1(n), L2(n), LD(n), LW1(n), LW2(n);   // per-member LDS bytes per op
+    std::vector<size_t> L1(n), L2(n), LD(n), LDF(n), LW1(n), LW2(n);   // per-member LDS bytes per op
     for (int i = 0; i < n; ++i) {
         const Member& m = P.mem[i];
         const int k = m.k, F = m.F, nt = m.nt;
@@ -1709,12 +1734,26 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         while (Rd > 4 && dgrad_lds_bytes(Rd, k, F, m.H2) > dgb) Rd -= 4;
         const size_t l1 = conv_lds_bytes(R1 + k - 1, kImg, 1, m.H1, k * k, nt);
         const size_t l2 = conv_lds_bytes(R2 + k - 1, m.H1, F, m.H2, k * k * F, nt);
-        const size_t ld = dgrad_lds_bytes(Rd, k, F, m.H2);
-        L1[i] = l1; L2[i] = l2; LD[i] = ld;
+        size_t ld = dgrad_lds_bytes(Rd, k, F, m.H2);
+        // the zero-bordered forward formulation (k small: (H1 / H2)^2 of padded work)
+        // r06, MI355X, 320 members (profiles/r06/mnist/ao_*, ap_*): k <= 4 -> 36.70 ms per train step
+        // 35.85 (k = 4 carries it; k = 2-3 neutral), with an 80 KiB first LDS budget 35.67; adding k =
+        // 5..10 one at a time: 5-7 within noise, 8 +0.2, 9 +0.6, 10 +2.2 ms.  Bits unchanged.
+        if (i == 0) P.dgfwd = plan_knob("dgfwd", 4);
+        if (i == 0) P.dgfset = plan_knob("dgfset", 0);
+        const bool fwd_dg = k <= P.dgfwd || ((P.dgfset >> k) & 1);
+        const int F4 = (F + 3) & ~3, Hp = m.H1 + k - 1;
+        const int Rf = choose_rows(m.H1, [&](int R) { return conv_lds_bytes(R + k - 1, Hp, F4, m.H1, k * k * F4, nt); },
+                                   plan_knob("dgf_kb1", 80), plan_knob("dgf_kb2", kc2), mcap);
+        if (fwd_dg) ld = conv_lds_bytes(Rf + k - 1, Hp, F4, m.H1, k * k * F4, nt);
+        L1[i] = l1; L2[i] = l2; LD[i] = ld; LDF[i] = ld;
         for (int b = 0; b < B; ++b) {
             for (int y = 0; y < m.H1; y += R1) P.conv1.push_back({i, b, y, std::min(R1, m.H1 - y)});
             for (int y = 0; y < m.H2; y += R2) P.conv2.push_back({i, b, y, std::min(R2, m.H2 - y)});
-            for (int y = 0; y < m.H1; y += Rd) P.dgrad.push_back({i, b, y, std::min(Rd, m.H1 - y)});
+            if (fwd_dg)
+                for (int y = 0; y < m.H1; y += Rf) P.dgf.push_back({i, b, y, std::min(Rf, m.H1 - y)});
+            else
+                for (int y = 0; y < m.H1; y += Rd) P.dgrad.push_back({i, b, y, std::min(Rd, m.H1 - y)});
             P.per_sample.push_back({i, b});
         }
         P.lds_conv_max = std::max({P.lds_conv_max, l1, l2, ld});
@@ -1771,12 +1810,14 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
     bucket_segs(P.conv1, P.bc1, P.mem, L1, occ);
     bucket_segs(P.conv2, P.bc2, P.mem, L2, occ);
     bucket_segs(P.dgrad, P.bdg, P.mem, LD, occ);
+    bucket_segs(P.dgf, P.bdf, P.mem, LDF, occ);
     bucket_segs(P.wg1, P.bw1, P.mem, LW1, occ);
     bucket_segs(P.wg2, P.bw2, P.mem, LW2, occ);
     const int xc = plan_knob("xcd", 4);
     xcd_deal(P.conv1, P.bc1, xc);
     xcd_deal(P.conv2, P.bc2, xc);
     xcd_deal(P.dgrad, P.bdg, xc);
+    xcd_deal(P.dgf, P.bdf, xc);
     xcd_deal(P.wg1, P.bw1, xc);
     xcd_deal(P.wg2, P.bw2, xc);
 
@@ -1794,6 +1835,7 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
     P.off_conv1 = put(P.conv1.data(), P.conv1.size() * sizeof(ConvItem));
     P.off_conv2 = put(P.conv2.data(), P.conv2.size() * sizeof(ConvItem));
     P.off_dgrad = put(P.dgrad.data(), P.dgrad.size() * sizeof(ConvItem));
+    P.off_dgf = put(P.dgf.data(), P.dgf.size() * sizeof(ConvItem));
     P.off_wg1 = put(P.wg1.data(), P.wg1.size() * sizeof(WgItem));
     P.off_wg2 = put(P.wg2.data(), P.wg2.size() * sizeof(WgItem));
     P.off_d1f = put(P.d1f.data(), P.d1f.size() * sizeof(GemmItem));
@@ -1901,6 +1943,11 @@ hipError_t launch_conv(Plan& P, const StepArgs& a, size_t table_off, const Bucke
 
 hipError_t launch_dgrad(Plan& P, const StepArgs& a, hipStream_t s, hipStream_t s2 = nullptr, hipStream_t s3 = nullptr) {
     const ConvItem* base = dev_table<ConvItem>(P, P.off_dgrad);
+    const ConvItem* fbase = dev_table<ConvItem>(P, P.off_dgf);
+    if (hipError_t e = launch_segs(P, P.bdf, "conv2_dgrad_fwd", s, [&](const Seg& sg, hipStream_t st) {
+            return MPO_NT_SWITCH(ConvLaunch<CONV2_DGRAD>::template go, sg, a, fbase + sg.begin, sg.end - sg.begin, sg.lds, st);
+        }, s2, s3))
+        return e;
     return launch_segs(P, P.bdg, "conv2_dgrad", s, [&](const Seg& sg, hipStream_t st) {
         return MPO_NT_SWITCH(launch_dgrad_nt, sg, a, base + sg.begin, sg.end - sg.begin, sg.lds, st);
     }, s2, s3);
