@@ -250,6 +250,29 @@ def test_side_stream_schedule_is_bit_identical(monkeypatch):
         np.testing.assert_array_equal(out[0][1], out[k][1])
 
 
+def test_input_gradient_formulations_are_bit_identical(monkeypatch):
+    """The conv2 input gradient as the halo-skipping gather kernel (MPO_POP_PLAN
+    dgfwd=0) and as the forward conv over a zero-bordered dz2 (dgfwd=13: every k;
+    the default takes it for k <= 4): every MFMA step multiplies the same operands,
+    so losses and parameters agree bit for bit after 3 train steps, for k = 2..10
+    and F both a multiple of 16 and not."""
+    members = MEMBERS + [(32, 4, 2, 60, 1e-3, 0.25, 1), (21, 6, 2, 70, 1e-3, 0.25, 2), (48, 8, 3, 90, 1e-3, 0.25, 3),
+                         (13, 9, 2, 40, 1e-3, 0.25, 4)]
+    x, y = dataset(8)
+    xd, yd = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    tr, _ = orders(members, x)
+    otr = torch.from_numpy(tr).cuda()
+    out = []
+    for knob in ("dgfwd=0", "dgfwd=13"):
+        monkeypatch.setenv("MPO_POP_PLAN", knob)
+        eng, _, _ = make_engine(members)
+        losses = [eng.train_step(xd, yd, otr, st * BATCH).cpu().numpy().copy() for st in range(3)]
+        torch.cuda.synchronize()
+        out.append((np.stack(losses), eng.params.cpu().numpy().copy()))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+
+
 def test_engines_sharing_side_streams_are_bit_identical():
     """Population engines of one process share the pooled side streams
     (mpo::pooled_side_stream): two engines alive and stepped alternately give the
