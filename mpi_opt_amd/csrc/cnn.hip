@@ -96,6 +96,7 @@ struct StepArgs {
                              // 4 conv fwd / dgrad weight fragments re-read from groups 0-1 (cache-resident; timing only)
     int conv_mt;             // forward conv m-tiles per wave at most (2: M <= 128 pixels per item; 4: <= 256)
     int wgrpb;               // conv2 weight gradient: output rows per barrier (1 | 2)
+    int wgpair;              // wgrpb 2 and Ho = 2 (mod 4): a row pair as one K run (plan knob wgpair)
 };
 
 
@@ -651,6 +652,46 @@ __device__ __forceinline__ void wgrad_row(const float* __restrict__ img, const f
     }
 }
 
+// Two output rows as ONE K run of 2 Ho pixels (RPB = 2, Ho = 2 (mod 4)): pixel x of
+// the pair is row x >= Ho's pixel x - Ho (a per-lane select), so no k-step straddles
+// zero padding -- row-by-row, ceil(Ho / 4) steps per row multiply 2 padding pixels
+// (Ho = 10: 6 steps for 10 pixels).  The pair's run: 2 Ho / 4 steps.
+template <int MT, int NT>
+__device__ __forceinline__ void wgrad_row_pair(const float* __restrict__ img, const float* __restrict__ dl0,
+                                               const float* __restrict__ dl1, const int (&abase0)[MT],
+                                               const int (&abase1)[MT], const int (&astep)[MT], int dstride, int Ho,
+                                               int nk, int krow, int kcol, f32x4 (&acc)[MT][NT]) {
+    float a0[MT], a1[MT], b0[NT], b1[NT];
+    auto rd = [&](int s, float (&av)[MT], float (&bv)[NT]) {
+        const int x = 4 * s + krow;
+        const bool second = x >= Ho;
+        const int px = second ? x - Ho : x;
+        const float* dl = second ? dl1 : dl0;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) av[i] = img[(second ? abase1[i] : abase0[i]) + px * astep[i]];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) bv[j] = dl[px * dstride + j * 16 + kcol];
+    };
+    auto mma = [&](const float (&av)[MT], const float (&bv)[NT]) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    };
+    rd(0, a0, b0);
+    for (int s = 0; s < nk; s += 2) {
+        rd(s + 1, a1, b1);   // s + 1 <= nk: the second row's padding (zero dout) / finite LDS
+        __builtin_amdgcn_sched_barrier(0);
+        mma(a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 1 >= nk) break;
+        rd(s + 2, a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(a1, b1);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // MT = the m-tiles every wave of this launch runs (the plan buckets m-groups by
 // ceil(tiles / 8)): a single loop body keeps the kernel at <= 128 VGPRs, i.e. two
 // 8-wave workgroups per CU.  A wave with fewer real tiles multiplies the constant
@@ -768,6 +809,20 @@ __global__ __launch_bounds__(kWgThreads) void conv_wgrad_kernel(StepArgs a, cons
                         dma(dob + (y + 3) * dcnt, dcnt, dl + ((y + 3) & 3) * dS);
                     }
                 }
+                if (a.wgpair && (Ho & 3) == 2) {   // Ho even here (H2 = 30 - 2k): pairs are whole
+                    int ab0[MT], ab1[MT];
+#pragma unroll
+                    for (int i = 0; i < MT; ++i) {
+                        int sl = slot0 + tky[i];
+                        sl = sl >= RS ? sl - RS : sl;
+                        ab0[i] = astep[i] ? sl * rowS + tcol[i] : tcol[i];
+                        sl = sl + 1 == RS ? 0 : sl + 1;
+                        ab1[i] = astep[i] ? sl * rowS + tcol[i] : tcol[i];
+                    }
+                    if (a.debug != 1 && mine > 0)
+                        wgrad_row_pair<MT, NT>(ring, dl + (y & 3) * dS, dl + ((y + 1) & 3) * dS, ab0, ab1, astep, N, Ho,
+                                               Ho >> 1, krow, kcol, acc);
+                } else
 #pragma unroll
                 for (int dy = 0; dy < 2; ++dy) {
                     if (y + dy >= Ho) break;
@@ -1502,6 +1557,7 @@ struct Plan {
     int dgfset = 0;         // ... and members whose bit k is set (MPO_POP_PLAN dgfset, a mask over k)
     int dgfwd = 4;          // r06: members with k <= dgfwd take the zero-bordered forward conv for their input gradient (MPO_POP_PLAN dgfwd)
     int wgrpb = 2;          // conv2 weight gradient output rows per barrier (MPO_POP_PLAN wgrpb = 1 | 2)
+    int wgpair = 1;         // r06: with wgrpb 2, a row pair of Ho = 2 (mod 4) pixels as one K run (MPO_POP_PLAN wgpair)
     // Second stream for independent launches (MPO_POP_PLAN streams=1 keeps one): the
     // forward conv2 buckets alternate between the two, and the conv2 weight gradient
     // runs beside the input gradient + conv1 weight gradient, so one launch's tail
@@ -1759,6 +1815,9 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         P.lds_conv_max = std::max({P.lds_conv_max, l1, l2, ld});
         // wgrad items: (member, 512-row m-group, sample group)
         if (i == 0) P.wgrpb = plan_knob("wgrpb", 2) == 1 ? 1 : 2;
+        // r06, MI355X (profiles/r06/mnist/as_*.log): 37.70 -> 37.29 ms per 320-member step,
+        // 1.64 -> 1.63 ms at 20; losses bit-identical (a padding pixel's MFMA product is an exact zero)
+        if (i == 0) P.wgpair = plan_knob("wgpair", 1);
         const size_t lw2 = wg_lds_bytes(k, m.H1, F, m.H2, F, P.wgrpb);
         const size_t lw1 = wg_lds_bytes(k, kImg, 1, m.H1, F);
         LW2[i] = lw2; LW1[i] = lw1;
@@ -2001,6 +2060,7 @@ StepArgs make_args(const Plan& P, const float* x, const int* labels, const int* 
     a.debug = P.debug;
     a.conv_mt = P.conv_mt;
     a.wgrpb = P.wgrpb;
+    a.wgpair = P.wgpair;
     a.zero_off = P.zero_off;
     return a;
 }
