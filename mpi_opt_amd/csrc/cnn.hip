@@ -1763,7 +1763,9 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
     // r03: forward items of up to 256 pixels (4 m-tiles per wave) in <= 40 KiB (4 workgroups per CU) where
     // rows in [rmax/2, rmax] fit, else <= 100 KiB: conv2 fwd 9.66 -> 8.53 ms per 320-member batch
     // (profiles/r03/train_sweep_mt4_budget_am.log; 128-pixel items at 52/78 KiB were r01-r02's plan)
-    const int kc1 = plan_knob("conv_kb1", 40), kc2 = plan_knob("conv_kb2", 100);
+    // r06, after dgfwd + wgpair (profiles/r06/mnist/av_*, aw_*): a 30 KiB first budget, 37.41 / 37.28 ->
+    // 37.13 / 37.08 ms per 320-member step, 3.95 -> 3.86 ms at 40, 1.633 -> 1.642 at 20 (24 and 36 alike)
+    const int kc1 = plan_knob("conv_kb1", 30), kc2 = plan_knob("conv_kb2", 100);
     const int kdg = plan_knob("dg_kb", 78);
     std::vector<size_t> L1(n), L2(n), LD(n), LDF(n), LW1(n), LW2(n);   // per-member LDS bytes per op
     for (int i = 0; i < n; ++i) {
