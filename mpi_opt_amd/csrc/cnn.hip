@@ -1733,7 +1733,14 @@ int build_plan(Plan& P, const MpoCnnSpec* specs, int n, int B) {
         // profiles/r04/train_probe_spg_i.log), 4 per conv1 slab (its GEMM is tiny).  A
         // function of the member only, never of the population: a member's trajectory
         // must not depend on who trains beside it (isolation tests, chunked populations)
-        const int spg2 = std::max(1, plan_knob("wg_spg2", 2));
+        // r06: members whose conv2 weight gradient has >= wg_big m-groups of 512 rows (k^2 F + 1
+        // rows) take wg_spg2_big = 4 samples per slab -- they launch g2 x m-groups workgroups, so
+        // halving g2 still fills the chip and halves their slab writes / reduction: 37.10 -> 36.65
+        // ms per 320-member step, 3.85 -> 3.82 at 40, 20 unchanged (profiles/r06/mnist/bc_*.log).
+        // Still a function of the member alone (isolation); wg_spg2_big=0 restores one spg2
+        const int mg2 = (k * k * F + 1 + kWgRows - 1) / kWgRows;
+        const int big = plan_knob("wg_spg2_big", 4), bigmg = plan_knob("wg_big", 3);
+        const int spg2 = std::max(1, big > 0 && mg2 >= bigmg ? big : plan_knob("wg_spg2", 2));
         const int spg1 = std::max(1, plan_knob("wg_spg1", 4));
         m.g2 = std::max(1, std::min(B, (B + spg2 - 1) / spg2));
         m.g1 = std::max(1, std::min(B, (B + spg1 - 1) / spg1));
